@@ -1,0 +1,193 @@
+/*
+ * meshclust_amd.h -- C-ABI of libmcgpu, the MI355X (gfx950) engine for MeShClust's
+ * data-parallel hot path.  Plain pointers and sizes only; no C++ or torch types.
+ *
+ * MeShClust v1 has no plugin/FFI API: its hot path is reached through C++ template
+ * seams inside one binary.  Each entry point below replaces one of those
+ * seams; the reference interface it stands in for is cited as file:line relative to the
+ * reference tree (src/...).  The host program (bin/meshclust, meshclust_amd/csrc/host)
+ * restates the reference control flow and calls only these functions for the hot path.
+ *
+ * Conventions
+ *   - every function returns MC_OK (0) or an MC_ERR_* code; mc_last_error() gives text.
+ *     Nothing throws across the ABI.  Errors are loud: there is no CPU fallback.
+ *   - point ids are the reference's ids: input order over all files (Runner.cpp:345-349).
+ *   - one host thread per context; calls are synchronous at the ABI (HIP streams inside).
+ *   - the caller owns every host array; the library owns device memory.
+ */
+#ifndef MESHCLUST_AMD_H
+#define MESHCLUST_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MC_ABI_VERSION 1
+
+#define MC_OK 0
+#define MC_ERR_ARG 1     /* bad argument / shape                                  */
+#define MC_ERR_HIP 2     /* HIP runtime or kernel failure                         */
+#define MC_ERR_STATE 3   /* call made in the wrong order (e.g. no sequences yet)  */
+#define MC_ERR_OOM 4     /* device allocation failed                              */
+#define MC_ERR_INPUT 5   /* input the reference would reject (bad nucleotide ...) */
+
+/* Feature flags and combo kinds: identical values to src/cluster/src/Feature.h:9-22. */
+#define MC_FEAT_ALIGN (1 << 0)
+#define MC_FEAT_LD (1 << 1)
+#define MC_FEAT_MANHATTAN (1 << 2)
+#define MC_FEAT_INTERSECTION (1 << 4)
+#define MC_FEAT_PEARSON (1 << 5)
+#define MC_FEAT_KULCZYNSKI2 (1 << 10)
+#define MC_COMBO_SQUARED 1
+#define MC_COMBO_SELF 2
+
+#define MC_MAX_SINGLE 8
+#define MC_MAX_COMBO 8
+#define MC_MAX_COMBO_LEN 4
+
+/*
+ * Trained classifier = Feature<T> state after normalize()/finalize() plus the GLM weight
+ * column (Feature.h:122-130, Trainer.h:45-46).  `lookup` is the single-feature order,
+ * `combo_*` the products of Feature::operator() (Feature.h:69-88), `weights[0]` the
+ * intercept and `weights[1+c]` the weight of combo c (Trainer.cpp:84-95).
+ */
+typedef struct mc_classifier {
+  int32_t n_single;
+  uint16_t lookup[MC_MAX_SINGLE];
+  int32_t is_sim[MC_MAX_SINGLE];
+  double mins[MC_MAX_SINGLE];
+  double maxs[MC_MAX_SINGLE];
+  int32_t n_combo;
+  int32_t combo_kind[MC_MAX_COMBO];
+  int32_t combo_len[MC_MAX_COMBO];
+  int32_t combo_idx[MC_MAX_COMBO][MC_MAX_COMBO_LEN];
+  double weights[MC_MAX_COMBO + 1];
+} mc_classifier;
+
+/* Result of one accumulation step (Trainer::get_close + ClusterFactory get_mean). */
+typedef struct mc_scan_result {
+  int32_t is_min;       /* get_close's is_min_r: no candidate classified similar      */
+  int32_t has_best;     /* get<0>(result) != NULL (some combo-0 value > -1)            */
+  uint64_t best_pos;    /* static position of the first maximum of combo 0            */
+  double best_val;      /* that maximum                                                */
+  uint64_t n_flagged;   /* candidates marked similar (removed from the window)         */
+  uint32_t new_centre;  /* get_mean's argmin distance_d over the cluster (if !is_min)  */
+  uint32_t n_members;   /* cluster size after this step                                */
+} mc_scan_result;
+
+typedef struct mc_ctx mc_ctx;
+
+const char *mc_last_error(void);
+int mc_abi_version(void);
+
+/* Context on one GPU (hipSetDevice(device)); one process per GPU. */
+int mc_ctx_create(int device, mc_ctx **out);
+int mc_ctx_destroy(mc_ctx *ctx);
+
+/*
+ * Upload the encoded sequences.  codes: concatenation of every sequence's one-digit
+ * string as ChromosomeOneDigit leaves it (0..3 inside segments, 'N' or the raw upper-case
+ * byte outside; ChromosomeOneDigit.cpp:95-144).  seq_off[n+1] byte offsets.  seg: int32
+ * pairs [start,end] (inclusive) per segment (Chromosome.cpp:162-258), seg_off[n+1] pair
+ * offsets.  Replaces the Chromosome objects consumed by fill_table (ClusterFactory.h:40-55)
+ * and by GlobAlignE through Point::get_data_str (Trainer.cpp:18-27).
+ */
+int mc_load_sequences(mc_ctx *ctx, const uint8_t *codes, const uint64_t *seq_off, uint64_t n,
+                      const int32_t *seg, const uint64_t *seg_off);
+
+/* Largest k-mer count of the pseudocount-1 uint64 tables (Runner.cpp:57-67). */
+int mc_kmer_max(mc_ctx *ctx, int k, uint64_t *largest);
+
+/*
+ * Device-resident histograms, pseudocount 1, of width 1/2/4/8 bytes, plus their
+ * magnitudes (DivergencePoint mag incl. pseudocounts).  Replaces
+ * ClusterFactory::get_divergence_point (ClusterFactory.cpp:989-1010) + KmerHashTable
+ * wholesaleIncrement (KmerHashTable.cpp:193-223).
+ */
+int mc_kmer_build(mc_ctx *ctx, int k, int width_bytes);
+
+/* Copy histograms (n * 4^k * width bytes, id order) and magnitudes to the host. */
+int mc_get_histograms(mc_ctx *ctx, void *hist, uint64_t *mags);
+
+/*
+ * keys[p * m + i] = points[ids[i]]->distance(*points[pivots[p]])
+ * (DivergencePoint::distance, DivergencePoint.cpp:68-81; used by Trainer::split's sort
+ * comparators, Trainer.cpp:681-701).  Keys are <= 10000.
+ */
+int mc_distance_keys(mc_ctx *ctx, const uint32_t *pivots, uint32_t npiv, const uint32_t *ids,
+                     uint64_t m, uint16_t *keys);
+
+/*
+ * raw[i * nflag + f] = Feature<T>::raw(flags[f], *points[a[i]], *points[b[i]])
+ * (Feature.cpp:117-160) for the k-mer features LD/MANHATTAN/INTERSECTION/PEARSON/
+ * KULCZYNSKI2.  Used by Feature::normalize (Feature.cpp:86-114).
+ */
+int mc_pair_features(mc_ctx *ctx, const uint32_t *a, const uint32_t *b, uint64_t m,
+                     const uint16_t *flags, int nflag, double *raw);
+
+/* Install the trained classifier used by every classify/scan/mean-shift call. */
+int mc_set_classifier(mc_ctx *ctx, const mc_classifier *cls);
+
+/*
+ * For each pair i: cache = feat->compute(*points[a[i]], *points[b[i]]); sum = w0 + fma
+ * chain over combos; similar = round(1/(1+exp(-sum))) == 1.  Replaces the per-pair body
+ * of Trainer::merge (Trainer.cpp:129-157), filter (:334-349) and generate_feat_mat
+ * (:367-414).  Any output pointer may be NULL.
+ */
+int mc_classify_pairs(mc_ctx *ctx, const uint32_t *a, const uint32_t *b, uint64_t m,
+                      uint8_t *similar, double *combo0, double *sum);
+
+/*
+ * Batched utility::GlobAlignE(seqA,0,la-1,seqB,0,lb-1,1,-1,2,1).getIdentity() on the loaded
+ * sequences (GlobAlignE.cpp:123-305; called by Trainer::align, Trainer.cpp:15-31, and
+ * Feature::align, Feature.cpp:221-243).  len/ids may be NULL.
+ */
+int mc_nw_identity(mc_ctx *ctx, const uint32_t *a, const uint32_t *b, uint64_t m, double *ident,
+                   int32_t *len, int32_t *ids);
+
+/* The same on caller-provided byte strings (no loaded sequences needed). */
+int mc_nw_identity_raw(mc_ctx *ctx, const uint8_t *a, const uint64_t *a_off, const uint8_t *b,
+                       const uint64_t *b_off, uint64_t m, double *ident, int32_t *len,
+                       int32_t *ids, int32_t *score);
+
+/*
+ * Accumulation (ClusterFactory::accumulate, ClusterFactory.cpp:637-714).
+ * The bvec of Runner.cpp:342-350 is only ever shrunk after insert_finalize, so the device
+ * holds one static candidate order (bin-major, length-sorted within bins) plus an alive
+ * mask.  order[pos] = point id.
+ */
+int mc_set_order(mc_ctx *ctx, const uint32_t *order, uint64_t n);
+/* bvec::pop / bvec::erase of one static position (bvec.cpp:95-106, 349-353). */
+int mc_kill(mc_ctx *ctx, uint64_t pos);
+/* Start a new cluster whose member list is {first} (accumulate's `current = {last}`). */
+int mc_cluster_begin(mc_ctx *ctx, uint32_t first_id);
+/*
+ * One get_close step (Trainer.cpp:34-114) of centre `centre_id` over the alive static
+ * positions S..E (inclusive; the bvec_iterator range of ClusterFactory.cpp:650-654), then,
+ * if some candidate was similar, bvec::remove_available (bvec.cpp:289-318) + get_mean
+ * (ClusterFactory.cpp:382-425).  flagged_pos receives the removed static positions in
+ * ascending (bvec) order; cap is its capacity.
+ */
+int mc_scan(mc_ctx *ctx, uint32_t centre_id, uint64_t S, uint64_t E, uint32_t *flagged_pos,
+            uint64_t cap, mc_scan_result *res);
+
+/*
+ * One mean-shift iteration over all centres (the omp parallel for of ClusterFactory.cpp:
+ * 744-749 around mean_shift_update, :289-380): for centre j, the members of clusters
+ * j-delta..j+delta (CSR member_off[C+1]/members, cluster order) are filtered by the
+ * classifier (Trainer::filter) and the first member closest (distance_d) to their mean
+ * becomes new_centre[j] (Trainer::closest, Trainer.cpp:351-365); unchanged if none pass.
+ */
+int mc_mean_shift(mc_ctx *ctx, const uint32_t *centre_ids, uint32_t C, const uint64_t *member_off,
+                  const uint32_t *members, int delta, uint32_t *new_centre);
+
+/* Device time (ms) accumulated per kernel family since the last reset (diagnostics). */
+int mc_timers(mc_ctx *ctx, double *ms_out, int n, int reset);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,293 @@
+"""Regenerate the golden fixtures in tests/golden from the reference itself.
+
+Runs ONLY in the build container (it needs oracle/_ref, which is compiled from the
+read-only reference sources by oracle/Makefile).  Inputs are either the hand-written
+edge-case FASTA committed here (edge.fa) or synthetic FASTA produced by
+meshclust_amd.synth (deterministic, so only the generator arguments and a SHA-256 of the
+generated file are committed, not the file).  Outputs:
+
+  edge_parse.json          ChromListMaker/Chromosome/ChromosomeOneDigit per record
+  edge_hist.npz            fill_table + KmerHashTable histograms (k = 1, 3, 4, 6)
+  nw.npz                   GlobAlignE identity/length/matches/score for many pairs
+  train_<name>.npz         Trainer split/labels/feature bounds/weights + per-pair vectors
+  e2e_<name>.clstr.gz      meshclust --threads 1 output for the e2e configs
+  manifest.json            generator arguments, flags, SHA-256 of generated inputs
+
+Usage: python tests/golden/make_golden.py [--only NAME ...]
+"""
+import argparse
+import gzip
+import hashlib
+import json
+import os
+import subprocess
+import sys
+import tempfile
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+from meshclust_amd import synth  # noqa: E402
+
+REF = os.path.join(ROOT, "oracle", "_ref", "meshclust")
+PROBE = os.path.join(ROOT, "oracle", "_ref", "ref_probe")
+
+# name -> (generator args (n, L, T, mut, seed) or variable-length spec, meshclust flags)
+E2E = {
+    "a1k": ((1000, 500, 20, 0.04, 1), ["--id", "0.90", "--kmer", "3"]),
+    "b3k30": ((3000, 1000, 30, 0.03, 11), ["--id", "0.90"]),
+    "b3k300": ((3000, 1000, 300, 0.03, 12), ["--id", "0.90"]),
+    "m2k_id80": (("mixed", 2000, 40, 0.08, 21), ["--id", "0.80"]),
+    "m2k_id95": (("mixed", 2000, 40, 0.02, 22), ["--id", "0.95", "--delta", "3", "--iterations", "5"]),
+    "s1k_k5": ((1200, 400, 60, 0.05, 23), ["--id", "0.85", "--kmer", "5"]),
+}
+TRAIN = {"a1k": ("a1k", 3, 0.90)}
+
+
+def sha256(path):
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 20), b""):
+            h.update(chunk)
+    return h.hexdigest()
+
+
+def mixed_reads(n, n_templates, mut, seed):
+    """Templates of uniform length 700..1300 (exercises many bvec length bins)."""
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(700, 1301, size=n_templates)
+    temps = [rng.integers(0, 4, size=int(l), dtype=np.uint8) for l in lens]
+    alpha = np.frombuffer(b"ACGT", dtype=np.uint8)
+    p = mut / 3.0
+    for i in range(n):
+        t = i % n_templates
+        s = temps[t]
+        r = rng.random(len(s))
+        sub = r < p
+        dele = (r >= p) & (r < 2 * p)
+        ins = (r >= 2 * p) & (r < mut)
+        s2 = s.copy()
+        s2[sub] = rng.integers(0, 4, size=int(sub.sum()), dtype=np.uint8)
+        keep = ~dele
+        reps = np.where(ins, 2, 1)[keep]
+        base = np.repeat(s2[keep], reps)
+        idx = np.cumsum(reps) - 1
+        insm = reps == 2
+        base[idx[insm]] = rng.integers(0, 4, size=int(insm.sum()), dtype=np.uint8)
+        yield b"read%d template_%d" % (i, t), alpha[base].tobytes()
+
+
+def make_input(spec, path):
+    if spec[0] == "mixed":
+        _, n, t, mut, seed = spec
+        synth.write_fasta(path, mixed_reads(n, t, mut, seed))
+    else:
+        synth.generate(path, *spec)
+    return sha256(path)
+
+
+def run_probe(*args):
+    with tempfile.NamedTemporaryFile("r", suffix=".txt", delete=False) as tf:
+        out = tf.name
+    subprocess.run([PROBE, out] + [str(a) for a in args], check=True,
+                   stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    with open(out) as f:
+        text = f.read()
+    os.unlink(out)
+    return text
+
+
+def golden_parse():
+    text = run_probe("parse", os.path.join(HERE, "edge.fa"))
+    recs = []
+    cur = None
+    for line in text.splitlines():
+        tag, _, rest = line.partition(" ")
+        if tag == "R":
+            i, length, nseg = map(int, rest.split())
+            cur = {"length": length, "nseg": nseg}
+            recs.append(cur)
+        elif tag == "H":
+            cur["header"] = rest
+        elif tag == "S":
+            v = list(map(int, rest.split())) if rest.strip() else []
+            cur["segments"] = [v[k:k + 2] for k in range(0, len(v), 2)]
+        elif line.startswith("S"):
+            cur["segments"] = []
+        elif tag == "D":
+            cur["data_hex"] = rest.strip()
+    with open(os.path.join(HERE, "edge_parse.json"), "w") as f:
+        json.dump(recs, f, indent=1)
+    hist = {}
+    for k in (1, 3, 4, 6):
+        text = run_probe("hist", os.path.join(HERE, "edge.fa"), k)
+        rows, mags = [], []
+        for line in text.splitlines():
+            if line.startswith("K "):
+                v = list(map(int, line.split()[2:]))
+                mags.append(v[0])
+                rows.append(v[1:])
+        hist["k%d" % k] = np.array(rows, dtype=np.uint64)
+        hist["mag%d" % k] = np.array(mags, dtype=np.uint64)
+    np.savez_compressed(os.path.join(HERE, "edge_hist.npz"), **hist)
+
+
+def nw_pairs():
+    """Pairs covering identical, near, distant, unequal-length, N-containing, tiny inputs."""
+    rng = np.random.default_rng(5)
+    pairs = []
+    def mutate(s, mut):
+        out = bytearray()
+        for c in s:
+            r = rng.random()
+            if r < mut / 3:
+                out.append(int(rng.integers(0, 4)))
+            elif r < 2 * mut / 3:
+                continue
+            elif r < mut:
+                out.append(c)
+                out.append(int(rng.integers(0, 4)))
+            else:
+                out.append(c)
+        return bytes(out)
+    for length in (1, 2, 3, 5, 17, 64, 100, 257, 500, 1000):
+        for mut in (0.0, 0.03, 0.1, 0.3, 0.6):
+            a = bytes(rng.integers(0, 4, size=length, dtype=np.uint8))
+            b = mutate(a, mut) or bytes([int(rng.integers(0, 4))])
+            pairs.append((a, b))
+            pairs.append((b, a))
+    for _ in range(40):  # unrelated, unequal lengths
+        la, lb = int(rng.integers(1, 700)), int(rng.integers(1, 700))
+        pairs.append((bytes(rng.integers(0, 4, size=la, dtype=np.uint8)),
+                      bytes(rng.integers(0, 4, size=lb, dtype=np.uint8))))
+    for _ in range(20):  # 'N' (78) bytes outside segments and raw ASCII (no segments)
+        a = bytearray(rng.integers(0, 4, size=int(rng.integers(20, 300)), dtype=np.uint8))
+        b = bytearray(mutate(bytes(a), 0.1))
+        for arr in (a, b):
+            for _ in range(int(rng.integers(0, 6))):
+                arr[int(rng.integers(0, len(arr)))] = 78
+        pairs.append((bytes(a), bytes(b)))
+    pairs.append((b"GACGCTGTCTGA", b"GACGCTGTCTGA"))
+    pairs.append((b"ACGTACGT", bytes([0, 1, 2, 3, 0, 1, 2, 3])))
+    a = bytes(rng.integers(0, 4, size=3000, dtype=np.uint8))
+    pairs.append((a, mutate(a, 0.05)))
+    with tempfile.NamedTemporaryFile("w", suffix=".txt", delete=False) as tf:
+        for a, b in pairs:
+            tf.write(a.hex() + " " + b.hex() + "\n")
+        pf = tf.name
+    text = run_probe("nw", pf)
+    os.unlink(pf)
+    ident, length, ids, score = [], [], [], []
+    for line in text.splitlines():
+        _, i, l, m, s = line.split()
+        ident.append(float.fromhex(i))
+        length.append(int(l))
+        ids.append(int(m))
+        score.append(int(s))
+    a_cat = b"".join(a for a, _ in pairs)
+    b_cat = b"".join(b for _, b in pairs)
+    a_off = np.cumsum([0] + [len(a) for a, _ in pairs]).astype(np.int64)
+    b_off = np.cumsum([0] + [len(b) for _, b in pairs]).astype(np.int64)
+    np.savez_compressed(os.path.join(HERE, "nw.npz"),
+                        a=np.frombuffer(a_cat, np.uint8), a_off=a_off,
+                        b=np.frombuffer(b_cat, np.uint8), b_off=b_off,
+                        identity=np.array(ident), length=np.array(length, np.int32),
+                        ids=np.array(ids, np.int32), score=np.array(score, np.int32))
+
+
+def golden_train(name, fa, k, ident, npts=40):
+    text = run_probe("train", fa, k, ident, 3000, 20, npts)
+    sp, lp, ln, fl, fs, fmin, fmax, fc, w, P, DD = [], [], [], [], [], [], [], [], [], [], []
+    for line in text.splitlines():
+        t = line.split()
+        if not t:
+            continue
+        if t[0] == "SP":
+            sp.append((int(t[1]), int(t[2])))
+        elif t[0] in ("LP", "LN"):
+            (lp if t[0] == "LP" else ln).append((int(t[1]), int(t[2]), float.fromhex(t[3])))
+        elif t[0] == "FL":
+            fl = [int(x) for x in t[1:]]
+        elif t[0] == "FS":
+            fs = [int(x) for x in t[1:]]
+        elif t[0] == "FMIN":
+            fmin = [float.fromhex(x) for x in t[1:]]
+        elif t[0] == "FMAX":
+            fmax = [float.fromhex(x) for x in t[1:]]
+        elif t[0] == "FC":
+            fc.append([int(x) for x in t[1:]])
+        elif t[0] == "W":
+            w = [float.fromhex(x) for x in t[1:]]
+        elif t[0] == "P":
+            parts = line.split("|")
+            head = parts[0].split()
+            raw = [float.fromhex(x) for x in head[3:]]
+            cache = [float.fromhex(x) for x in parts[1].split()]
+            combos = [float.fromhex(x) for x in parts[2].split()]
+            tail = parts[3].split()
+            P.append((int(head[1]), int(head[2]), raw, cache, combos,
+                      float.fromhex(tail[0]), int(tail[1]), int(tail[2])))
+        elif t[0] == "DD":
+            DD.append([float.fromhex(x) for x in t[2:]])
+    ncombo = max(len(c) for c in fc)
+    combos_arr = np.full((len(fc), ncombo), -1, np.int32)
+    for i, c in enumerate(fc):
+        combos_arr[i, :len(c)] = c
+    np.savez_compressed(
+        os.path.join(HERE, "train_%s.npz" % name),
+        split_pairs=np.array(sp, np.int64), pos=np.array(lp), neg=np.array(ln),
+        lookup=np.array(fl, np.int32), is_sim=np.array(fs, np.int32),
+        mins=np.array(fmin), maxs=np.array(fmax), combos=combos_arr, weights=np.array(w),
+        pair_ij=np.array([(p[0], p[1]) for p in P], np.int32),
+        raw=np.array([p[2] for p in P]), cache=np.array([p[3] for p in P]),
+        combo_vals=np.array([p[4] for p in P]), sums=np.array([p[5] for p in P]),
+        decision=np.array([p[6] for p in P], np.int8),
+        distance=np.array([p[7] for p in P], np.uint64), dist_d=np.array(DD),
+        k=k, identity=ident)
+
+
+def golden_e2e(name, spec, flags, tmp):
+    fa = os.path.join(tmp, name + ".fa")
+    digest = make_input(spec, fa)
+    out = os.path.join(tmp, name + ".clstr")
+    log = subprocess.run([REF, fa] + flags + ["--threads", "1", "--output", out],
+                         capture_output=True, text=True)
+    if log.returncode != 0:
+        raise RuntimeError("reference failed on %s: %s" % (name, log.stderr[-2000:]))
+    with open(out, "rb") as f, open(os.path.join(HERE, "e2e_%s.clstr.gz" % name), "wb") as raw, \
+            gzip.GzipFile(fileobj=raw, mode="wb", mtime=0, filename="") as g:
+        g.write(f.read())
+    return name, {"generator": list(spec), "flags": flags, "sha256": digest}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", nargs="*")
+    args = ap.parse_args()
+    want = set(args.only) if args.only else None
+    man_path = os.path.join(HERE, "manifest.json")
+    manifest = json.load(open(man_path)) if os.path.exists(man_path) else {"e2e": {}}
+    manifest["reference_flags"] = "g++ -O3 -march=x86-64-v3 -fopenmp -std=c++11 (oracle/Makefile)"
+    with tempfile.TemporaryDirectory() as tmp:
+        if want is None or "parse" in want:
+            golden_parse()
+        if want is None or "nw" in want:
+            nw_pairs()
+        if want is None or "train" in want:
+            for name, (e2e_name, k, ident) in TRAIN.items():
+                fa = os.path.join(tmp, e2e_name + "_train.fa")
+                make_input(E2E[e2e_name][0], fa)
+                golden_train(name, fa, k, ident)
+        todo = [(n, s, f) for n, (s, f) in E2E.items() if want is None or n in want]
+        with ThreadPoolExecutor(max_workers=6) as ex:
+            for name, meta in ex.map(lambda a: golden_e2e(a[0], a[1], a[2], tmp), todo):
+                manifest["e2e"][name] = meta
+    with open(man_path, "w") as f:
+        json.dump(manifest, f, indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()
