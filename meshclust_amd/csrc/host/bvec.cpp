@@ -1,0 +1,232 @@
+// bvec.cpp -- see bvec.hpp.  Index arithmetic follows the reference line by line in meaning
+// (size_t wrap-arounds included); storage is ids instead of (Point*, bool) pairs because the
+// "similar" marks live on the device.
+#include "bvec.hpp"
+
+#include <algorithm>
+#include <limits>
+
+#include "common.hpp"
+
+namespace mc {
+
+BVec::BVec(const std::vector<uint64_t> &lengths_by_id, uint64_t bin_size) : len_(lengths_by_id) {
+  std::vector<uint64_t> lengths = lengths_by_id;
+  std::sort(lengths.begin(), lengths.end());
+  for (uint64_t i = 0; i < lengths.size(); i += bin_size) begin_bounds_.push_back(lengths[i]);
+  data_.resize(begin_bounds_.size());
+}
+
+bool BVec::index_of(uint64_t point, size_t *pfront, size_t *pback) const {
+  size_t low = begin_bounds_.size() - 1, high = 0;
+  for (size_t i = 0; i < begin_bounds_.size(); i++) {
+    size_t prev = 0, prev_index = 0;
+    if (i > 0) {
+      prev_index = i - 1;
+      prev = begin_bounds_[i - 1];
+    }
+    if (point >= prev && point <= begin_bounds_[i]) {
+      low = std::min(low, prev_index);
+      high = std::max(high, prev_index);
+    }
+  }
+  if (point >= begin_bounds_[begin_bounds_.size() - 1]) high = std::max(high, begin_bounds_.size() - 1);
+  if (pfront) *pfront = low;
+  if (pback) *pback = high;
+  return true;
+}
+
+bool BVec::inner_index_of(uint64_t length, size_t &idx, size_t *pfront, size_t *pback) const {
+  if (data_.at(idx).empty() || idx == data_.size()) {
+    if (pfront) {
+      for (size_t i = 0; i < data_.size(); i++)
+        if (!data_.at(i).empty()) {
+          idx = i;
+          *pfront = 0;
+          break;
+        }
+    }
+    if (pback) {
+      for (int i = (int)data_.size() - 1; i >= 0; i--)
+        if (!data_.at(i).empty()) {
+          idx = i;
+          *pback = 0;
+          break;
+        }
+    }
+    return true;
+  }
+  const auto &bin = data_[idx];
+  size_t front = 0, back = 0;
+  size_t low = 0, high = bin.size() - 1;
+  if (length < len_[bin[low]] && pfront != nullptr) *pfront = low;
+  if (length > len_[bin[high]] && pback != nullptr) *pback = high;
+  for (; low <= high;) {
+    size_t mid = (low + high) / 2;
+    uint64_t d = len_[bin[mid]];
+    if (d == length) {
+      front = mid;
+      back = mid;
+      break;
+    } else if (length < d) {
+      high = mid;
+    } else if (length > d) {
+      low = mid + 1;
+    }
+    if (low == high) {
+      front = low;
+      back = high;
+      break;
+    }
+  }
+  if (pfront) {
+    for (long i = (long)front; i >= 0 && len_[bin[i]] == length; i--) front = (size_t)i;
+    *pfront = front;
+  }
+  if (pback) {
+    for (long i = (long)back; i < (long)bin.size() && len_[bin[i]] == length; i++) back = (size_t)i;
+    *pback = back;
+  }
+  return true;
+}
+
+void BVec::insert(uint32_t id) {
+  uint64_t len = len_[id];
+  size_t front = 0, back = 0;
+  index_of(len, &front, &back);
+  std::vector<size_t> min_sizes;
+  size_t minimum = std::numeric_limits<size_t>::max();
+  for (size_t i = front; i <= back; i++) {
+    size_t sz = data_[i].size();
+    if (sz < minimum) {
+      minimum = sz;
+      min_sizes.clear();
+      min_sizes.push_back(i);
+    } else if (sz == minimum) {
+      min_sizes.push_back(i);
+    }
+  }
+  if (min_sizes.empty()) throw Error("bvec: no bins to insert into", 1);
+  data_.at(min_sizes[min_sizes.size() / 2]).push_back(id);
+}
+
+void BVec::insert_finalize() {
+  for (auto &bin : data_)
+    std::sort(bin.begin(), bin.end(), [&](uint32_t a, uint32_t b) { return len_[a] < len_[b]; });
+  order_.clear();
+  spos_.assign(len_.size(), std::numeric_limits<uint64_t>::max());
+  for (const auto &bin : data_)
+    for (uint32_t id : bin) {
+      spos_[id] = order_.size();
+      order_.push_back(id);
+    }
+}
+
+uint32_t BVec::pop() {
+  for (auto &bin : data_)
+    if (!bin.empty()) {
+      uint32_t p = bin[0];
+      bin.erase(bin.begin());
+      return p;
+    }
+  return NONE;
+}
+
+std::pair<BIdx, BIdx> BVec::get_range(uint64_t begin_len, uint64_t end_len) const {
+  BIdx front, back;
+  front.first = 0;
+  front.second = 0;
+  back.first = data_.size() - 1;
+  back.second = data_[back.first].size() - 1;
+  index_of(begin_len, &front.first, nullptr);
+  index_of(end_len, nullptr, &back.first);
+  inner_index_of(begin_len, front.first, &front.second, nullptr);
+  inner_index_of(end_len, back.first, nullptr, &back.second);
+  return {front, back};
+}
+
+void BVec::erase(size_t r, size_t c) { data_.at(r).erase(data_.at(r).begin() + c); }
+
+int64_t BVec::window(const BIdx &b, const BIdx &e, uint64_t *S, uint64_t *E) const {
+  // bvec_iterator::operator- (bvec_iterator.h:61-76), size_t arithmetic wrapping
+  auto less = [](const BIdx &x, const BIdx &y) {
+    return x.first < y.first || (x.first == y.first && x.second < y.second);
+  };
+  auto minus = [&](const BIdx &x, const BIdx &y) -> int64_t {  // x - y with x >= y
+    if (x.first == y.first) return (int64_t)(x.second - y.second);
+    uint64_t sum = 0;
+    sum += x.second;
+    sum += data_.at(y.first).size() - y.second;
+    for (size_t i = y.first + 1; i < x.first; i++) sum += data_.at(i).size();
+    return (int64_t)sum;
+  };
+  int64_t diff = less(e, b) ? -minus(b, e) : minus(e, b);
+  int64_t count = diff + 1;
+  if (count <= 0) return count;
+  // the first visited element is istart itself; deref = col->at(r).at(c)
+  size_t r = b.first, c = b.second;
+  if (r >= data_.size() || c >= data_[r].size()) throw Error("bvec_iterator dereference out of range", 1);
+  *S = spos_[data_[r][c]];
+  int64_t remaining = count - 1;
+  while (remaining > 0) {  // operator++ (bvec_iterator.cpp:3-21)
+    int64_t avail = (int64_t)data_[r].size() - 1 - (int64_t)c;
+    if (remaining <= avail) {
+      c += (size_t)remaining;
+      remaining = 0;
+      break;
+    }
+    remaining -= avail + 1;
+    r++;
+    c = 0;
+    while (r < data_.size() && data_[r].empty()) r++;
+    if (r >= data_.size()) throw Error("tried incrementing null iterator", 1);
+  }
+  *E = spos_[data_[r][c]];
+  return count;
+}
+
+void BVec::remove_positions(const std::vector<uint32_t> &pos_sorted, size_t a, size_t b,
+                            std::vector<uint32_t> &available) {
+  if (pos_sorted.empty()) return;
+  size_t k = 0;
+  for (size_t i = a; i <= b && k < pos_sorted.size(); i++) {
+    auto &bin = data_[i];
+    size_t w = 0;
+    for (size_t j = 0; j < bin.size(); j++) {
+      uint32_t id = bin[j];
+      if (k < pos_sorted.size() && spos_[id] == pos_sorted[k]) {
+        available.push_back(id);
+        k++;
+      } else {
+        bin[w++] = id;
+      }
+    }
+    bin.resize(w);
+  }
+  if (k != pos_sorted.size()) throw Error("remove_available: flagged candidate outside the window bins", 3);
+}
+
+std::pair<size_t, size_t> BVec::locate(uint64_t pos) const {
+  uint32_t id = order_[pos];
+  // static positions are bin-major, so the bin is found by the first element's position
+  size_t lo = 0, hi = data_.size();
+  for (size_t r = 0; r < data_.size(); r++) {
+    (void)lo;
+    (void)hi;
+    const auto &bin = data_[r];
+    if (bin.empty()) continue;
+    if (spos_[bin.back()] < pos) continue;
+    for (size_t c = 0; c < bin.size(); c++)
+      if (bin[c] == id) return {r, c};
+    break;
+  }
+  throw Error("bvec: static position not alive", 3);
+}
+
+size_t BVec::size() const {
+  size_t t = 0;
+  for (const auto &b : data_) t += b.size();
+  return t;
+}
+
+}  // namespace mc

@@ -1,0 +1,43 @@
+// cluster.hpp -- restatement of ClusterFactory<T>::MS and its helpers
+// (src/cluster/src/ClusterFactory.cpp:289-380 mean_shift_update, 382-425 get_mean,
+// 427-493 merge, 495-520 print_output, 637-714 accumulate, 717-761 MS).
+#pragma once
+#include <cstddef>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "bvec.hpp"
+#include "common.hpp"
+#include "fasta.hpp"
+
+namespace mc {
+
+struct Center {
+  uint32_t centre;               // id of the point the centre was cloned from (Center.h:14-27)
+  std::vector<uint32_t> points;  // members, in the reference's order
+  bool del = false;
+};
+
+struct ClusterConfig {
+  double sim = 0.90;
+  int iterations = 15;
+  int delta = 5;
+  bool verbose = true;
+};
+
+struct ClusterStats {
+  uint64_t scan_steps = 0;
+  uint64_t scan_candidates = 0;  // sum of get_close window sizes (K2 evaluations)
+  uint64_t update_evals = 0;     // filter evaluations in the mean-shift updates
+  uint64_t merge_evals = 0;
+};
+
+// Runs accumulation + `iterations` rounds of mean-shift update and merge.
+std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv, const ClusterConfig &cfg,
+                                       PhaseTimer &timer, ClusterStats &stats);
+
+// CD-HIT style writer (ClusterFactory.cpp:495-520).
+void write_clstr(const std::string &path, const Dataset &ds, const std::vector<Center> &part);
+
+}  // namespace mc

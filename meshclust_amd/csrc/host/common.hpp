@@ -1,0 +1,51 @@
+// common.hpp -- shared host-side helpers for the meshclust driver.
+#pragma once
+#include <chrono>
+#include <cstdint>
+#include <cstdio>
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../../include/meshclust_amd.h"
+
+namespace mc {
+
+// Error the reference would raise (uncaught exception / exit).  The driver prints it and
+// exits non-zero, as the reference does.
+struct Error : std::runtime_error {
+  int code;
+  explicit Error(const std::string &m, int c = 1) : std::runtime_error(m), code(c) {}
+};
+
+// Throws mc::Error when an ABI call fails (no fallback path exists).
+inline void check(int rc, const char *what) {
+  if (rc != MC_OK) {
+    const char *e = mc_last_error();
+    throw Error(std::string(what) + " failed: " + (e ? e : "?"), 3);
+  }
+}
+
+// Per-phase wall-clock accounting (printed with --timing, read by bench.py).
+struct PhaseTimer {
+  std::map<std::string, double> ms;
+  std::vector<std::string> order;
+  void add(const std::string &k, double v) {
+    if (!ms.count(k)) order.push_back(k);
+    ms[k] += v;
+  }
+};
+
+struct Scope {
+  PhaseTimer &t;
+  std::string k;
+  std::chrono::steady_clock::time_point s;
+  Scope(PhaseTimer &tt, std::string kk) : t(tt), k(std::move(kk)), s(std::chrono::steady_clock::now()) {}
+  ~Scope() {
+    auto e = std::chrono::steady_clock::now();
+    t.add(k, std::chrono::duration<double, std::milli>(e - s).count());
+  }
+};
+
+}  // namespace mc

@@ -1,0 +1,247 @@
+// runner.cpp -- see runner.hpp.
+#include "runner.hpp"
+
+#include <libgen.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <limits>
+
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+namespace mc {
+
+static void usage(const char *prog) {
+  printf("Usage: %s *.fasta [--id 0.90] [--kmer 3] [--delta 5] [--output output.clstr] [--iterations 20] "
+         "[--align] [--sample 3000] [--pivot 40] [--threads TMAX] [--device GPU] [--stats-json FILE]\n",
+         prog);
+  printf("MI355X-native MeShClust (meshclust_amd, C-ABI v%d)\n", MC_ABI_VERSION);
+}
+
+Options parse_options(int argc, char **argv, bool require_files) {
+  Options o;
+  for (int i = 1; i < argc; i++) {
+    std::string arg = argv[i];
+    auto need_long = [&](long lo, const char *msg) -> long {
+      errno = 0;
+      long v = strtol(argv[i + 1], nullptr, 10);
+      if (errno) {
+        perror(argv[i + 1]);
+        exit(EXIT_FAILURE);
+      } else if (v < lo) {
+        fprintf(stderr, "%s\n", msg);
+        exit(EXIT_FAILURE);
+      }
+      return v;
+    };
+    if (arg == "--id" && i + 1 < argc) {
+      char *end = nullptr;
+      double v = strtod(argv[i + 1], &end);
+      if (end == argv[i + 1] || v <= 0 || v >= 1) {
+        fprintf(stderr, "Similarity must be between 0 and 1\n");
+        exit(EXIT_FAILURE);
+      }
+      o.similarity = v;
+      i++;
+    } else if ((arg == "-k" || arg == "--kmer") && i + 1 < argc) {
+      o.k = (int)need_long(1, "K must be greater than 0.");
+      i++;
+    } else if ((arg == "-o" || arg == "--output") && i + 1 < argc) {
+      o.output = argv[++i];
+    } else if (arg == "-a" || arg == "--align") {
+      o.align = true;
+    } else if ((arg == "-s" || arg == "--sample") && i + 1 < argc) {
+      o.sample_size = (int)need_long(1, "Sample size must be greater than 0.");
+      i++;
+    } else if ((arg == "-p" || arg == "--pivot") && i + 1 < argc) {
+      o.pivots = (int)need_long(1, "Points per pivot must be greater than 0.");
+      i++;
+    } else if ((arg == "-t" || arg == "--threads") && i + 1 < argc) {
+      int t = atoi(argv[i + 1]);
+      if (t <= 0) {
+        fprintf(stderr, "Number of threads must be greater than 0.\n");
+        exit(1);
+      }
+      o.threads = t;
+      i++;
+    } else if ((arg == "-d" || arg == "--delta") && i + 1 < argc) {
+      o.delta = (int)need_long(0, "Delta must be greater than 0.");
+      i++;
+    } else if ((arg == "-i" || arg == "--iter" || arg == "--iterations") && i + 1 < argc) {
+      o.iterations = (int)need_long(1, "Iterations must be greater than 0.");
+      i++;
+    } else if (arg == "--device" && i + 1 < argc) {
+      o.device = atoi(argv[++i]);
+    } else if (arg == "--stats-json" && i + 1 < argc) {
+      o.stats_json = argv[++i];
+    } else if (arg == "--quiet") {
+      o.quiet = true;
+    } else {
+      struct stat st;
+      if (stat(argv[i], &st) == 0 && S_ISREG(st.st_mode)) {
+        o.files.push_back(argv[i]);
+      } else {
+        usage(argv[0]);
+        exit(EXIT_FAILURE);
+      }
+    }
+  }
+  if (o.files.empty() && require_files) {
+    usage(argv[0]);
+    exit(EXIT_FAILURE);
+  }
+  std::sort(o.files.begin(), o.files.end(), [](const std::string &a, const std::string &b) {
+    char *as = strdup(a.c_str()), *bs = strdup(b.c_str());
+    bool r = std::string(basename(as)) < std::string(basename(bs));
+    free(as);
+    free(bs);
+    return r;
+  });
+  return o;
+}
+
+// Runner::find_k (Runner.cpp:265-292): integer mean length per file, mean over files.
+static int find_k(const Dataset &ds, bool verbose) {
+  unsigned long long length = 0;
+  for (size_t f = 0; f < ds.file_count.size(); f++) length += ds.file_len_sum[f] / ds.file_count[f];
+  length /= ds.file_count.size();
+  int newk = (int)std::ceil(std::log((double)length) / std::log(4)) - 1;
+  if (verbose) printf("avg length: %llu\nRecommended K: %d\n", length, newk);
+  return newk;
+}
+
+RunResult run_pipeline(const Dataset &ds, mc_ctx *ctx, Options opt, bool upload) {
+  RunResult rr;
+  rr.n = ds.size();
+  const bool verbose = !opt.quiet;
+  int threads = opt.threads;
+#ifdef _OPENMP
+  if (threads <= 0) threads = omp_get_max_threads();
+#else
+  threads = 1;
+#endif
+  if (opt.k == -1) opt.k = find_k(ds, verbose);
+  if (opt.similarity < 0.6) opt.align = true;
+  if (opt.sample_size == 0) opt.sample_size = 3000;
+  if (opt.k < 1 || opt.k > 12) throw Error("k must be in 1..12 on this engine (4^k-bin dense histograms)", 1);
+  rr.k = opt.k;
+  auto t0 = std::chrono::steady_clock::now();
+  if (upload) {
+    Scope s(rr.timer, "upload");
+    check(mc_load_sequences(ctx, ds.codes.data(), ds.seq_off.data(), ds.size(), ds.seg.data(), ds.seg_off.data()),
+          "mc_load_sequences");
+  }
+  {
+    Scope s(rr.timer, "kmer");
+    check(mc_kmer_max(ctx, opt.k, &rr.largest), "mc_kmer_max");
+    int width = rr.largest <= 0xff ? 1 : rr.largest <= 0xffff ? 2 : rr.largest <= 0xffffffffull ? 4 : 8;
+    rr.width = width;
+    if (verbose) printf("Using %d bit histograms\n", 8 * width);
+    check(mc_kmer_build(ctx, opt.k, width), "mc_kmer_build");
+  }
+  TrainerConfig tc;
+  tc.n_points = opt.sample_size;
+  tc.max_pts_from_one = opt.pivots;
+  tc.cutoff = opt.similarity;
+  tc.k = opt.align ? 0 : opt.k;
+  tc.threads = threads;
+  tc.verbose = verbose;
+  Trainer tr(ds, ctx, tc, rr.timer);
+  {
+    Scope s(rr.timer, "train");
+    tr.train();
+  }
+  if (opt.align) throw Error("--align / --id < 0.6 (NW-only classification) is not wired into the GPU scan yet", 2);
+  mc_classifier cls = tr.classifier();
+  check(mc_set_classifier(ctx, &cls), "mc_set_classifier");
+  BVec bv(ds.lengths, 1000);
+  {
+    Scope s(rr.timer, "bvec");
+    for (uint32_t id = 0; id < ds.size(); id++) bv.insert(id);
+    bv.insert_finalize();
+  }
+  ClusterConfig cc;
+  cc.sim = opt.similarity;
+  cc.iterations = opt.iterations;
+  cc.delta = opt.delta;
+  cc.verbose = verbose;
+  rr.part = mean_shift_cluster(ds, ctx, bv, cc, rr.timer, rr.stats);
+  rr.timer.add("total_pipeline",
+               std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+  return rr;
+}
+
+std::string stats_json(const RunResult &rr, double parse_ms, double write_ms) {
+  char b[512];
+  std::string o;
+  snprintf(b, sizeof b, "{\"n\": %zu, \"k\": %d, \"width\": %d, \"clusters\": %zu, \"parse_ms\": %.3f, \"write_ms\": %.3f",
+           rr.n, rr.k, rr.width, rr.part.size(), parse_ms, write_ms);
+  o += b;
+  snprintf(b, sizeof b, ", \"scan_steps\": %llu, \"scan_candidates\": %llu, \"update_evals\": %llu, \"merge_evals\": %llu",
+           (unsigned long long)rr.stats.scan_steps, (unsigned long long)rr.stats.scan_candidates,
+           (unsigned long long)rr.stats.update_evals, (unsigned long long)rr.stats.merge_evals);
+  o += b;
+  o += ", \"phases_ms\": {";
+  for (size_t i = 0; i < rr.timer.order.size(); i++) {
+    snprintf(b, sizeof b, "%s\"%s\": %.3f", i ? ", " : "", rr.timer.order[i].c_str(), rr.timer.ms.at(rr.timer.order[i]));
+    o += b;
+  }
+  o += "}}";
+  return o;
+}
+
+static void write_stats(const std::string &path, const RunResult &rr, double parse_ms, double write_ms) {
+  FILE *f = fopen(path.c_str(), "w");
+  if (!f) return;
+  fprintf(f, "%s\n", stats_json(rr, parse_ms, write_ms).c_str());
+  fclose(f);
+}
+
+int meshclust_main(int argc, char **argv) {
+  Options opt = parse_options(argc, argv);
+  int threads = opt.threads;
+#ifdef _OPENMP
+  if (threads > 0) omp_set_num_threads(threads);
+  threads = omp_get_max_threads();
+#endif
+  mc_ctx *ctx = nullptr;
+  try {
+    for (const auto &f : opt.files)
+      if (access(f.c_str(), F_OK) == -1) {
+        fprintf(stderr, "File \"%s\" does not exist\n", f.c_str());
+        exit(1);
+      }
+    auto t0 = std::chrono::steady_clock::now();
+    Dataset ds;
+    parse_fasta_files(opt.files, ds, threads);
+    double parse_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    check(mc_ctx_create(opt.device, &ctx), "mc_ctx_create");
+    RunResult rr = run_pipeline(ds, ctx, opt);
+    auto t1 = std::chrono::steady_clock::now();
+    if (!opt.quiet) printf("Printing output\n");
+    write_clstr(opt.output, ds, rr.part);
+    double write_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();
+    if (!opt.stats_json.empty()) write_stats(opt.stats_json, rr, parse_ms, write_ms);
+    mc_ctx_destroy(ctx);
+    return 0;
+  } catch (const Error &e) {
+    if (e.code != 0) fprintf(stderr, "meshclust: %s\n", e.what());
+    if (ctx) mc_ctx_destroy(ctx);
+    return e.code;
+  } catch (const std::exception &e) {
+    fprintf(stderr, "meshclust: %s\n", e.what());
+    if (ctx) mc_ctx_destroy(ctx);
+    return 1;
+  }
+}
+
+}  // namespace mc

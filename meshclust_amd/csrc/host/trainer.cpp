@@ -1,0 +1,319 @@
+// trainer.cpp -- see trainer.hpp.  Compiled with -ffp-contract=off.
+#include "trainer.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <set>
+
+namespace mc {
+
+namespace {
+
+struct ExitZero : Error {
+  ExitZero(const std::string &m) : Error(m, 0) {}
+};
+
+// get_bin of resize_vec / bin_data (Trainer.cpp:217-225, 493-501)
+inline int get_bin(double x, double min_align, double max_align, int num_bins) {
+  if (x >= max_align) return num_bins - 1;
+  if (x <= min_align) return 0;
+  return (int)(num_bins * (x - min_align) / (max_align - min_align));
+}
+
+using Labeled = std::pair<PairId, double>;
+
+// resize_vec (Trainer.cpp:201-243): bins by identity, then repeatedly takes the first
+// ceil(left/bins) items of every bin from the top bin down -- it can over-fill.
+std::vector<Labeled> resize_vec(const std::vector<Labeled> &vec, size_t new_size, double min_align,
+                                double max_align, int num_bins) {
+  if (new_size == vec.size()) return vec;
+  std::vector<std::vector<Labeled>> bins(num_bins);
+  for (const auto &p : vec) bins.at(get_bin(p.second, min_align, max_align, num_bins)).push_back(p);
+  std::vector<Labeled> data;
+  while (data.size() < new_size) {
+    int items_left = (int)(new_size - data.size());
+    int take = (int)std::ceil((double)items_left / num_bins);
+    for (int i = (int)bins.size() - 1; i >= 0; i--)
+      for (int j = 0; j < (int)std::min((size_t)take, bins[i].size()); j++) data.push_back(bins[i][j]);
+  }
+  return data;
+}
+
+// bin_data (Trainer.cpp:490-526): 10 identity bins, alternate rows go to train / test,
+// the parity flipping from bin to bin.
+std::pair<std::vector<PairId>, std::vector<PairId>> bin_data(const std::vector<Labeled> &vec, double min_align,
+                                                             double max_align) {
+  const int n_bins = 10;
+  std::vector<std::vector<Labeled>> bins(n_bins);
+  for (const auto &d : vec) bins.at(get_bin(d.second, min_align, max_align, n_bins)).push_back(d);
+  std::vector<PairId> train, test;
+  int last = 0;
+  for (const auto &bin : bins) {
+    for (int i = 0; i < (int)bin.size(); i++) {
+      if (i % 2 == last) train.push_back(bin[i].first);
+      else test.push_back(bin[i].first);
+    }
+    last = !last;
+  }
+  return {train, test};
+}
+
+}  // namespace
+
+bool Trainer::hdr_less(uint32_t a, uint32_t b) const { return ds_.headers[a].compare(ds_.headers[b]) < 0; }
+
+void Trainer::nw_batch(const std::vector<PairId> &pairs, std::vector<double> &ident) {
+  std::vector<uint32_t> a(pairs.size()), b(pairs.size());
+  for (size_t i = 0; i < pairs.size(); i++) {
+    a[i] = pairs[i].first;
+    b[i] = pairs[i].second;
+  }
+  ident.assign(pairs.size(), 0.0);
+  if (pairs.empty()) return;
+  check(mc_nw_identity(ctx_, a.data(), b.data(), pairs.size(), ident.data(), nullptr, nullptr), "mc_nw_identity");
+}
+
+// Trainer::split (Trainer.cpp:653-783)
+std::vector<PairId> Trainer::split() {
+  const size_t N = ds_.size();
+  auto hcmp = [&](const PairId &a, const PairId &b) {
+    int c = ds_.headers[a.first].compare(ds_.headers[b.first]);
+    return c < 0 || (c == 0 && ds_.headers[a.second].compare(ds_.headers[b.second]) < 0);
+  };
+  std::set<PairId, decltype(hcmp)> pairs(hcmp);
+  std::vector<uint32_t> points(N);
+  for (size_t i = 0; i < N; i++) points[i] = (uint32_t)i;
+  std::vector<uint32_t> all_ids = points;  // distance keys are requested in id order
+  {
+    Scope s(timer_, "train.sort_keys");
+    std::sort(points.begin(), points.end(),
+              [&](uint32_t a, uint32_t b) { return ds_.lengths[a] < ds_.lengths[b]; });
+    uint32_t begin_pt = points[N / 2];
+    std::vector<uint16_t> key0(N);
+    check(mc_distance_keys(ctx_, &begin_pt, 1, all_ids.data(), N, key0.data()), "mc_distance_keys");
+    std::sort(points.begin(), points.end(), [&](uint32_t a, uint32_t b) { return key0[a] < key0[b]; });
+  }
+  int num_iterations = (int)std::ceil(((double)cfg_.n_points) / cfg_.max_pts_from_one) - 1;
+  if (num_iterations <= 0) throw Error("sample size must exceed points per pivot (integer division by zero in Trainer::split)", 1);
+  std::vector<uint32_t> indices;
+  for (int i = 0; i <= num_iterations; i++) indices.push_back(points[(size_t)i * (N - 1) / (size_t)num_iterations]);
+  if (cfg_.verbose) printf("Point pairs: %zu\n", indices.size());
+  const size_t to_add_each = cfg_.max_pts_from_one / 2;
+  const size_t P = indices.size();
+  // every pivot's distance to every point: one GPU launch
+  std::vector<uint16_t> keys(P * N);
+  std::vector<std::vector<uint32_t>> sorted(P);
+  {
+    Scope s(timer_, "train.sort_keys");
+    check(mc_distance_keys(ctx_, indices.data(), (uint32_t)P, all_ids.data(), N, keys.data()), "mc_distance_keys");
+#pragma omp parallel for schedule(dynamic) num_threads(cfg_.threads)
+    for (size_t i = 0; i < P; i++) {
+      const uint16_t *kk = &keys[i * N];
+      sorted[i] = points;
+      std::sort(sorted[i].begin(), sorted[i].end(), [&](uint32_t a, uint32_t b) { return kk[a] < kk[b]; });
+    }
+  }
+  // binary search with alignment (:703-721): the 150 dependent chains advance together, one
+  // batched NW launch per step.
+  std::vector<size_t> offset(P, N / 4), pivot(P, 2 * (N / 4));
+  std::vector<char> active(P, 1);
+  {
+    Scope s(timer_, "train.nw_search");
+    for (;;) {
+      std::vector<PairId> batch;
+      std::vector<size_t> who;
+      for (size_t i = 0; i < P; i++) {
+        if (active[i] && offset[i] == 0) active[i] = 0;
+        if (active[i]) {
+          batch.emplace_back(indices[i], sorted[i][pivot[i]]);
+          who.push_back(i);
+        }
+      }
+      if (batch.empty()) break;
+      std::vector<double> al;
+      nw_batch(batch, al);
+      for (size_t t = 0; t < who.size(); t++) {
+        size_t i = who[t];
+        double algn = al[t];
+        if (algn < cfg_.cutoff) pivot[i] -= offset[i];
+        else if (algn > cfg_.cutoff) pivot[i] += offset[i];
+        else { active[i] = 0; continue; }
+        offset[i] /= 2;
+      }
+    }
+  }
+  int aerr = 0;
+  for (size_t i = 0; i < P; i++) {
+    const auto &pts = sorted[i];
+    const uint32_t p = indices[i];
+    double before_inc = (double)pivot[i] / to_add_each;
+    double after_inc = ((double)(pts.size() - pivot[i])) / to_add_each;
+    if (before_inc < 1) aerr = 1;
+    else if (after_inc < 1) aerr = -1;
+    double before_start = 0, after_start = (double)pivot[i];
+    std::vector<PairId> buf;
+    for (int t = 0; t < (int)to_add_each; t++) {
+      int idx = (int)std::round(before_start);
+      uint32_t q = pts[idx];
+      buf.push_back(hdr_less(p, q) ? PairId(p, q) : PairId(q, p));
+      before_start += before_inc;
+    }
+    for (int t = 0; t < (int)to_add_each && std::round(after_start) < (double)pts.size(); t++) {
+      int idx = (int)std::round(after_start);
+      uint32_t q = pts[idx];
+      buf.push_back(hdr_less(p, q) ? PairId(p, q) : PairId(q, p));
+      after_start += after_inc;
+    }
+    pairs.insert(buf.begin(), buf.end());
+  }
+  if (aerr < 0) fprintf(stderr, "Warning: Alignment may be too small for sampling\n");
+  else if (aerr > 0) fprintf(stderr, "Warning: Alignment may be too large for sampling\n");
+  return std::vector<PairId>(pairs.begin(), pairs.end());
+}
+
+// Trainer::get_labels (Trainer.cpp:253-333).  random_shuffle only permutes the alignment
+// order; results land in header-ordered sets, so it has no effect and is skipped.
+void Trainer::get_labels(const std::vector<PairId> &vec, std::vector<Labeled> &bp, std::vector<Labeled> &bn) {
+  auto hcmp = [&](const Labeled &a, const Labeled &b) {
+    int c = ds_.headers[a.first.first].compare(ds_.headers[b.first.first]);
+    return c < 0 || (c == 0 && ds_.headers[a.first.second].compare(ds_.headers[b.first.second]) < 0);
+  };
+  std::vector<double> al;
+  {
+    Scope s(timer_, "train.nw_labels");
+    nw_batch(vec, al);
+  }
+  std::set<Labeled, decltype(hcmp)> buf_pos(hcmp), buf_neg(hcmp);
+  for (size_t i = 0; i < vec.size(); i++) {
+    if (al[i] >= cfg_.cutoff) buf_pos.insert({vec[i], al[i]});
+    else buf_neg.insert({vec[i], al[i]});
+  }
+  if (cfg_.verbose) printf("positive=%zu negative=%zu\n", buf_pos.size(), buf_neg.size());
+  if (buf_pos.empty() || buf_neg.empty()) {
+    std::string m = "Identity value does not match sampled data: ";
+    m += buf_pos.empty() ? "Too many sequences below identity" : "Too many sequences above identity";
+    printf("%s\n", m.c_str());
+    throw ExitZero(m);
+  }
+  size_t m_size = std::min(buf_pos.size(), buf_neg.size());
+  std::vector<Labeled> vpos(buf_pos.begin(), buf_pos.end()), vneg(buf_neg.begin(), buf_neg.end());
+  bp = resize_vec(vpos, m_size, cfg_.cutoff, 1, 5);
+  bn = resize_vec(vneg, m_size, 0.4, cfg_.cutoff, 5);
+  if (cfg_.verbose) printf("positive=%zu negative=%zu\n", bp.size(), bn.size());
+}
+
+// generate_feat_mat (Trainer.cpp:367-414): column 0 is the constant 1, then the combos of
+// feat->compute(first, second); labels +1 for the positive block, -1 for the negative.
+Matrix Trainer::feat_matrix(const std::vector<PairId> &pos, const std::vector<PairId> &neg, int ncols,
+                            Matrix &labels) {
+  const size_t n = pos.size() + neg.size();
+  Matrix fm((int)n, ncols);
+  labels = Matrix((int)n, 1);
+  std::vector<uint32_t> a(n), b(n);
+  for (size_t i = 0; i < n; i++) {
+    const PairId &p = i < pos.size() ? pos[i] : neg[i - pos.size()];
+    a[i] = p.first;
+    b[i] = p.second;
+  }
+  const size_t ns = feat.lookup.size();
+  std::vector<double> raw(n * ns);
+  if (n) check(mc_pair_features(ctx_, a.data(), b.data(), n, feat.lookup.data(), (int)ns, raw.data()), "mc_pair_features");
+  for (size_t i = 0; i < n; i++) {
+    double *cache = &raw[i * ns];
+    feat.normalize_cache(cache);
+    fm.set((int)i, 0, 1);
+    for (int col = 1; col < ncols; col++) fm.set((int)i, col, feat.combo(col - 1, cache));
+    labels.set((int)i, 0, i < pos.size() ? 1 : -1);
+  }
+  return fm;
+}
+
+void Trainer::train(double acc_cutoff) {
+  std::pair<std::vector<PairId>, std::vector<PairId>> training, testing;
+  if (cfg_.k != 0) {
+    if (cfg_.verbose) printf("Splitting data\n");
+    split_pairs = split();
+    get_labels(split_pairs, label_pos, label_neg);
+    auto pos = bin_data(label_pos, cfg_.cutoff, 1);
+    training.first = pos.first;
+    testing.first = pos.second;
+    auto neg = bin_data(label_neg, 0, cfg_.cutoff);
+    training.second = neg.first;
+    testing.second = neg.second;
+    if (cfg_.verbose)
+      printf("training positive: %zu\ntraining negative: %zu\ntesting positive: %zu\ntesting negative: %zu\n",
+             training.first.size(), training.second.size(), testing.first.size(), testing.second.size());
+    if (testing.first.empty() || testing.second.empty()) throw Error("not enough points to sample", 1);
+  }
+  if (cfg_.k == 0) {  // alignment mode (Trainer.cpp:570-577)
+    feat.add_feature(MC_FEAT_ALIGN, MC_COMBO_SELF);
+    feat.normalize_with({}, 0);
+    feat.finalize();
+    weights = {-1 * cfg_.cutoff, 1};
+    return;
+  }
+  Scope s(timer_, "train.glm");
+  const std::vector<std::pair<uint16_t, int>> bit_feats = {
+      {MC_FEAT_INTERSECTION | MC_FEAT_LD, MC_COMBO_SELF},
+      {MC_FEAT_MANHATTAN | MC_FEAT_LD, MC_COMBO_SQUARED},
+      {MC_FEAT_PEARSON, MC_COMBO_SELF},
+      {MC_FEAT_KULCZYNSKI2 | MC_FEAT_LD, MC_COMBO_SQUARED}};
+  double prev_acc = -10000;
+  std::vector<std::vector<double>> matvec;
+  std::vector<FeatureSet> features;
+  GLM glm;
+  const size_t min_no_features = std::max(1, (int)bit_feats.size() - 1);
+  for (size_t num_features = min_no_features; num_features <= bit_feats.size(); num_features++) {
+    for (size_t j = feat.size(); j < num_features && j < bit_feats.size(); j++)
+      feat.add_feature(bit_feats[j].first, bit_feats[j].second);
+    // feat->normalize(training.first); feat->normalize(training.second); (min/max carry over)
+    {
+      auto need = feat.flags_needed();
+      std::vector<uint32_t> a, b;
+      for (auto *v : {&training.first, &training.second})
+        for (const auto &p : *v) {
+          a.push_back(p.first);
+          b.push_back(p.second);
+        }
+      std::vector<double> raw(a.size() * need.size());
+      if (!need.empty() && !a.empty())
+        check(mc_pair_features(ctx_, a.data(), b.data(), a.size(), need.data(), (int)need.size(), raw.data()),
+              "mc_pair_features");
+      feat.normalize_with(raw, a.size());
+    }
+    feat.finalize();
+    if (cfg_.verbose) feat.print_bounds();
+    Matrix ltrain, ltest;
+    Matrix mtrain = feat_matrix(training.first, training.second, (int)num_features + 1, ltrain);
+    Matrix mtest = feat_matrix(testing.first, testing.second, (int)num_features + 1, ltest);
+    glm.train(mtrain, ltrain);
+    std::vector<double> w(glm.weights.rows);
+    for (int r = 0; r < glm.weights.rows; r++) w[r] = glm.weights.get(r, 0);
+    weights = w;
+    Matrix p = glm.predict(mtest);
+    for (int row = 0; row < p.rows; row++)
+      if (p.get(row, 0) == 0) p.set(row, 0, -1);
+    double acc = std::get<0>(glm.accuracy(ltest, p, cfg_.verbose));
+    Matrix q = glm.predict(mtrain);
+    for (int row = 0; row < q.rows; row++)
+      if (q.get(row, 0) == 0) q.set(row, 0, -1);
+    glm.accuracy(ltrain, q, cfg_.verbose);
+    if (acc - prev_acc <= 1 && acc >= 90.0) {
+      weights = matvec.back();
+      feat = features.back();
+      if (cfg_.verbose) printf("feat size is %zu\n", feat.size());
+      break;
+    }
+    matvec.push_back(weights);
+    features.push_back(feat);
+    prev_acc = acc;
+    if (acc >= acc_cutoff) {
+      if (cfg_.verbose) printf("breaking from acc cutoff\n");
+      break;
+    }
+  }
+  if (cfg_.verbose) printf("Final: feat size is %zu\nUsing %zu features\n", feat.size(), weights.size() - 1);
+}
+
+}  // namespace mc

@@ -1,0 +1,293 @@
+// mc_oracle_engine.cpp -- TEST INFRASTRUCTURE ONLY.
+//
+// A sequential CPU implementation of the libmcgpu C-ABI (include/meshclust_amd.h) built
+// from the oracle restatement (mc_oracle.c).  tests/ link the host driver objects against
+// this library instead of libmcgpu to check, without a GPU, that the host restatement of
+// the reference control flow (training sampler, bvec, accumulate, mean shift, merge,
+// writer) reproduces the reference's .clstr byte for byte.  The shipped bin/meshclust
+// links only libmcgpu; this file is never part of the product.
+#include <cfloat>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "mc_oracle.h"
+
+struct mc_ctx {
+  std::vector<uint8_t> codes;
+  std::vector<uint64_t> seq_off, seg_off;
+  std::vector<int32_t> seg;
+  uint64_t n = 0;
+  int k = 0, B = 0, width = 1;
+  std::vector<uint8_t> hist;  // n * B * width
+  std::vector<uint64_t> mags;
+  mc_classifier cls{};
+  bool has_cls = false;
+  std::vector<uint32_t> order;
+  std::vector<uint8_t> alive;
+  std::vector<uint32_t> members;  // current cluster, in `current` order
+};
+
+static thread_local std::string g_err;
+static int fail(int code, const std::string &m) {
+  g_err = m;
+  return code;
+}
+
+extern "C" {
+
+const char *mc_last_error(void) { return g_err.c_str(); }
+int mc_abi_version(void) { return MC_ABI_VERSION; }
+
+int mc_ctx_create(int, mc_ctx **out) {
+  *out = new mc_ctx();
+  return MC_OK;
+}
+int mc_ctx_destroy(mc_ctx *c) {
+  delete c;
+  return MC_OK;
+}
+
+int mc_load_sequences(mc_ctx *c, const uint8_t *codes, const uint64_t *seq_off, uint64_t n, const int32_t *seg,
+                      const uint64_t *seg_off) {
+  c->n = n;
+  c->codes.assign(codes, codes + seq_off[n]);
+  c->seq_off.assign(seq_off, seq_off + n + 1);
+  c->seg_off.assign(seg_off, seg_off + n + 1);
+  c->seg.assign(seg, seg + 2 * seg_off[n]);
+  return MC_OK;
+}
+
+static int hist_of(mc_ctx *c, uint64_t i, int k, std::vector<uint64_t> &h) {
+  h.resize((size_t)1 << (2 * k));
+  const uint8_t *s = c->codes.data() + c->seq_off[i];
+  int64_t len = (int64_t)(c->seq_off[i + 1] - c->seq_off[i]);
+  int nseg = (int)(c->seg_off[i + 1] - c->seg_off[i]);
+  return mco_kmer_hist(s, len, c->seg.data() + 2 * c->seg_off[i], nseg, k, 1, h.data());
+}
+
+int mc_kmer_max(mc_ctx *c, int k, uint64_t *largest) {
+  uint64_t mx = 0;
+  std::vector<uint64_t> h;
+  for (uint64_t i = 0; i < c->n; i++) {
+    int rc = hist_of(c, i, k, h);
+    if (rc) return fail(rc, "invalid nucleotide in k-mer");
+    for (auto v : h) mx = v > mx ? v : mx;
+  }
+  *largest = mx;
+  return MC_OK;
+}
+
+int mc_kmer_build(mc_ctx *c, int k, int width) {
+  c->k = k;
+  c->B = 1 << (2 * k);
+  c->width = width;
+  c->hist.assign(c->n * c->B * width, 0);
+  c->mags.assign(c->n, 0);
+  std::vector<uint64_t> h;
+  for (uint64_t i = 0; i < c->n; i++) {
+    int rc = hist_of(c, i, k, h);
+    if (rc) return fail(rc, "invalid nucleotide in k-mer");
+    uint64_t mag = 0;
+    uint8_t *dst = c->hist.data() + i * c->B * width;
+    for (int b = 0; b < c->B; b++) {
+      uint64_t v = h[b];
+      mag += v;
+      switch (width) {
+        case 1: ((uint8_t *)dst)[b] = (uint8_t)v; break;
+        case 2: ((uint16_t *)dst)[b] = (uint16_t)v; break;
+        case 4: ((uint32_t *)dst)[b] = (uint32_t)v; break;
+        default: ((uint64_t *)dst)[b] = v; break;
+      }
+    }
+    c->mags[i] = mag;
+  }
+  return MC_OK;
+}
+
+int mc_get_histograms(mc_ctx *c, void *hist, uint64_t *mags) {
+  if (hist) memcpy(hist, c->hist.data(), c->hist.size());
+  if (mags) memcpy(mags, c->mags.data(), c->mags.size() * 8);
+  return MC_OK;
+}
+
+static const void *row(mc_ctx *c, uint32_t id) { return c->hist.data() + (size_t)id * c->B * c->width; }
+static uint64_t len_of(mc_ctx *c, uint32_t id) { return c->seq_off[id + 1] - c->seq_off[id]; }
+
+int mc_distance_keys(mc_ctx *c, const uint32_t *piv, uint32_t np, const uint32_t *ids, uint64_t m, uint16_t *keys) {
+#pragma omp parallel for schedule(dynamic)
+  for (uint32_t p = 0; p < np; p++)
+    for (uint64_t i = 0; i < m; i++)
+      keys[p * m + i] = (uint16_t)mco_distance(row(c, ids[i]), row(c, piv[p]), c->width, c->B, c->mags[ids[i]],
+                                               c->mags[piv[p]]);
+  return MC_OK;
+}
+
+static int raw_one(mc_ctx *c, uint16_t f, uint32_t a, uint32_t b, double *out) {
+  return mco_raw(f, row(c, a), row(c, b), c->width, c->B, c->mags[a], c->mags[b], len_of(c, a), len_of(c, b), out);
+}
+
+int mc_pair_features(mc_ctx *c, const uint32_t *a, const uint32_t *b, uint64_t m, const uint16_t *flags, int nflag,
+                     double *raw) {
+  for (uint64_t i = 0; i < m; i++)
+    for (int f = 0; f < nflag; f++) {
+      int rc = raw_one(c, flags[f], a[i], b[i], &raw[i * nflag + f]);
+      if (rc) return fail(rc, "feature error");
+    }
+  return MC_OK;
+}
+
+int mc_set_classifier(mc_ctx *c, const mc_classifier *cls) {
+  c->cls = *cls;
+  c->has_cls = true;
+  return MC_OK;
+}
+
+static int classify(mc_ctx *c, uint32_t a, uint32_t b, double *sum, double *c0) {
+  double raw[MC_MAX_SINGLE];
+  for (int f = 0; f < c->cls.n_single; f++) raw_one(c, c->cls.lookup[f], a, b, &raw[f]);
+  return mco_classify(&c->cls, raw, sum, c0);
+}
+
+int mc_classify_pairs(mc_ctx *c, const uint32_t *a, const uint32_t *b, uint64_t m, uint8_t *similar, double *combo0,
+                      double *sum) {
+  for (uint64_t i = 0; i < m; i++) {
+    double s, c0;
+    int d = classify(c, a[i], b[i], &s, &c0);
+    if (similar) similar[i] = (uint8_t)d;
+    if (combo0) combo0[i] = c0;
+    if (sum) sum[i] = s;
+  }
+  return MC_OK;
+}
+
+int mc_nw_identity(mc_ctx *c, const uint32_t *a, const uint32_t *b, uint64_t m, double *ident, int32_t *len,
+                   int32_t *ids) {
+#pragma omp parallel for schedule(dynamic)
+  for (uint64_t i = 0; i < m; i++) {
+    int sc, l, d;
+    double id;
+    mco_nw(c->codes.data() + c->seq_off[a[i]], (int)len_of(c, a[i]), c->codes.data() + c->seq_off[b[i]],
+           (int)len_of(c, b[i]), 1, -1, 2, 1, &sc, &l, &d, &id);
+    ident[i] = id;
+    if (len) len[i] = l;
+    if (ids) ids[i] = d;
+  }
+  return MC_OK;
+}
+
+int mc_nw_identity_raw(mc_ctx *, const uint8_t *a, const uint64_t *ao, const uint8_t *b, const uint64_t *bo,
+                       uint64_t m, double *ident, int32_t *len, int32_t *ids, int32_t *score) {
+  for (uint64_t i = 0; i < m; i++) {
+    int sc, l, d;
+    double id;
+    mco_nw(a + ao[i], (int)(ao[i + 1] - ao[i]), b + bo[i], (int)(bo[i + 1] - bo[i]), 1, -1, 2, 1, &sc, &l, &d, &id);
+    ident[i] = id;
+    if (len) len[i] = l;
+    if (ids) ids[i] = d;
+    if (score) score[i] = sc;
+  }
+  return MC_OK;
+}
+
+int mc_set_order(mc_ctx *c, const uint32_t *order, uint64_t n) {
+  c->order.assign(order, order + n);
+  c->alive.assign(n, 1);
+  return MC_OK;
+}
+int mc_kill(mc_ctx *c, uint64_t pos) {
+  c->alive[pos] = 0;
+  return MC_OK;
+}
+int mc_cluster_begin(mc_ctx *c, uint32_t first) {
+  c->members.assign(1, first);
+  return MC_OK;
+}
+
+static uint32_t mean_closest(mc_ctx *c, const std::vector<uint32_t> &mem) {
+  std::vector<double> mean(c->B, 0.0);
+  for (uint32_t id : mem) {
+    const void *r = row(c, id);
+    for (int b = 0; b < c->B; b++) {
+      double v;
+      switch (c->width) {
+        case 1: v = ((const uint8_t *)r)[b]; break;
+        case 2: v = ((const uint16_t *)r)[b]; break;
+        case 4: v = ((const uint32_t *)r)[b]; break;
+        default: v = (double)((const uint64_t *)r)[b]; break;
+      }
+      mean[b] += v;
+    }
+  }
+  double bottom = (double)mem.size();
+  for (auto &m : mean) m /= bottom;
+  uint32_t best = 0xffffffffu;
+  double bd = DBL_MAX;
+  for (uint32_t id : mem) {
+    double d = mco_distance_d(row(c, id), c->width, c->B, mean.data());
+    if (best == 0xffffffffu || d < bd) {
+      bd = d;
+      best = id;
+    }
+  }
+  return best;
+}
+
+int mc_scan(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, uint32_t *flagged, uint64_t cap, mc_scan_result *res) {
+  memset(res, 0, sizeof *res);
+  double best_val = -1;
+  bool has = false;
+  uint64_t best_pos = 0, nf = 0;
+  bool is_min = true;
+  for (uint64_t pos = S; pos <= E; pos++) {
+    if (!c->alive[pos]) continue;
+    uint32_t id = c->order[pos];
+    double s, c0;
+    int d = classify(c, id, centre, &s, &c0);
+    if (c0 > best_val) {
+      best_val = c0;
+      best_pos = pos;
+      has = true;
+    }
+    if (d) {
+      is_min = false;
+      if (nf >= cap) return fail(MC_ERR_ARG, "flag buffer too small");
+      flagged[nf++] = (uint32_t)pos;
+      c->alive[pos] = 0;
+      c->members.push_back(id);
+    }
+  }
+  res->is_min = is_min;
+  res->has_best = has;
+  res->best_pos = best_pos;
+  res->best_val = best_val;
+  res->n_flagged = nf;
+  if (!is_min) res->new_centre = mean_closest(c, c->members);
+  res->n_members = (uint32_t)c->members.size();
+  return MC_OK;
+}
+
+int mc_mean_shift(mc_ctx *c, const uint32_t *cid, uint32_t C, const uint64_t *off, const uint32_t *members, int delta,
+                  uint32_t *newc) {
+#pragma omp parallel for schedule(dynamic)
+  for (uint32_t j = 0; j < C; j++) {
+    long b = (long)j - delta < 0 ? 0 : (long)j - delta;
+    long e = (long)j + delta < (long)C - 1 ? (long)j + delta : (long)C - 1;
+    std::vector<uint32_t> good;
+    for (uint64_t q = off[b]; q < off[e + 1]; q++) {
+      double s, c0;
+      if (classify(c, members[q], cid[j], &s, &c0)) good.push_back(members[q]);
+    }
+    newc[j] = good.empty() ? cid[j] : mean_closest(c, good);
+  }
+  return MC_OK;
+}
+
+int mc_timers(mc_ctx *, double *ms, int n, int) {
+  for (int i = 0; i < n; i++) ms[i] = 0;
+  return MC_OK;
+}
+
+}  // extern "C"

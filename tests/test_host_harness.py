@@ -1,0 +1,36 @@
+"""Host restatement of the reference control flow, checked end to end on the CPU.
+
+bin/meshclust's host objects are linked against the CPU oracle engine (oracle/_build/
+meshclust_cpu; test-only) and must reproduce the reference's --threads 1 .clstr byte for
+byte on every e2e golden.  The GPU run of the real product is checked against the same
+goldens in test_gpu_parity.py.
+"""
+import gzip
+import os
+import subprocess
+
+import pytest
+
+import fixtures
+
+ROOT = fixtures.HERE.rsplit(os.sep, 1)[0]
+HARNESS = os.path.join(ROOT, "oracle", "_build", "meshclust_cpu")
+NAMES = sorted(fixtures.manifest()["e2e"])
+
+
+@pytest.fixture(scope="module")
+def harness(built):
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "harness"], check=True)
+    return HARNESS
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_e2e_byte_identical(harness, name, tmp_path):
+    fa, flags = fixtures.e2e_input(name, tmp_path)
+    out = tmp_path / (name + ".clstr")
+    r = subprocess.run([harness, fa] + flags + ["--output", str(out), "--quiet"],
+                       capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-2000:]
+    with gzip.open(fixtures.golden("e2e_%s.clstr.gz" % name), "rb") as f:
+        want = f.read()
+    assert out.read_bytes() == want
