@@ -1,0 +1,257 @@
+"""meshclust_amd -- MI355X-native engine for MeShClust's data-parallel hot path.
+
+The product is native code built in-tree by ``meshclust_amd/csrc/Makefile``:
+
+* ``lib/libmcgpu.so``      gfx950 HIP kernels behind the C-ABI of ``include/meshclust_amd.h``
+* ``lib/libmeshclust.so``  the host driver (reference control flow) + in-process C API
+* ``bin/meshclust``        drop-in CLI for the reference's ``bin/meshclust``
+
+This module is a thin ctypes view of those libraries for tests and ``bench.py``.  It never
+computes anything itself: if the libraries are missing or no GPU is present, the calls fail
+loudly (``ImportError`` / ``MCError``); there is no CPU fallback.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+LIB_DIR = os.path.join(HERE, "lib")
+BIN = os.path.join(HERE, "bin", "meshclust")
+GPU_LIB = os.path.join(LIB_DIR, "libmcgpu.so")
+HOST_LIB = os.path.join(LIB_DIR, "libmeshclust.so")
+HEADER = os.path.join(ROOT, "include", "meshclust_amd.h")
+
+FEAT_ALIGN, FEAT_LD, FEAT_MANHATTAN = 1, 2, 4
+FEAT_INTERSECTION, FEAT_PEARSON, FEAT_KULCZYNSKI2 = 16, 32, 1024
+COMBO_SQUARED, COMBO_SELF = 1, 2
+FAMILIES = ("kmer", "keys", "pairs", "scan", "finalize", "mean_shift", "nw")
+
+
+class MCError(RuntimeError):
+    pass
+
+
+def build(jobs=8):
+    """Compile libmcgpu / libmeshclust / bin/meshclust for gfx950 (hipcc cross-compiles)."""
+    subprocess.run(["make", "-s", "-j%d" % jobs, "-C", os.path.join(HERE, "csrc")], check=True)
+
+
+class Classifier(C.Structure):
+    _fields_ = [
+        ("n_single", C.c_int32),
+        ("lookup", C.c_uint16 * 8),
+        ("is_sim", C.c_int32 * 8),
+        ("mins", C.c_double * 8),
+        ("maxs", C.c_double * 8),
+        ("n_combo", C.c_int32),
+        ("combo_kind", C.c_int32 * 8),
+        ("combo_len", C.c_int32 * 8),
+        ("combo_idx", (C.c_int32 * 4) * 8),
+        ("weights", C.c_double * 9),
+    ]
+
+
+class ScanResult(C.Structure):
+    _fields_ = [
+        ("is_min", C.c_int32),
+        ("has_best", C.c_int32),
+        ("best_pos", C.c_uint64),
+        ("best_val", C.c_double),
+        ("n_flagged", C.c_uint64),
+        ("new_centre", C.c_uint32),
+        ("n_members", C.c_uint32),
+    ]
+
+
+_gpu = None
+_host = None
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p) if a is not None else None
+
+
+def gpu_lib():
+    global _gpu
+    if _gpu is None:
+        if not os.path.exists(GPU_LIB):
+            raise ImportError("libmcgpu.so not built (run meshclust_amd.build()); no CPU fallback exists")
+        lib = C.CDLL(GPU_LIB)
+        lib.mc_last_error.restype = C.c_char_p
+        lib.mc_ctx_create.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
+        lib.mc_ctx_destroy.argtypes = [C.c_void_p]
+        for name in ("mc_load_sequences", "mc_kmer_max", "mc_kmer_build", "mc_get_histograms", "mc_distance_keys",
+                     "mc_pair_features", "mc_set_classifier", "mc_classify_pairs", "mc_nw_identity",
+                     "mc_nw_identity_raw", "mc_set_order", "mc_kill", "mc_cluster_begin", "mc_scan",
+                     "mc_mean_shift", "mc_timers"):
+            getattr(lib, name).restype = C.c_int
+        _gpu = lib
+    return _gpu
+
+
+def host_lib():
+    global _host
+    if _host is None:
+        if not os.path.exists(HOST_LIB):
+            raise ImportError("libmeshclust.so not built (run meshclust_amd.build())")
+        gpu_lib()
+        lib = C.CDLL(HOST_LIB)
+        lib.mcl_parse.restype = C.c_void_p
+        lib.mcl_parse.argtypes = [C.POINTER(C.c_char_p), C.c_int, C.c_int, C.c_char_p, C.c_int]
+        lib.mcl_num_seqs.restype = C.c_uint64
+        lib.mcl_num_seqs.argtypes = [C.c_void_p]
+        lib.mcl_free.argtypes = [C.c_void_p]
+        lib.mcl_run.restype = C.c_int
+        lib.mcl_run.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_char_p), C.c_int, C.c_char_p,
+                                C.c_char_p, C.c_int]
+        _host = lib
+    return _host
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise MCError("%s failed (%d): %s" % (what, rc, gpu_lib().mc_last_error().decode()))
+
+
+class Engine:
+    """One libmcgpu context on one GPU (``mc_ctx``)."""
+
+    def __init__(self, device=0):
+        self.lib = gpu_lib()
+        self.ctx = C.c_void_p()
+        _check(self.lib.mc_ctx_create(device, C.byref(self.ctx)), "mc_ctx_create")
+        self.n = 0
+        self.width = 0
+        self.B = 0
+
+    def close(self):
+        if self.ctx:
+            self.lib.mc_ctx_destroy(self.ctx)
+            self.ctx = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def load_sequences(self, codes, seq_off, seg, seg_off):
+        codes = np.ascontiguousarray(codes, np.uint8)
+        seq_off = np.ascontiguousarray(seq_off, np.uint64)
+        seg = np.ascontiguousarray(seg, np.int32).reshape(-1)
+        seg_off = np.ascontiguousarray(seg_off, np.uint64)
+        if seg.size == 0:
+            seg = np.zeros(2, np.int32)
+        self.n = len(seq_off) - 1
+        _check(self.lib.mc_load_sequences(self.ctx, _p(codes), _p(seq_off), C.c_uint64(self.n), _p(seg),
+                                          _p(seg_off)), "mc_load_sequences")
+
+    def kmer_max(self, k):
+        out = C.c_uint64()
+        _check(self.lib.mc_kmer_max(self.ctx, k, C.byref(out)), "mc_kmer_max")
+        return out.value
+
+    def kmer_build(self, k, width):
+        _check(self.lib.mc_kmer_build(self.ctx, k, width), "mc_kmer_build")
+        self.width, self.B = width, 4 ** k
+
+    def histograms(self):
+        dt = {1: np.uint8, 2: np.uint16, 4: np.uint32, 8: np.uint64}[self.width]
+        h = np.zeros((self.n, self.B), dt)
+        m = np.zeros(self.n, np.uint64)
+        _check(self.lib.mc_get_histograms(self.ctx, _p(h), _p(m)), "mc_get_histograms")
+        return h, m
+
+    def distance_keys(self, pivots, ids):
+        pivots = np.ascontiguousarray(pivots, np.uint32)
+        ids = np.ascontiguousarray(ids, np.uint32)
+        keys = np.zeros((len(pivots), len(ids)), np.uint16)
+        _check(self.lib.mc_distance_keys(self.ctx, _p(pivots), C.c_uint32(len(pivots)), _p(ids),
+                                         C.c_uint64(len(ids)), _p(keys)), "mc_distance_keys")
+        return keys
+
+    def pair_features(self, a, b, flags):
+        a = np.ascontiguousarray(a, np.uint32)
+        b = np.ascontiguousarray(b, np.uint32)
+        fl = np.ascontiguousarray(flags, np.uint16)
+        raw = np.zeros((len(a), len(fl)), np.float64)
+        _check(self.lib.mc_pair_features(self.ctx, _p(a), _p(b), C.c_uint64(len(a)), _p(fl), len(fl), _p(raw)),
+               "mc_pair_features")
+        return raw
+
+    def set_classifier(self, cls):
+        _check(self.lib.mc_set_classifier(self.ctx, C.byref(cls)), "mc_set_classifier")
+
+    def classify_pairs(self, a, b):
+        a = np.ascontiguousarray(a, np.uint32)
+        b = np.ascontiguousarray(b, np.uint32)
+        sim = np.zeros(len(a), np.uint8)
+        c0 = np.zeros(len(a))
+        s = np.zeros(len(a))
+        _check(self.lib.mc_classify_pairs(self.ctx, _p(a), _p(b), C.c_uint64(len(a)), _p(sim), _p(c0), _p(s)),
+               "mc_classify_pairs")
+        return sim, c0, s
+
+    def nw_identity(self, a, b):
+        a = np.ascontiguousarray(a, np.uint32)
+        b = np.ascontiguousarray(b, np.uint32)
+        ident = np.zeros(len(a))
+        ln = np.zeros(len(a), np.int32)
+        ids = np.zeros(len(a), np.int32)
+        _check(self.lib.mc_nw_identity(self.ctx, _p(a), _p(b), C.c_uint64(len(a)), _p(ident), _p(ln), _p(ids)),
+               "mc_nw_identity")
+        return ident, ln, ids
+
+    def nw_identity_raw(self, a_cat, a_off, b_cat, b_off):
+        a_cat = np.ascontiguousarray(a_cat, np.uint8)
+        b_cat = np.ascontiguousarray(b_cat, np.uint8)
+        a_off = np.ascontiguousarray(a_off, np.uint64)
+        b_off = np.ascontiguousarray(b_off, np.uint64)
+        m = len(a_off) - 1
+        ident = np.zeros(m)
+        ln = np.zeros(m, np.int32)
+        ids = np.zeros(m, np.int32)
+        sc = np.zeros(m, np.int32)
+        _check(self.lib.mc_nw_identity_raw(self.ctx, _p(a_cat), _p(a_off), _p(b_cat), _p(b_off), C.c_uint64(m),
+                                           _p(ident), _p(ln), _p(ids), _p(sc)), "mc_nw_identity_raw")
+        return ident, ln, ids, sc
+
+    def timers(self, reset=False):
+        out = np.zeros(2 * len(FAMILIES))
+        _check(self.lib.mc_timers(self.ctx, _p(out), len(out), 1 if reset else 0), "mc_timers")
+        return {f: (out[2 * i], int(out[2 * i + 1])) for i, f in enumerate(FAMILIES)}
+
+
+class Dataset:
+    """Parsed FASTA held by libmeshclust (one parse, many GPU runs)."""
+
+    def __init__(self, files, threads=8):
+        self.lib = host_lib()
+        arr = (C.c_char_p * len(files))(*[f.encode() for f in files])
+        err = C.create_string_buffer(1024)
+        self.h = self.lib.mcl_parse(arr, len(files), threads, err, 1024)
+        if not self.h:
+            raise MCError("parse failed: " + err.value.decode())
+        self.n = self.lib.mcl_num_seqs(self.h)
+
+    def run(self, engine, args=(), upload=True, clstr=None):
+        """Run the full pipeline (reference options in ``args``); returns the stats dict."""
+        import json
+        argv = [b"meshclust"] + [a.encode() for a in args]
+        arr = (C.c_char_p * len(argv))(*argv)
+        buf = C.create_string_buffer(1 << 16)
+        rc = self.lib.mcl_run(self.h, engine.ctx, len(argv), arr, 1 if upload else 0,
+                              clstr.encode() if clstr else None, buf, len(buf))
+        st = json.loads(buf.value.decode() or "{}")
+        if rc != 0:
+            raise MCError("mcl_run failed (%d): %s" % (rc, st))
+        return st
+
+    def __del__(self):
+        try:
+            self.lib.mcl_free(self.h)
+        except Exception:
+            pass

@@ -1,0 +1,516 @@
+// abi.hip -- the C-ABI of include/meshclust_amd.h on top of the gfx950 kernels.
+// Every entry point is synchronous at the ABI (one HIP stream per context inside) and fails
+// loudly: there is no CPU fallback anywhere in libmcgpu.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+#include <string>
+
+#include "mcgpu.hpp"
+
+namespace mcg {
+
+static thread_local std::string g_err;
+
+void set_error(const std::string &m) { g_err = m; }
+
+int hip_fail(hipError_t e, const char *what) {
+  g_err = std::string(what) + ": " + hipGetErrorString(e);
+  return e == hipErrorOutOfMemory ? MC_ERR_OOM : MC_ERR_HIP;
+}
+
+int ensure(Buf &b, size_t bytes) {
+  if (bytes <= b.bytes) return MC_OK;
+  if (b.p) (void)hipFree(b.p);
+  b.p = nullptr;
+  b.bytes = 0;
+  size_t want = std::max<size_t>(bytes, 256);
+  if (hipMalloc(&b.p, want) != hipSuccess) {
+    g_err = "hipMalloc of " + std::to_string(want) + " bytes failed";
+    b.p = nullptr;
+    return MC_ERR_OOM;
+  }
+  b.bytes = want;
+  return MC_OK;
+}
+
+static void release(Buf &b) {
+  if (b.p) (void)hipFree(b.p);
+  b.p = nullptr;
+  b.bytes = 0;
+}
+
+static hipEvent_t pool_event(mc_ctx *c, size_t i) {
+  while (c->ev_pool.size() <= i) {
+    hipEvent_t e;
+    (void)hipEventCreate(&e);
+    c->ev_pool.push_back(e);
+  }
+  return c->ev_pool[i];
+}
+
+void timed_begin(mc_ctx *c) {
+  const int i = (int)(2 * c->ev_pending.size());
+  (void)hipEventRecord(pool_event(c, i), c->stream);
+  c->ev_open = i;
+}
+
+void timed_end(mc_ctx *c, Family f) {
+  const int i = c->ev_open;
+  (void)hipEventRecord(pool_event(c, i + 1), c->stream);
+  c->ev_pending.emplace_back((int)f, i);
+}
+
+void flush_timers(mc_ctx *c) {
+  for (auto &pr : c->ev_pending) {
+    float ms = 0;
+    (void)hipEventSynchronize(c->ev_pool[pr.second + 1]);
+    (void)hipEventElapsedTime(&ms, c->ev_pool[pr.second], c->ev_pool[pr.second + 1]);
+    c->fam_ms[pr.first] += ms;
+    c->fam_n[pr.first] += 1;
+  }
+  c->ev_pending.clear();
+}
+
+HistView hist_view(const mc_ctx *c) {
+  return HistView{(const uint8_t *)c->hist.p, (const uint64_t *)c->mag.p, (const uint64_t *)c->sumsq.p,
+                  (const uint64_t *)c->len.p, c->pitch, c->B, c->width};
+}
+
+// round(1/(1+exp(-s))) == 1 is monotone in s; find the smallest double s with that
+// outcome using the host's libm exp -- the same glibc the reference links -- so the device
+// decision `sum >= thr` equals the reference's for every sum.
+static double decision_threshold() {
+  auto pos = [](double s) { return std::round(1.0 / (1 + std::exp(-s))) == 1.0; };
+  double lo = -1e-12, hi = 0.0;  // pos(lo) false, pos(hi) true
+  if (pos(lo) || !pos(hi)) return 0.0;
+  for (int it = 0; it < 200; it++) {
+    double mid = lo / 2 + hi / 2;
+    if (mid == lo || mid == hi) break;
+    if (pos(mid)) hi = mid;
+    else lo = mid;
+  }
+  while (true) {  // hi is positive, nextafter(hi, lo) is not
+    double d = std::nextafter(hi, lo);
+    if (d == lo || !pos(d)) break;
+    hi = d;
+  }
+  return hi;
+}
+
+template <typename T>
+static int upload(Buf &b, const T *h, size_t count, hipStream_t s) {
+  if (int rc = ensure(b, count * sizeof(T) + 16)) return rc;
+  if (count) MCG_CHECK(hipMemcpyAsync(b.p, h, count * sizeof(T), hipMemcpyHostToDevice, s));
+  return MC_OK;
+}
+
+template <typename T>
+static int download(T *h, const void *d, size_t count, hipStream_t s) {
+  if (count) MCG_CHECK(hipMemcpyAsync(h, d, count * sizeof(T), hipMemcpyDeviceToHost, s));
+  return MC_OK;
+}
+
+}  // namespace mcg
+
+using namespace mcg;
+
+#define TRY(x)                  \
+  do {                          \
+    int _rc = (x);              \
+    if (_rc != MC_OK) return _rc; \
+  } while (0)
+
+extern "C" {
+
+const char *mc_last_error(void) { return mcg::g_err.c_str(); }
+int mc_abi_version(void) { return MC_ABI_VERSION; }
+
+int mc_ctx_create(int device, mc_ctx **out) {
+  if (!out) return MC_ERR_ARG;
+  int ndev = 0;
+  hipError_t e = hipGetDeviceCount(&ndev);
+  if (e != hipSuccess || ndev == 0) {
+    set_error("no HIP device available (libmcgpu requires an MI355X / gfx950 GPU)");
+    return MC_ERR_HIP;
+  }
+  if (device < 0 || device >= ndev) {
+    set_error("device index out of range");
+    return MC_ERR_ARG;
+  }
+  MCG_CHECK(hipSetDevice(device));
+  hipDeviceProp_t prop;
+  MCG_CHECK(hipGetDeviceProperties(&prop, device));
+  if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos) {
+    set_error(std::string("libmcgpu is built for gfx950, device is ") + prop.gcnArchName);
+    return MC_ERR_HIP;
+  }
+  auto *c = new mc_ctx();
+  c->device = device;
+  MCG_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  MCG_CHECK(hipEventCreate(&c->ev0));
+  MCG_CHECK(hipEventCreate(&c->ev1));
+  c->cls.thr = decision_threshold();
+  *out = c;
+  return MC_OK;
+}
+
+int mc_ctx_destroy(mc_ctx *c) {
+  if (!c) return MC_OK;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  for (Buf *b : {&c->codes, &c->seq_off, &c->seg, &c->seg_off, &c->hist, &c->mag, &c->sumsq, &c->len, &c->order,
+                 &c->alive, &c->members, &c->member_keys, &c->partials, &c->scan_dev, &c->flags_out, &c->s_a, &c->s_b,
+                 &c->s_c, &c->s_d, &c->s_e, &c->s_f, &c->s_g})
+    release(*b);
+  if (c->h_scan) (void)hipHostFree(c->h_scan);
+  for (auto e : c->ev_pool) (void)hipEventDestroy(e);
+  (void)hipEventDestroy(c->ev0);
+  (void)hipEventDestroy(c->ev1);
+  (void)hipStreamDestroy(c->stream);
+  delete c;
+  return MC_OK;
+}
+
+int mc_load_sequences(mc_ctx *c, const uint8_t *codes, const uint64_t *seq_off, uint64_t n, const int32_t *seg,
+                      const uint64_t *seg_off) {
+  if (!c || !seq_off || !seg_off || (n && !codes)) return MC_ERR_ARG;
+  MCG_CHECK(hipSetDevice(c->device));
+  c->n = n;
+  c->h_seq_off.assign(seq_off, seq_off + n + 1);
+  TRY(upload(c->codes, codes, seq_off[n], c->stream));
+  TRY(upload(c->seq_off, seq_off, n + 1, c->stream));
+  TRY(upload(c->seg, seg, 2 * seg_off[n], c->stream));
+  TRY(upload(c->seg_off, seg_off, n + 1, c->stream));
+  MCG_CHECK(hipStreamSynchronize(c->stream));
+  flush_timers(c);
+  c->k = 0;
+  return MC_OK;
+}
+
+static int kmer_common(mc_ctx *c, int k, int width, bool build, uint64_t *largest) {
+  if (!c || k < 1 || k > 7) {
+    set_error("k must be in 1..7 (4^k bins held in LDS)");
+    return MC_ERR_ARG;
+  }
+  if (c->n == 0 || !c->codes.p) {
+    set_error("no sequences loaded");
+    return MC_ERR_STATE;
+  }
+  MCG_CHECK(hipSetDevice(c->device));
+  TRY(ensure(c->s_f, 64));
+  MCG_CHECK(hipMemsetAsync(c->s_f.p, 0, 64, c->stream));
+  uint64_t *d_max = (uint64_t *)c->s_f.p;
+  int *d_err = (int *)((char *)c->s_f.p + 8);
+  if (build) {
+    c->k = k;
+    c->B = 1 << (2 * k);
+    c->width = width;
+    c->pitch = ((uint64_t)c->B * width + 15) / 16 * 16;
+    TRY(ensure(c->hist, c->n * c->pitch));
+    TRY(ensure(c->mag, c->n * 8));
+    TRY(ensure(c->sumsq, c->n * 8));
+    TRY(ensure(c->len, c->n * 8));
+  }
+  TRY(launch_kmer(c, k, width, build, d_max, d_err));
+  uint64_t h[2] = {0, 0};
+  MCG_CHECK(hipMemcpyAsync(h, c->s_f.p, 16, hipMemcpyDeviceToHost, c->stream));
+  MCG_CHECK(hipStreamSynchronize(c->stream));
+  flush_timers(c);
+  if ((int)h[1] != 0) {
+    set_error("a k-mer contains a code outside 0..3 (KmerHashTable::hash would throw InvalidInputException)");
+    return MC_ERR_INPUT;
+  }
+  if (largest) *largest = h[0];
+  return MC_OK;
+}
+
+int mc_kmer_max(mc_ctx *c, int k, uint64_t *largest) { return kmer_common(c, k, 8, false, largest); }
+
+int mc_kmer_build(mc_ctx *c, int k, int width) {
+  if (width != 1 && width != 2 && width != 4 && width != 8) return MC_ERR_ARG;
+  return kmer_common(c, k, width, true, nullptr);
+}
+
+int mc_get_histograms(mc_ctx *c, void *hist, uint64_t *mags) {
+  if (!c || c->k == 0) return MC_ERR_STATE;
+  MCG_CHECK(hipSetDevice(c->device));
+  const size_t rowb = (size_t)c->B * c->width;
+  if (hist) MCG_CHECK(hipMemcpy2DAsync(hist, rowb, c->hist.p, c->pitch, rowb, c->n, hipMemcpyDeviceToHost, c->stream));
+  if (mags) TRY(download(mags, c->mag.p, c->n, c->stream));
+  MCG_CHECK(hipStreamSynchronize(c->stream));
+  flush_timers(c);
+  return MC_OK;
+}
+
+static int check_ids(mc_ctx *c, const uint32_t *ids, uint64_t m) {
+  for (uint64_t i = 0; i < m; i++)
+    if (ids[i] >= c->n) {
+      set_error("point id out of range");
+      return MC_ERR_ARG;
+    }
+  return MC_OK;
+}
+
+int mc_distance_keys(mc_ctx *c, const uint32_t *pivots, uint32_t npiv, const uint32_t *ids, uint64_t m, uint16_t *keys) {
+  if (!c || c->k == 0) return MC_ERR_STATE;
+  MCG_CHECK(hipSetDevice(c->device));
+  TRY(check_ids(c, pivots, npiv));
+  TRY(check_ids(c, ids, m));
+  TRY(upload(c->s_a, pivots, npiv, c->stream));
+  TRY(upload(c->s_b, ids, m, c->stream));
+  TRY(ensure(c->s_c, (size_t)npiv * m * 2 + 16));
+  TRY(launch_distance_keys(c, (uint32_t *)c->s_a.p, npiv, (uint32_t *)c->s_b.p, m, (uint16_t *)c->s_c.p));
+  TRY(download(keys, c->s_c.p, (size_t)npiv * m, c->stream));
+  MCG_CHECK(hipStreamSynchronize(c->stream));
+  flush_timers(c);
+  return MC_OK;
+}
+
+int mc_pair_features(mc_ctx *c, const uint32_t *a, const uint32_t *b, uint64_t m, const uint16_t *flags, int nflag,
+                     double *raw) {
+  if (!c || c->k == 0) return MC_ERR_STATE;
+  if (nflag < 0 || nflag > 5) return MC_ERR_ARG;
+  for (int f = 0; f < nflag; f++)
+    if (flags[f] == MC_FEAT_ALIGN) {
+      set_error("mc_pair_features: ALIGN is not a k-mer feature (use mc_nw_identity)");
+      return MC_ERR_ARG;
+    }
+  MCG_CHECK(hipSetDevice(c->device));
+  TRY(check_ids(c, a, m));
+  TRY(check_ids(c, b, m));
+  TRY(upload(c->s_a, a, m, c->stream));
+  TRY(upload(c->s_b, b, m, c->stream));
+  TRY(ensure(c->s_c, m * nflag * 8 + 16));
+  TRY(launch_pairs(c, (uint32_t *)c->s_a.p, (uint32_t *)c->s_b.p, m, flags, nflag, (double *)c->s_c.p, nullptr,
+                   nullptr, nullptr, false));
+  TRY(download(raw, c->s_c.p, m * nflag, c->stream));
+  MCG_CHECK(hipStreamSynchronize(c->stream));
+  flush_timers(c);
+  return MC_OK;
+}
+
+int mc_set_classifier(mc_ctx *c, const mc_classifier *cls) {
+  if (!c || !cls) return MC_ERR_ARG;
+  if (cls->n_single < 1 || cls->n_single > MC_MAX_SINGLE || cls->n_combo < 1 || cls->n_combo > MC_MAX_COMBO)
+    return MC_ERR_ARG;
+  for (int i = 0; i < cls->n_single; i++)
+    if (cls->lookup[i] == MC_FEAT_ALIGN) {
+      set_error("alignment-feature classifiers are not supported by the k-mer kernels");
+      return MC_ERR_ARG;
+    }
+  c->cls.c = *cls;
+  c->has_cls = true;
+  return MC_OK;
+}
+
+int mc_classify_pairs(mc_ctx *c, const uint32_t *a, const uint32_t *b, uint64_t m, uint8_t *similar, double *combo0,
+                      double *sum) {
+  if (!c || c->k == 0 || !c->has_cls) return MC_ERR_STATE;
+  MCG_CHECK(hipSetDevice(c->device));
+  TRY(check_ids(c, a, m));
+  TRY(check_ids(c, b, m));
+  TRY(upload(c->s_a, a, m, c->stream));
+  TRY(upload(c->s_b, b, m, c->stream));
+  TRY(ensure(c->s_c, m * 17 + 64));
+  uint8_t *d_sim = (uint8_t *)c->s_c.p;
+  double *d_c0 = (double *)((char *)c->s_c.p + (m + 15) / 16 * 16);
+  double *d_sum = d_c0 + m;
+  TRY(launch_pairs(c, (uint32_t *)c->s_a.p, (uint32_t *)c->s_b.p, m, nullptr, 0, nullptr, d_sim, d_c0, d_sum, true));
+  if (similar) TRY(download(similar, d_sim, m, c->stream));
+  if (combo0) TRY(download(combo0, d_c0, m, c->stream));
+  if (sum) TRY(download(sum, d_sum, m, c->stream));
+  MCG_CHECK(hipStreamSynchronize(c->stream));
+  flush_timers(c);
+  return MC_OK;
+}
+
+int mc_nw_identity(mc_ctx *c, const uint32_t *a, const uint32_t *b, uint64_t m, double *ident, int32_t *len,
+                   int32_t *ids) {
+  if (!c || !c->codes.p) return MC_ERR_STATE;
+  if (m == 0) return MC_OK;
+  MCG_CHECK(hipSetDevice(c->device));
+  TRY(check_ids(c, a, m));
+  TRY(check_ids(c, b, m));
+  std::vector<uint64_t> la(m), lb(m);
+  for (uint64_t i = 0; i < m; i++) {
+    la[i] = c->h_seq_off[a[i] + 1] - c->h_seq_off[a[i]];
+    lb[i] = c->h_seq_off[b[i] + 1] - c->h_seq_off[b[i]];
+  }
+  TRY(upload(c->s_d, a, m, c->stream));
+  TRY(upload(c->s_e, b, m, c->stream));
+  TRY(ensure(c->s_f, m * 16 + 64));
+  double *d_id = (double *)c->s_f.p;
+  int32_t *d_len = (int32_t *)(d_id + m), *d_ids = d_len + m;
+  TRY(launch_nw(c, (uint8_t *)c->codes.p, (uint64_t *)c->seq_off.p, (uint32_t *)c->s_d.p, (uint8_t *)c->codes.p,
+                (uint64_t *)c->seq_off.p, (uint32_t *)c->s_e.p, m, la, lb, d_id, d_len, d_ids, nullptr));
+  TRY(download(ident, d_id, m, c->stream));
+  if (len) TRY(download(len, d_len, m, c->stream));
+  if (ids) TRY(download(ids, d_ids, m, c->stream));
+  MCG_CHECK(hipStreamSynchronize(c->stream));
+  flush_timers(c);
+  return MC_OK;
+}
+
+int mc_nw_identity_raw(mc_ctx *c, const uint8_t *a, const uint64_t *a_off, const uint8_t *b, const uint64_t *b_off,
+                       uint64_t m, double *ident, int32_t *len, int32_t *ids, int32_t *score) {
+  if (!c) return MC_ERR_ARG;
+  if (m == 0) return MC_OK;
+  MCG_CHECK(hipSetDevice(c->device));
+  std::vector<uint64_t> la(m), lb(m);
+  std::vector<uint32_t> idx(m);
+  for (uint64_t i = 0; i < m; i++) {
+    la[i] = a_off[i + 1] - a_off[i];
+    lb[i] = b_off[i + 1] - b_off[i];
+    idx[i] = (uint32_t)i;
+    if (la[i] == 0 || lb[i] == 0) {
+      set_error("empty sequence in NW pair");
+      return MC_ERR_ARG;
+    }
+  }
+  // one scratch region: A bytes | B bytes | offsets | indices | outputs
+  const size_t abytes = (a_off[m] - a_off[0] + 15) / 16 * 16, bbytes = (b_off[m] - b_off[0] + 15) / 16 * 16;
+  const size_t total = abytes + bbytes + 2 * (m + 1) * 8 + m * 4 + m * 16 + 64;
+  TRY(ensure(c->s_g, total));
+  char *base = (char *)c->s_g.p;
+  uint8_t *dA = (uint8_t *)base;
+  uint8_t *dB = dA + abytes;
+  uint64_t *dAo = (uint64_t *)(dB + bbytes), *dBo = dAo + (m + 1);
+  uint32_t *dI = (uint32_t *)(dBo + (m + 1));
+  double *dId = (double *)(((uintptr_t)(dI + m) + 15) / 16 * 16);
+  int32_t *dL = (int32_t *)(dId + m), *dIds = dL + m;
+  int32_t *dSc = nullptr;
+  TRY(ensure(c->s_f, m * 4 + 16));
+  dSc = (int32_t *)c->s_f.p;
+  std::vector<uint64_t> ao(a_off, a_off + m + 1), bo(b_off, b_off + m + 1);
+  for (auto &v : ao) v -= a_off[0];
+  for (auto &v : bo) v -= b_off[0];
+  MCG_CHECK(hipMemcpyAsync(dA, a + a_off[0], ao[m], hipMemcpyHostToDevice, c->stream));
+  MCG_CHECK(hipMemcpyAsync(dB, b + b_off[0], bo[m], hipMemcpyHostToDevice, c->stream));
+  MCG_CHECK(hipMemcpyAsync(dAo, ao.data(), (m + 1) * 8, hipMemcpyHostToDevice, c->stream));
+  MCG_CHECK(hipMemcpyAsync(dBo, bo.data(), (m + 1) * 8, hipMemcpyHostToDevice, c->stream));
+  MCG_CHECK(hipMemcpyAsync(dI, idx.data(), m * 4, hipMemcpyHostToDevice, c->stream));
+  TRY(launch_nw(c, dA, dAo, dI, dB, dBo, dI, m, la, lb, dId, dL, dIds, dSc));
+  TRY(download(ident, dId, m, c->stream));
+  if (len) TRY(download(len, dL, m, c->stream));
+  if (ids) TRY(download(ids, dIds, m, c->stream));
+  if (score) TRY(download(score, dSc, m, c->stream));
+  MCG_CHECK(hipStreamSynchronize(c->stream));
+  flush_timers(c);
+  return MC_OK;
+}
+
+static const size_t kFlagPrefix = 4096;  // flagged positions copied back with the result
+
+int mc_set_order(mc_ctx *c, const uint32_t *order, uint64_t n) {
+  if (!c || !order || n != c->n) return MC_ERR_ARG;
+  MCG_CHECK(hipSetDevice(c->device));
+  TRY(check_ids(c, order, n));
+  c->norder = n;
+  TRY(upload(c->order, order, n, c->stream));
+  TRY(ensure(c->alive, n + 16));
+  MCG_CHECK(hipMemsetAsync(c->alive.p, 1, n, c->stream));
+  TRY(ensure(c->members, (n + 1) * 4));
+  TRY(ensure(c->member_keys, (n + 1) * 8));
+  TRY(ensure(c->partials, 4096 * sizeof(ScanPartial)));
+  TRY(ensure(c->scan_dev, sizeof(ScanDev) + std::max<uint64_t>(n + 1, kFlagPrefix) * 4));
+  if (!c->h_scan) {
+    c->h_scan_cap = sizeof(ScanDev) + kFlagPrefix * 4;
+    MCG_CHECK(hipHostMalloc((void **)&c->h_scan, c->h_scan_cap, hipHostMallocDefault));
+  }
+  MCG_CHECK(hipMemsetAsync(c->scan_dev.p, 0, sizeof(ScanDev), c->stream));
+  MCG_CHECK(hipStreamSynchronize(c->stream));
+  flush_timers(c);
+  c->step = 0;
+  return MC_OK;
+}
+
+int mc_kill(mc_ctx *c, uint64_t pos) {
+  if (!c || pos >= c->norder) return MC_ERR_ARG;
+  MCG_CHECK(hipMemsetAsync((uint8_t *)c->alive.p + pos, 0, 1, c->stream));
+  return MC_OK;
+}
+
+int mc_cluster_begin(mc_ctx *c, uint32_t first) {
+  if (!c || first >= c->n || c->norder == 0) return MC_ERR_ARG;
+  ScanDev sd;
+  memset(&sd, 0, sizeof sd);
+  sd.nmembers = 1;
+  // members[0] = first with tie-break key 0 (it is `current`'s first element)
+  static thread_local uint64_t zero = 0;
+  MCG_CHECK(hipMemcpyAsync(c->members.p, &first, 4, hipMemcpyHostToDevice, c->stream));
+  MCG_CHECK(hipMemcpyAsync(c->member_keys.p, &zero, 8, hipMemcpyHostToDevice, c->stream));
+  MCG_CHECK(hipMemcpyAsync(c->scan_dev.p, &sd, sizeof sd, hipMemcpyHostToDevice, c->stream));
+  MCG_CHECK(hipStreamSynchronize(c->stream));
+  flush_timers(c);
+  return MC_OK;
+}
+
+int mc_scan(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, uint32_t *flagged_pos, uint64_t cap,
+            mc_scan_result *res) {
+  if (!c || !res || !c->has_cls || c->norder == 0) return MC_ERR_STATE;
+  if (S > E || E >= c->norder || centre >= c->n) return MC_ERR_ARG;
+  c->step++;
+  int nblocks = 0;
+  TRY(launch_scan(c, centre, S, E, &nblocks));
+  TRY(launch_finalize(c, nblocks));
+  MCG_CHECK(hipMemcpyAsync(c->h_scan, c->scan_dev.p, c->h_scan_cap, hipMemcpyDeviceToHost, c->stream));
+  MCG_CHECK(hipStreamSynchronize(c->stream));
+  flush_timers(c);
+  *res = c->h_scan->r;
+  const uint64_t nf = res->n_flagged;
+  if (nf > cap) {
+    set_error("flagged buffer too small");
+    return MC_ERR_ARG;
+  }
+  const uint32_t *hf = (const uint32_t *)((char *)c->h_scan + sizeof(ScanDev));
+  const uint64_t first = std::min<uint64_t>(nf, kFlagPrefix);
+  memcpy(flagged_pos, hf, first * 4);
+  if (nf > first) {
+    MCG_CHECK(hipMemcpyAsync(flagged_pos + first, (char *)c->scan_dev.p + sizeof(ScanDev) + first * 4, (nf - first) * 4,
+                             hipMemcpyDeviceToHost, c->stream));
+    MCG_CHECK(hipStreamSynchronize(c->stream));
+  flush_timers(c);
+  }
+  std::sort(flagged_pos, flagged_pos + nf);
+  return MC_OK;
+}
+
+int mc_mean_shift(mc_ctx *c, const uint32_t *centre_ids, uint32_t C, const uint64_t *member_off, const uint32_t *members,
+                  int delta, uint32_t *new_centre) {
+  if (!c || !c->has_cls || delta < 0) return MC_ERR_STATE;
+  if (C == 0) return MC_OK;
+  MCG_CHECK(hipSetDevice(c->device));
+  TRY(check_ids(c, centre_ids, C));
+  const uint64_t nm = member_off[C];
+  TRY(check_ids(c, members, nm));
+  TRY(upload(c->s_a, centre_ids, C, c->stream));
+  TRY(upload(c->s_b, member_off, C + 1, c->stream));
+  TRY(upload(c->s_c, members, nm, c->stream));
+  // output goes to the tail of s_a
+  TRY(ensure(c->flags_out, (size_t)C * 4 + 16));
+  TRY(launch_mean_shift(c, (uint32_t *)c->s_a.p, C, (uint64_t *)c->s_b.p, member_off, (uint32_t *)c->s_c.p, delta,
+                        (uint32_t *)c->flags_out.p));
+  TRY(download(new_centre, c->flags_out.p, C, c->stream));
+  MCG_CHECK(hipStreamSynchronize(c->stream));
+  flush_timers(c);
+  return MC_OK;
+}
+
+int mc_timers(mc_ctx *c, double *ms_out, int n, int reset) {
+  if (!c) return MC_ERR_ARG;
+  (void)hipStreamSynchronize(c->stream);
+  flush_timers(c);
+  for (int f = 0; f < F_NFAM && 2 * f + 1 < n; f++) {
+    ms_out[2 * f] = c->fam_ms[f];
+    ms_out[2 * f + 1] = c->fam_n[f];
+  }
+  if (reset)
+    for (int f = 0; f < F_NFAM; f++) c->fam_ms[f] = c->fam_n[f] = 0;
+  return MC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,253 @@
+// features.hpp -- device-side K2 math: per-pair integer statistics of two k-mer histograms,
+// the raw similarity features of src/cluster/src/Feature.cpp and the GLM decision of
+// Trainer::get_close/filter/merge, all bit-exact with the reference build.
+//
+// For 8- and 16-bit histograms every feature is a function of four integer sums, computed
+// with packed byte instructions (v_sad_u8: sum |p-q| of 4 bytes, v_dot4_u32_u8: sum p*q):
+//   Smin = sum min(p,q) = (mag_p + mag_q - Sabs) / 2          intersection, kulczynski2, distance
+//   Sabs = sum |p-q|                                          manhattan
+//   Sdot = sum p*q, with per-point sum p^2 precomputed        pearson:
+//     sum (p-ap)(q-aq) = Sdot - aq*mag_p - ap*mag_q + B*ap*aq  (exact int64 identity)
+// 32/64-bit histograms fall back to a per-bin loop that mirrors the reference's C++ types
+// including its unsigned wrap-arounds (raw_exact).
+#pragma once
+#include "mcgpu.hpp"
+
+namespace mcg {
+
+struct PS {  // pair statistics
+  uint64_t smin, sabs, sdot;
+};
+
+struct PInfo {
+  uint64_t mag, sumsq, len;
+};
+
+template <typename T>
+struct Acc;
+
+template <>
+struct Acc<uint8_t> {
+  uint32_t sad = 0, dot = 0;
+  __device__ __forceinline__ void add(const uint4 &a, const uint4 &b) {
+    sad = __builtin_amdgcn_sad_u8(a.x, b.x, sad);
+    sad = __builtin_amdgcn_sad_u8(a.y, b.y, sad);
+    sad = __builtin_amdgcn_sad_u8(a.z, b.z, sad);
+    sad = __builtin_amdgcn_sad_u8(a.w, b.w, sad);
+    dot = __builtin_amdgcn_udot4(a.x, b.x, dot, false);
+    dot = __builtin_amdgcn_udot4(a.y, b.y, dot, false);
+    dot = __builtin_amdgcn_udot4(a.z, b.z, dot, false);
+    dot = __builtin_amdgcn_udot4(a.w, b.w, dot, false);
+  }
+  __device__ __forceinline__ void reduce16() {
+#pragma unroll
+    for (int o = 8; o >= 1; o >>= 1) {
+      sad += __shfl_xor(sad, o, 64);
+      dot += __shfl_xor(dot, o, 64);
+    }
+  }
+  __device__ __forceinline__ PS finish(uint64_t magp, uint64_t magq) const {
+    PS s;
+    s.sabs = sad;
+    s.smin = (magp + magq - sad) >> 1;
+    s.sdot = dot;
+    return s;
+  }
+};
+
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int o) {
+  uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+  lo = __shfl_xor(lo, o, 64);
+  hi = __shfl_xor(hi, o, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
+  uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+  lo = __shfl(lo, src, 64);
+  hi = __shfl(hi, src, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// Generic element accumulator (16/32/64-bit bins): Smin, Sabs (mod 2^32 like `int sum`), Sdot.
+template <typename T>
+struct Acc {
+  uint64_t smin = 0, sabs = 0, sdot = 0;
+  __device__ __forceinline__ void add(const uint4 &a, const uint4 &b) {
+    const T *pa = reinterpret_cast<const T *>(&a);
+    const T *pb = reinterpret_cast<const T *>(&b);
+#pragma unroll
+    for (int i = 0; i < (int)(16 / sizeof(T)); i++) {
+      uint64_t x = pa[i], y = pb[i];
+      smin += x < y ? x : y;
+      sabs += (uint32_t)(x > y ? x - y : y - x);
+      sdot += x * y;
+    }
+  }
+  __device__ __forceinline__ void reduce16() {
+#pragma unroll
+    for (int o = 8; o >= 1; o >>= 1) {
+      smin += shfl_xor64(smin, o);
+      sabs += shfl_xor64(sabs, o);
+      sdot += shfl_xor64(sdot, o);
+    }
+  }
+  __device__ __forceinline__ PS finish(uint64_t, uint64_t) const { return PS{smin, sabs, sdot}; }
+};
+
+// DivergencePoint::distance (DivergencePoint.cpp:68-81): trunc_u64(fma(-f,f,1)*1e4)
+__device__ __forceinline__ uint64_t distance_key(uint64_t smin, uint64_t magp, uint64_t magq) {
+  uint64_t dist = smin * 2;
+  double frac = (double)dist / (double)(magp + magq);
+  return (uint64_t)(__builtin_fma(-frac, frac, 1.0) * 10000.0);
+}
+
+// Feature.cpp:273-294 via the integer identity (8/16-bit bins: dp = p - ap is exact int math).
+__device__ __forceinline__ double pearson_fast(const PS &s, const PInfo &p, const PInfo &q, int B) {
+  double dap = (double)p.mag / B, daq = (double)q.mag / B;
+  int64_t ap = (int)round(dap), aq = (int)round(daq);
+  int64_t mp = (int64_t)p.mag, mq = (int64_t)q.mag, b = B;
+  int64_t dot = (int64_t)s.sdot - aq * mp - ap * mq + b * ap * aq;
+  int64_t np = (int64_t)p.sumsq - 2 * ap * mp + b * ap * ap;
+  int64_t nq = (int64_t)q.sumsq - 2 * aq * mq + b * aq * aq;
+  double prod = (double)(int64_t)((uint64_t)np * (uint64_t)nq);
+  return (double)dot / sqrt(0.5 < prod ? prod : 0.5);
+}
+
+__device__ __forceinline__ double raw_fast(uint16_t f, const PS &s, const PInfo &p, const PInfo &q, int B) {
+  switch (f) {
+    case MC_FEAT_LD: return (double)(p.len > q.len ? p.len - q.len : q.len - p.len);
+    case MC_FEAT_MANHATTAN: return (double)(int32_t)(uint32_t)s.sabs;
+    case MC_FEAT_INTERSECTION: return (double)(s.smin * 2) / (double)(p.mag + q.mag);
+    case MC_FEAT_PEARSON: return pearson_fast(s, p, q, B);
+    case MC_FEAT_KULCZYNSKI2: {
+      double ap = (double)p.mag / B, aq = (double)q.mag / B;
+      double coeff = ((double)B * (ap + aq)) / ((2.0 * ap) * aq);
+      return coeff * (double)s.smin;
+    }
+    default: return __builtin_nan("");
+  }
+}
+
+// Per-bin restatement for 32/64-bit bins (mirrors oracle mco_raw / Feature.cpp exactly).
+template <typename T>
+__device__ double raw_exact(uint16_t f, const T *p, const T *q, int B, const PInfo &pi, const PInfo &qi) {
+  if (f == MC_FEAT_LD) return (double)(pi.len > qi.len ? pi.len - qi.len : qi.len - pi.len);
+  if (f == MC_FEAT_MANHATTAN) {
+    uint32_t sum = 0;
+    for (int i = 0; i < B; i++) sum += (uint32_t)(p[i] > q[i] ? p[i] - q[i] : q[i] - p[i]);
+    return (double)(int32_t)sum;
+  }
+  if (f == MC_FEAT_INTERSECTION || f == MC_FEAT_KULCZYNSKI2) {
+    uint64_t d = 0, ms = 0;
+    for (int i = 0; i < B; i++) {
+      T m = p[i] < q[i] ? p[i] : q[i];
+      d += (uint64_t)(T)(m * 2);  // `2 * std::min` in T (unsigned wrap for 32/64-bit T)
+      ms += m;
+    }
+    if (f == MC_FEAT_INTERSECTION) return (double)d / (double)(pi.mag + qi.mag);
+    double ap = (double)pi.mag / B, aq = (double)qi.mag / B;
+    double coeff = ((double)B * (ap + aq)) / ((2.0 * ap) * aq);
+    return coeff * (double)ms;
+  }
+  if (f == MC_FEAT_PEARSON) {
+    double dap = (double)pi.mag / B, daq = (double)qi.mag / B;
+    int ap = (int)round(dap), aq = (int)round(daq);
+    uint64_t dot = 0, np = 0, nq = 0;
+    for (int i = 0; i < B; i++) {
+      int64_t dp, dq;
+      if (sizeof(T) == 4) {
+        dp = (int64_t)(uint64_t)(uint32_t)((uint32_t)p[i] - (uint32_t)ap);
+        dq = (int64_t)(uint64_t)(uint32_t)((uint32_t)q[i] - (uint32_t)aq);
+      } else {
+        dp = (int64_t)((uint64_t)p[i] - (uint64_t)(int64_t)ap);
+        dq = (int64_t)((uint64_t)q[i] - (uint64_t)(int64_t)aq);
+      }
+      np += (uint64_t)dp * (uint64_t)dp;
+      nq += (uint64_t)dq * (uint64_t)dq;
+      dot += (uint64_t)dp * (uint64_t)dq;
+    }
+    double prod = (double)(int64_t)(np * nq);
+    return (double)(int64_t)dot / sqrt(0.5 < prod ? prod : 0.5);
+  }
+  return __builtin_nan("");
+}
+
+__device__ __forceinline__ double pick8(const double (&v)[MC_MAX_SINGLE], int idx) {
+  double r = 0;
+#pragma unroll
+  for (int i = 0; i < MC_MAX_SINGLE; i++) r = (idx == i) ? v[i] : r;
+  return r;
+}
+
+// normalize_cache (Feature.cpp:41-52) + operator() (Feature.h:69-88) + the fma GLM sum of
+// Trainer.cpp:84-95.  Returns the decision round(1/(1+exp(-sum))) == 1 as sum >= thr.
+__device__ __forceinline__ int classify_raw(const DevClassifier &C, double (&raw)[MC_MAX_SINGLE], double *c0,
+                                            double *sum_out) {
+  const mc_classifier &c = C.c;
+#pragma unroll
+  for (int i = 0; i < MC_MAX_SINGLE; i++) {
+    if (i < c.n_single) {
+      double val = (raw[i] - c.mins[i]) / (c.maxs[i] - c.mins[i]);
+      raw[i] = c.is_sim[i] ? val : 1 - val;
+    }
+  }
+  double sum = c.weights[0];
+  double first = 0;
+  for (int col = 0; col < c.n_combo; col++) {
+    double prod = 1;
+    for (int j = 0; j < c.combo_len[col]; j++) {
+      double v = pick8(raw, c.combo_idx[col][j]);
+      if (c.combo_kind[col] == MC_COMBO_SELF) prod *= v;
+      else prod *= v * v;
+    }
+    if (col == 0) first = prod;
+    sum = __builtin_fma(c.weights[col + 1], prod, sum);
+  }
+  *c0 = first;
+  if (sum_out) *sum_out = sum;
+  return sum >= C.thr;
+}
+
+template <typename T>
+__device__ __forceinline__ uint4 ld16(const uint8_t *row, int ch) {
+  return reinterpret_cast<const uint4 *>(row)[ch];
+}
+
+// Integer pair statistics for the 64 candidates of one wave, 16 lanes per histogram row so
+// every load instruction reads four whole 256-byte rows (1 KiB) contiguously.  Lane l ends up
+// with the statistics of the pair it owns (my_a vs my_b, or my_a vs the LDS-resident centre).
+template <typename T>
+__device__ __forceinline__ PS wave_pair_stats(const HistView &H, uint32_t my_a, uint32_t my_b, bool valid,
+                                              const uint4 *centre_lds, uint64_t centre_mag) {
+  const int lane = threadIdx.x & 63, group = lane >> 4, lig = lane & 15;
+  const int nch = (int)((H.B * (int)sizeof(T) + 15) / 16);
+  PS mine{0, 0, 0};
+  for (int pass = 0; pass < 16; pass++) {
+    const int cl = pass * 4 + group;
+    uint32_t a = __shfl(my_a, cl, 64);
+    uint32_t b = __shfl(my_b, cl, 64);
+    int v = __shfl((int)valid, cl, 64);
+    Acc<T> acc;
+    if (v) {
+      const uint8_t *ra = H.hist + (uint64_t)a * H.pitch;
+      if (centre_lds) {
+        for (int ch = lig; ch < nch; ch += 16) acc.add(ld16<T>(ra, ch), centre_lds[ch]);
+      } else {
+        const uint8_t *rb = H.hist + (uint64_t)b * H.pitch;
+        for (int ch = lig; ch < nch; ch += 16) acc.add(ld16<T>(ra, ch), ld16<T>(rb, ch));
+      }
+    }
+    acc.reduce16();
+    uint64_t ma = v ? H.mag[a] : 0;
+    uint64_t mb = centre_lds ? centre_mag : (v ? H.mag[b] : 0);
+    PS s = acc.finish(ma, mb);
+    // lane l takes the result of pass l/4 from the leader of group l%4
+    const int src = (lane & 3) * 16;
+    uint64_t x0 = shfl64(s.smin, src), x1 = shfl64(s.sabs, src), x2 = shfl64(s.sdot, src);
+    if (pass == (lane >> 2)) mine = PS{x0, x1, x2};
+  }
+  return mine;
+}
+
+}  // namespace mcg

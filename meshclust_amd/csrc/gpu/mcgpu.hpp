@@ -1,0 +1,128 @@
+// mcgpu.hpp -- internal header of libmcgpu (MI355X / gfx950 engine behind include/meshclust_amd.h).
+//
+// Data layout in HBM (one context = one GPU):
+//   codes      n sequences' one-digit bytes, concatenated (the NW input, Point::get_data_str)
+//   seq_off    byte offsets (n+1), seg/seg_off: k-mer segments per sequence
+//   hist       n rows of B = 4^k bins of width w bytes, id order, row pitch 16-byte aligned
+//   mag/sumsq  per row: sum of bins (pseudo magnitude) and sum of squared bins
+//   len        per row: sequence length (incl. N) for the length-difference feature
+//   order/alive  static bvec order (position -> id) and the alive mask of accumulation
+//   members    the growing cluster of the current accumulation (ids + tie-break keys)
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../../include/meshclust_amd.h"
+
+namespace mcg {
+
+// Kernel families for the device timers (mc_timers): ms and launch count per family.
+enum Family { F_KMER = 0, F_KEYS, F_PAIRS, F_SCAN, F_FINAL, F_MSHIFT, F_NW, F_NFAM };
+
+// Classifier in the form the kernels consume (mc_classifier + the exact decision threshold).
+struct DevClassifier {
+  mc_classifier c;
+  double thr;  // round(1/(1+exp(-sum))) == 1  <=>  sum >= thr   (host glibc exp, see abi.hip)
+};
+
+// Read-only view of the device histogram matrix passed to kernels by value.
+struct HistView {
+  const uint8_t *hist;
+  const uint64_t *mag;
+  const uint64_t *sumsq;
+  const uint64_t *len;
+  uint64_t pitch;  // bytes per row
+  int B;           // bins
+  int width;       // bytes per bin
+};
+
+struct ScanPartial {
+  double val;
+  uint64_t pos;
+  int32_t has;
+  int32_t pad;
+};
+
+// Device-side result record of one accumulation step (mirrors mc_scan_result).
+struct ScanDev {
+  mc_scan_result r;
+  uint32_t nflag;     // atomic counter of flagged candidates this step
+  uint32_t nmembers;  // members in the current cluster
+};
+
+struct Buf {
+  void *p = nullptr;
+  size_t bytes = 0;
+};
+
+}  // namespace mcg
+
+struct mc_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  // sequences
+  uint64_t n = 0;
+  std::vector<uint64_t> h_seq_off;
+  mcg::Buf codes, seq_off, seg, seg_off;
+  // histograms
+  int k = 0, B = 0, width = 0;
+  uint64_t pitch = 0;
+  mcg::Buf hist, mag, sumsq, len;
+  // classifier
+  mcg::DevClassifier cls{};
+  bool has_cls = false;
+  // accumulation state
+  uint64_t norder = 0;
+  mcg::Buf order, alive, members, member_keys, partials, scan_dev, flags_out;
+  uint32_t step = 0;
+  mcg::ScanDev *h_scan = nullptr;  // pinned mirror of scan_dev + flagged prefix
+  size_t h_scan_cap = 0;
+  // scratch
+  mcg::Buf s_a, s_b, s_c, s_d, s_e, s_f, s_g;
+  std::vector<void *> pinned;
+  // timers: event pairs recorded around kernels, resolved lazily after the next stream sync
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  std::vector<hipEvent_t> ev_pool;
+  std::vector<std::pair<int, int>> ev_pending;  // (family, pool index of the begin event)
+  int ev_open = -1;
+  double fam_ms[mcg::F_NFAM] = {0};
+  double fam_n[mcg::F_NFAM] = {0};
+};
+
+namespace mcg {
+
+void set_error(const std::string &m);
+int hip_fail(hipError_t e, const char *what);
+int ensure(Buf &b, size_t bytes);  // grow-only device buffer
+void timed_begin(mc_ctx *c);
+void timed_end(mc_ctx *c, Family f);
+void flush_timers(mc_ctx *c);  // after a stream synchronisation
+
+HistView hist_view(const mc_ctx *c);
+
+// ---- launchers (defined in kmer.hip, k2.hip, nw.hip) -------------------------------------
+int launch_kmer(mc_ctx *c, int k, int width, bool build, uint64_t *d_max, int *d_err);
+int launch_distance_keys(mc_ctx *c, const uint32_t *d_piv, uint32_t npiv, const uint32_t *d_ids, uint64_t m,
+                         uint16_t *d_keys);
+int launch_pairs(mc_ctx *c, const uint32_t *d_a, const uint32_t *d_b, uint64_t m, const uint16_t *flags, int nflag,
+                 double *d_raw, uint8_t *d_sim, double *d_c0, double *d_sum, bool classify);
+int launch_scan(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, int *nblocks);
+int launch_finalize(mc_ctx *c, int nblocks);
+int launch_mean_shift(mc_ctx *c, const uint32_t *d_cid, uint32_t C, const uint64_t *d_off, const uint64_t *h_off,
+                      const uint32_t *d_mem, int delta, uint32_t *d_new);
+// NW on byte strings: pair p aligns A[aoff[ai[p]] .. aoff[ai[p]+1]) against B[...] (rows = A).
+int launch_nw(mc_ctx *c, const uint8_t *d_A, const uint64_t *d_aoff, const uint32_t *d_ai, const uint8_t *d_B,
+              const uint64_t *d_boff, const uint32_t *d_bi, uint64_t m, const std::vector<uint64_t> &h_alen,
+              const std::vector<uint64_t> &h_blen, double *d_ident, int32_t *d_len, int32_t *d_ids,
+              int32_t *d_score);
+
+}  // namespace mcg
+
+#define MCG_CHECK(expr)                                   \
+  do {                                                    \
+    hipError_t _e = (expr);                               \
+    if (_e != hipSuccess) return mcg::hip_fail(_e, #expr); \
+  } while (0)

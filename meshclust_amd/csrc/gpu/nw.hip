@@ -1,0 +1,338 @@
+// nw.hip -- K3: batched global alignment identity, bit-exact with utility::GlobAlignE
+// (src/utility/GlobAlignE.cpp:123-305; Gotoh affine gaps, match 1 / mismatch -1 / open 2 /
+// extend 1, each DP state carrying (score, path length, identities)).
+//
+// One wavefront per pair, anti-diagonal wavefront over the DP matrix: lane l owns R
+// consecutive rows of seq1 and sweeps the columns of seq2 one step behind lane l-1, so at
+// step t it computes column t-l+1 for its R rows.  The bottom row of lane l-1 (M, X, Y and
+// their payloads) and the seq2 code travel down the wave through one shuffle per value and
+// step; nothing but that hand-off leaves registers.  Length and identity count of a state
+// are packed into one payload word (len << 16 | ids, or 32/32 bits for long pairs), so a
+// predecessor choice moves both with one select.  Sequences longer than 64*R rows are cut
+// into row blocks whose boundary row is kept in global scratch.
+//
+// Recurrences (rows i over seq1, columns j over seq2; GlobAlignE's names in brackets):
+//   Y(i,j) [upperGap] = max(M(i,j-1) - (o+e), Y(i,j-1) - e)          ties: from M
+//   M(i,j) [matches]  = max(M, X, Y at (i-1,j-1)) + s(i,j)           ties: M, then X, then Y
+//   X(i,j) [lowerGap] = max(M(i-1,j) - (o+e), X(i-1,j) - e)          ties: from M
+// with the reference's finite "-infinity" and boundary rows/columns (:125-170, :250-256).
+#include "mcgpu.hpp"
+
+namespace mcg {
+
+namespace {
+
+constexpr int GO = 2, GE = 1, MATCH = 1, MISMATCH = -1;
+
+template <typename P>
+struct Pack;
+template <>
+struct Pack<uint32_t> {
+  static constexpr int SH = 16;
+};
+template <>
+struct Pack<uint64_t> {
+  static constexpr int SH = 32;
+};
+
+template <typename P>
+__device__ __forceinline__ P shup(P v) {
+  if constexpr (sizeof(P) == 4) {
+    return (P)__shfl_up((int)v, 1, 64);
+  } else {
+    uint32_t lo = __shfl_up((int)(uint32_t)v, 1, 64), hi = __shfl_up((int)(uint32_t)(v >> 32), 1, 64);
+    return ((uint64_t)hi << 32) | lo;
+  }
+}
+
+struct NWPairs {
+  const uint8_t *A;
+  const uint64_t *aoff;
+  const uint32_t *ai;
+  const uint8_t *Bq;
+  const uint64_t *boff;
+  const uint32_t *bi;
+  const uint32_t *pidx;   // pair indices handled by this launch
+  uint32_t npairs;
+  int *bnd;               // boundary scratch (multi-block pairs)
+  const uint64_t *bnd_off;  // per launch-slot offset into bnd (in ints)
+  double *ident;
+  int32_t *len;
+  int32_t *ids;
+  int32_t *score;
+};
+
+template <int R, typename P>
+__global__ __launch_bounds__(64) void nw_kernel(NWPairs q) {
+  constexpr int SH = Pack<P>::SH;
+  constexpr P LEN1 = (P)1 << SH;
+  const uint32_t slot = blockIdx.x;
+  if (slot >= q.npairs) return;
+  const uint32_t p = q.pidx[slot];
+  const uint8_t *a = q.A + q.aoff[q.ai[p]];
+  const int la = (int)(q.aoff[q.ai[p] + 1] - q.aoff[q.ai[p]]);
+  const uint8_t *b = q.Bq + q.boff[q.bi[p]];
+  const int lb = (int)(q.boff[q.bi[p] + 1] - q.boff[q.bi[p]]);
+  const int lane = threadIdx.x;
+  const int len1 = la + 1, len2 = lb + 1;
+  const int shorter = (len2 < len1 ? len2 : len1) - 1;
+  const int lenDiff = len2 > len1 ? len2 - len1 : len1 - len2;
+  int maxDiff = 0;
+  if (lenDiff >= 1) maxDiff += -GO - lenDiff * GE;
+  maxDiff += MISMATCH * shorter - 1;
+  const int NINF = maxDiff;
+  int *bnd = q.bnd ? q.bnd + q.bnd_off[slot] : nullptr;  // 6 ints per column, columns 0..lb
+  const int nblk = (la + 64 * R - 1) / (64 * R);
+  int fin_score = 0;
+  P fin_pay = 0;
+  for (int blk = 0; blk < (nblk > 0 ? nblk : 1); blk++) {
+    const int itop = blk * 64 * R + lane * R + 1;  // first row of this lane
+    uint8_t ac[R];
+    int M[R], X[R], Y[R];
+    P MP[R], XP[R], YP[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      const int i = itop + r;
+      ac[r] = i <= la ? a[i - 1] : (uint8_t)0xFF;
+      // column 0 (GlobAlignE.cpp:140-160): M = Y = -inf, X = -o - i*e, lengths i
+      M[r] = NINF;
+      Y[r] = NINF;
+      X[r] = -GO - i * GE;
+      MP[r] = XP[r] = YP[r] = (P)i << SH;
+    }
+    // diagonal input for column 1: row itop-1 at column 0
+    int dM, dX, dY;
+    P dMP, dXP, dYP;
+    {
+      const int i = itop - 1;
+      if (i == 0) {  // matches[0]=0, lowerGap[0]=-inf, upperGapLag at j=1 = -o
+        dM = 0;
+        dX = NINF;
+        dY = -GO;
+        dMP = dXP = dYP = 0;
+      } else {
+        dM = NINF;
+        dX = -GO - i * GE;
+        dY = NINF;
+        dMP = dXP = dYP = (P)i << SH;
+      }
+    }
+    int oM = NINF, oX = NINF, oY = NINF;  // this lane's bottom row, last computed column
+    P oMP = 0, oXP = 0, oYP = 0;
+    uint8_t ob = 0;
+    const int steps = lb + 63;
+    for (int t = 0; t < steps; t++) {
+      const int j = t - lane + 1;  // column of this lane at this step
+      // hand-off from lane-1: its bottom row at column j (computed at step t-1) + seq2 code
+      int uM = shup<int>(oM), uX = shup<int>(oX), uY = shup<int>(oY);
+      P uMP = shup<P>(oMP), uXP = shup<P>(oXP), uYP = shup<P>(oYP);
+      uint8_t bc = (uint8_t)__shfl_up((int)ob, 1, 64);
+      if (lane == 0) {
+        bc = (j >= 1 && j <= lb) ? b[j - 1] : 0;
+        if (blk == 0) {  // row 0 at column j: M = X = -inf, Y = -o - j*e, lengths j
+          uM = NINF;
+          uX = NINF;
+          uY = -GO - j * GE;
+          uMP = uXP = uYP = (P)j << SH;
+        } else if (j >= 1 && j <= lb) {
+          const int *s = bnd + 6 * j;
+          uM = s[0];
+          uX = s[1];
+          uY = s[2];
+          uMP = (P)(uint32_t)s[3];
+          uXP = (P)(uint32_t)s[4];
+          uYP = (P)(uint32_t)s[5];
+          if constexpr (sizeof(P) == 8) {
+            // long pairs keep 64-bit payloads in two boundary records
+            const int *s2 = bnd + 6 * (lb + 1) + 6 * j;
+            uMP |= (P)(uint32_t)s2[3] << 32;
+            uXP |= (P)(uint32_t)s2[4] << 32;
+            uYP |= (P)(uint32_t)s2[5] << 32;
+          }
+        }
+      }
+      if (j >= 1 && j <= lb) {
+        // above (row itop-1, column j) = u*, diagonal (row itop-1, column j-1) = d*
+        int aM = uM, aX = uX;
+        P aMP = uMP, aXP = uXP;
+        int gM = dM, gX = dX, gY = dY;
+        P gMP = dMP, gXP = dXP, gYP = dYP;
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+          const int pM = M[r], pX = X[r], pY = Y[r];  // (i, j-1): this row's previous column
+          const P pMP = MP[r], pXP = XP[r], pYP = YP[r];
+          // upperGap (GlobAlignE.cpp:233-251)
+          const int yb = pM - (GO + GE), yc = pY - GE;
+          const bool yFromM = yb >= yc;
+          Y[r] = yFromM ? yb : yc;
+          YP[r] = (yFromM ? pMP : pYP) + LEN1;
+          // matches (:255-299)
+          const bool hit = ac[r] == bc;
+          const int s = hit ? MATCH : MISMATCH;
+          const bool fromM = gM >= gX && gM >= gY;
+          const bool fromX = !fromM && gX >= gY;
+          const int best = fromM ? gM : (fromX ? gX : gY);
+          const P bestP = fromM ? gMP : (fromX ? gXP : gYP);
+          M[r] = best + s;
+          MP[r] = bestP + LEN1 + (hit ? (P)1 : (P)0);
+          // lowerGap (:316-330), from the row above in this column
+          const int xb = aM - (GO + GE), xc = aX - GE;
+          const bool xFromM = xb >= xc;
+          X[r] = xFromM ? xb : xc;
+          XP[r] = (xFromM ? aMP : aXP) + LEN1;
+          // next row: above = this row's new values, diagonal = this row's old values
+          aM = M[r];
+          aX = X[r];
+          aMP = MP[r];
+          aXP = XP[r];
+          gM = pM;
+          gX = pX;
+          gY = pY;
+          gMP = pMP;
+          gXP = pXP;
+          gYP = pYP;
+        }
+        dM = uM;
+        dX = uX;
+        dY = uY;
+        dMP = uMP;
+        dXP = uXP;
+        dYP = uYP;
+        oM = M[R - 1];
+        oX = X[R - 1];
+        oY = Y[R - 1];
+        oMP = MP[R - 1];
+        oXP = XP[R - 1];
+        oYP = YP[R - 1];
+        ob = bc;
+        if (lane == 63 && blk + 1 < nblk) {
+          int *s = bnd + 6 * j;
+          s[0] = oM;
+          s[1] = oX;
+          s[2] = oY;
+          s[3] = (int)(uint32_t)oMP;
+          s[4] = (int)(uint32_t)oXP;
+          s[5] = (int)(uint32_t)oYP;
+          if constexpr (sizeof(P) == 8) {
+            int *s2 = bnd + 6 * (lb + 1) + 6 * j;
+            s2[3] = (int)(uint32_t)(oMP >> 32);
+            s2[4] = (int)(uint32_t)(oXP >> 32);
+            s2[5] = (int)(uint32_t)(oYP >> 32);
+          }
+        }
+      } else {
+        ob = bc;
+      }
+    }
+    // the final cell (la, lb) lives in this block's lane/row
+    const int fl = la - blk * 64 * R - 1;
+    if (fl >= 0 && fl < 64 * R && lane == fl / R) {
+      const int r = fl % R;
+      int mM = 0, mX = 0, mY = 0;
+      P pM = 0, pX = 0, pY = 0;
+#pragma unroll
+      for (int rr = 0; rr < R; rr++)
+        if (rr == r) {
+          mM = M[rr];
+          mX = X[rr];
+          mY = Y[rr];
+          pM = MP[rr];
+          pX = XP[rr];
+          pY = YP[rr];
+        }
+      // GlobAlignE.cpp:278-291: M, then lowerGap (X), then upperGap (Y)
+      int sc = mM > mX ? mM : mX;
+      sc = sc > mY ? sc : mY;
+      fin_score = sc;
+      fin_pay = sc == mM ? pM : (sc == mX ? pX : pY);
+    }
+    __syncthreads();
+  }
+  const int fl = la - (nblk - 1) * 64 * R - 1;
+  const int owner = la == 0 ? 0 : fl / R;
+  if (lane == owner) {
+    int L, I;
+    if (la == 0) {  // no rows: alignmentScore = max(matches[0], ...) at the initial state
+      L = 0;
+      I = 0;
+      fin_score = 0;
+    } else {
+      L = (int)(fin_pay >> SH);
+      I = (int)(fin_pay & (((P)1 << SH) - 1));
+    }
+    q.ident[p] = (double)I / (double)L;
+    if (q.len) q.len[p] = L;
+    if (q.ids) q.ids[p] = I;
+    if (q.score) q.score[p] = fin_score;
+  }
+}
+
+template <int R, typename P>
+int launch_bucket(mc_ctx *c, NWPairs q) {
+  if (q.npairs == 0) return MC_OK;
+  nw_kernel<R, P><<<q.npairs, 64, 0, c->stream>>>(q);
+  MCG_CHECK(hipGetLastError());
+  return MC_OK;
+}
+
+}  // namespace
+
+int launch_nw(mc_ctx *c, const uint8_t *d_A, const uint64_t *d_aoff, const uint32_t *d_ai, const uint8_t *d_B,
+              const uint64_t *d_boff, const uint32_t *d_bi, uint64_t m, const std::vector<uint64_t> &alen,
+              const std::vector<uint64_t> &blen, double *d_ident, int32_t *d_len, int32_t *d_ids,
+              int32_t *d_score) {
+  if (m == 0) return MC_OK;
+  // bucket pairs by rows per lane and payload width; boundary scratch for multi-block pairs
+  enum { NB = 8 };
+  std::vector<uint32_t> bucket[NB];
+  std::vector<uint64_t> boff[NB];
+  uint64_t scratch[NB] = {0};
+  for (uint64_t i = 0; i < m; i++) {
+    const uint64_t la = alen[i], lb = blen[i];
+    const bool wide = la + lb >= 65535;
+    int r = la <= 256 ? 0 : la <= 512 ? 1 : 2;  // R = 4, 8, 16
+    int bk = r + (wide ? 3 : 0);
+    bucket[bk].push_back((uint32_t)i);
+    boff[bk].push_back(scratch[bk]);
+    const uint64_t rows = 64ull * (r == 0 ? 4 : r == 1 ? 8 : 16);
+    if (la > rows) scratch[bk] += 12 * (lb + 1);
+  }
+  timed_begin(c);
+  uint64_t total_idx = 0, total_scr = 0;
+  for (int k = 0; k < NB; k++) {
+    total_idx += bucket[k].size();
+    total_scr += scratch[k];
+  }
+  if (ensure(c->s_a, total_idx * 4 + 16) || ensure(c->s_b, total_idx * 8 + 16) ||
+      ensure(c->s_c, std::max<uint64_t>(total_scr, 1) * 4))
+    return MC_ERR_OOM;
+  uint64_t io = 0, so = 0;
+  for (int k = 0; k < NB; k++) {
+    if (bucket[k].empty()) continue;
+    for (auto &v : boff[k]) v += so;
+    MCG_CHECK(hipMemcpyAsync((uint32_t *)c->s_a.p + io, bucket[k].data(), bucket[k].size() * 4, hipMemcpyHostToDevice,
+                             c->stream));
+    MCG_CHECK(hipMemcpyAsync((uint64_t *)c->s_b.p + io, boff[k].data(), boff[k].size() * 8, hipMemcpyHostToDevice,
+                             c->stream));
+    NWPairs q{d_A, d_aoff, d_ai, d_B, d_boff, d_bi, (uint32_t *)c->s_a.p + io, (uint32_t)bucket[k].size(),
+              (int *)c->s_c.p, (uint64_t *)c->s_b.p + io, d_ident, d_len, d_ids, d_score};
+    int rc = MC_OK;
+    switch (k) {
+      case 0: rc = launch_bucket<4, uint32_t>(c, q); break;
+      case 1: rc = launch_bucket<8, uint32_t>(c, q); break;
+      case 2: rc = launch_bucket<16, uint32_t>(c, q); break;
+      case 3: rc = launch_bucket<4, uint64_t>(c, q); break;
+      case 4: rc = launch_bucket<8, uint64_t>(c, q); break;
+      default: rc = launch_bucket<16, uint64_t>(c, q); break;
+    }
+    if (rc) return rc;
+    io += bucket[k].size();
+    so += scratch[k];
+  }
+  // keep the host vectors alive until the async copies have run
+  timed_end(c, F_NW);
+  MCG_CHECK(hipStreamSynchronize(c->stream));
+  return MC_OK;
+}
+
+}  // namespace mcg

@@ -31,6 +31,7 @@ struct ClusterStats {
   uint64_t scan_candidates = 0;  // sum of get_close window sizes (K2 evaluations)
   uint64_t update_evals = 0;     // filter evaluations in the mean-shift updates
   uint64_t merge_evals = 0;
+  uint64_t nw_pairs = 0, nw_cells = 0;  // training alignments
 };
 
 // Runs accumulation + `iterations` rounds of mean-shift update and merge.

@@ -175,6 +175,8 @@ RunResult run_pipeline(const Dataset &ds, mc_ctx *ctx, Options opt, bool upload)
   cc.delta = opt.delta;
   cc.verbose = verbose;
   rr.part = mean_shift_cluster(ds, ctx, bv, cc, rr.timer, rr.stats);
+  rr.stats.nw_pairs = tr.nw_pairs;
+  rr.stats.nw_cells = tr.nw_cells;
   rr.timer.add("total_pipeline",
                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
   return rr;
@@ -186,9 +188,12 @@ std::string stats_json(const RunResult &rr, double parse_ms, double write_ms) {
   snprintf(b, sizeof b, "{\"n\": %zu, \"k\": %d, \"width\": %d, \"clusters\": %zu, \"parse_ms\": %.3f, \"write_ms\": %.3f",
            rr.n, rr.k, rr.width, rr.part.size(), parse_ms, write_ms);
   o += b;
-  snprintf(b, sizeof b, ", \"scan_steps\": %llu, \"scan_candidates\": %llu, \"update_evals\": %llu, \"merge_evals\": %llu",
+  snprintf(b, sizeof b,
+           ", \"scan_steps\": %llu, \"scan_candidates\": %llu, \"update_evals\": %llu, \"merge_evals\": %llu"
+           ", \"nw_pairs\": %llu, \"nw_cells\": %llu",
            (unsigned long long)rr.stats.scan_steps, (unsigned long long)rr.stats.scan_candidates,
-           (unsigned long long)rr.stats.update_evals, (unsigned long long)rr.stats.merge_evals);
+           (unsigned long long)rr.stats.update_evals, (unsigned long long)rr.stats.merge_evals,
+           (unsigned long long)rr.stats.nw_pairs, (unsigned long long)rr.stats.nw_cells);
   o += b;
   o += ", \"phases_ms\": {";
   for (size_t i = 0; i < rr.timer.order.size(); i++) {

@@ -71,6 +71,10 @@ void Trainer::nw_batch(const std::vector<PairId> &pairs, std::vector<double> &id
   }
   ident.assign(pairs.size(), 0.0);
   if (pairs.empty()) return;
+  for (const auto &p : pairs) {
+    nw_pairs++;
+    nw_cells += ds_.lengths[p.first] * ds_.lengths[p.second];
+  }
   check(mc_nw_identity(ctx_, a.data(), b.data(), pairs.size(), ident.data(), nullptr, nullptr), "mc_nw_identity");
 }
 

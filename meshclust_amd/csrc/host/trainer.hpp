@@ -39,6 +39,7 @@ class Trainer {
   // exposed for tests / diagnostics
   std::vector<PairId> split_pairs;
   std::vector<std::pair<PairId, double>> label_pos, label_neg;
+  uint64_t nw_pairs = 0, nw_cells = 0;  // work counters (NW cell updates)
 
  private:
   std::vector<PairId> split();

@@ -1,0 +1,163 @@
+"""GPU parity: libmcgpu (through its C-ABI) against the reference goldens and the C oracle.
+
+Bit-exact everywhere: integer histograms / sort keys / NW lengths and identity counts, and
+the IEEE-double features, GLM sums and decisions compared with ==.  End to end, the shipped
+bin/meshclust must reproduce the reference's --threads 1 .clstr byte for byte.
+"""
+import gzip
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import fixtures
+import meshclust_amd as M
+import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng(built):
+    M.build()
+    e = M.Engine(0)
+    yield e
+    e.close()
+
+
+def load_records(eng, recs):
+    """recs: list of (codes uint8, segments [[s,e],...])."""
+    codes = np.concatenate([c for c, _ in recs]).astype(np.uint8)
+    seq_off = np.cumsum([0] + [len(c) for c, _ in recs]).astype(np.uint64)
+    seg = np.array([x for _, s in recs for pair in s for x in pair], np.int32)
+    seg_off = np.cumsum([0] + [len(s) for _, s in recs]).astype(np.uint64)
+    eng.load_sequences(codes, seq_off, seg, seg_off)
+
+
+@pytest.mark.parametrize("k", [1, 3, 4, 6])
+def test_kmer_hist_edge(eng, k):
+    recs = [(np.frombuffer(bytes.fromhex(r["data_hex"]), np.uint8), r["segments"]) for r in fixtures.edge_records()]
+    g = np.load(fixtures.golden("edge_hist.npz"))
+    load_records(eng, recs)
+    assert eng.kmer_max(k) == int(g["k%d" % k].max())
+    eng.kmer_build(k, 1 if g["k%d" % k].max() <= 255 else 2)
+    h, mags = eng.histograms()
+    assert np.array_equal(h.astype(np.uint64), g["k%d" % k])
+    assert np.array_equal(mags, g["mag%d" % k])
+
+
+def test_kmer_widths_match_oracle(eng):
+    """u16/u32 histograms (forced widths) on long low-complexity sequences."""
+    rng = np.random.default_rng(3)
+    recs = []
+    for i in range(40):
+        L = int(rng.integers(300, 5000))
+        c = rng.integers(0, 2 if i % 3 == 0 else 4, size=L).astype(np.uint8)
+        recs.append((c, [[0, L - 1]]))
+    load_records(eng, recs)
+    for k in (2, 4):
+        want = np.array([O.kmer_hist(c, s, k) for c, s in recs])
+        assert eng.kmer_max(k) == int(want.max())
+        for width, dt in ((2, np.uint16), (4, np.uint32), (8, np.uint64)):
+            if want.max() > np.iinfo(dt).max:
+                continue
+            eng.kmer_build(k, width)
+            h, _ = eng.histograms()
+            assert h.dtype == dt and np.array_equal(h.astype(np.uint64), want)
+
+
+def test_nw_golden(eng):
+    g = np.load(fixtures.golden("nw.npz"))
+    ident, ln, ids, sc = eng.nw_identity_raw(g["a"], g["a_off"], g["b"], g["b_off"])
+    assert np.array_equal(ln, g["length"])
+    assert np.array_equal(ids, g["ids"])
+    assert np.array_equal(sc, g["score"])
+    assert np.array_equal(ident, g["identity"])
+
+
+def test_nw_long_multiblock_vs_oracle(eng):
+    """Pairs longer than one 1024-row block (boundary row in scratch) and >64k total length."""
+    rng = np.random.default_rng(9)
+    pairs = []
+    for la, lb in ((1500, 1400), (2100, 2500), (4000, 3900), (1025, 1030), (3000, 200)):
+        a = rng.integers(0, 4, size=la).astype(np.uint8)
+        b = a[:lb].copy() if lb <= la else np.concatenate([a, rng.integers(0, 4, size=lb - la).astype(np.uint8)])
+        flip = rng.random(len(b)) < 0.08
+        b[flip] = rng.integers(0, 4, size=int(flip.sum()))
+        pairs.append((a, b))
+    a_cat = np.concatenate([a for a, _ in pairs])
+    b_cat = np.concatenate([b for _, b in pairs])
+    a_off = np.cumsum([0] + [len(a) for a, _ in pairs])
+    b_off = np.cumsum([0] + [len(b) for _, b in pairs])
+    ident, ln, ids, sc = eng.nw_identity_raw(a_cat, a_off, b_cat, b_off)
+    for i, (a, b) in enumerate(pairs):
+        w = O.nw(a.tobytes(), b.tobytes())
+        assert (ident[i], ln[i], ids[i], sc[i]) == w, i
+
+
+@pytest.fixture(scope="module")
+def a1k(eng):
+    g = np.load(fixtures.golden("train_a1k.npz"))
+    man = fixtures.manifest()["e2e"]["a1k"]["generator"]
+    recs = fixtures.synth_records(*man)
+    load_records(eng, [(c, [[0, L - 1]]) for _, c, L in recs])
+    k = int(g["k"])
+    eng.kmer_build(k, 1)
+    return g, recs
+
+
+def test_distance_keys_golden(eng, a1k):
+    g, recs = a1k
+    ij = g["pair_ij"]
+    n = 40
+    keys = eng.distance_keys(np.arange(n), np.arange(n))  # keys[p, i] = distance(i, p)
+    want = g["distance"].reshape(n, n)                     # row i, col j: points[i].distance(points[j])
+    assert np.array_equal(keys.T.astype(np.uint64), want)
+    assert ij[1][0] == 0 and ij[1][1] == 1
+
+
+def test_distance_keys_many_pivots_vs_oracle(eng, a1k):
+    g, recs = a1k
+    h, mags = eng.histograms()
+    rng = np.random.default_rng(1)
+    piv = rng.choice(len(recs), size=150, replace=False)
+    keys = eng.distance_keys(piv, np.arange(len(recs)))
+    for pi in range(0, 150, 37):
+        for i in range(0, len(recs), 53):
+            assert keys[pi, i] == O.distance(h[i], h[piv[pi]])
+
+
+def test_features_and_classify_golden(eng, a1k):
+    g, recs = a1k
+    ij = g["pair_ij"]
+    flags = [2, 16, 4, 32, 1024]
+    raw = eng.pair_features(ij[:, 0], ij[:, 1], flags)
+    assert np.array_equal(raw, g["raw"])
+    eng.set_classifier(O.classifier_from_golden(g))
+    sim, c0, s = eng.classify_pairs(ij[:, 0], ij[:, 1])
+    assert np.array_equal(s, g["sums"])
+    assert np.array_equal(sim, g["decision"].astype(np.uint8))
+    assert np.array_equal(c0, g["combo_vals"][:, 0])
+
+
+def test_nw_loaded_sequences(eng, a1k):
+    g, recs = a1k
+    pos = g["pos"]
+    a, b = pos[:64, 0].astype(np.uint32), pos[:64, 1].astype(np.uint32)
+    ident, _, _ = eng.nw_identity(a, b)
+    assert np.array_equal(ident, pos[:64, 2])
+
+
+E2E = sorted(fixtures.manifest()["e2e"])
+
+
+@pytest.mark.parametrize("name", E2E)
+def test_e2e_cli_byte_identical(eng, name, tmp_path):
+    fa, flags = fixtures.e2e_input(name, tmp_path)
+    out = tmp_path / (name + ".clstr")
+    r = subprocess.run([M.BIN, fa] + flags + ["--output", str(out), "--quiet"], capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    with gzip.open(fixtures.golden("e2e_%s.clstr.gz" % name), "rb") as f:
+        assert out.read_bytes() == f.read()
