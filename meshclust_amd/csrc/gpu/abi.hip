@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cfloat>
 #include <cmath>
 #include <cstring>
@@ -164,9 +165,11 @@ int mc_ctx_destroy(mc_ctx *c) {
   (void)hipStreamSynchronize(c->stream);
   for (Buf *b : {&c->codes, &c->seq_off, &c->seg, &c->seg_off, &c->hist, &c->mag, &c->sumsq, &c->len, &c->order,
                  &c->alive, &c->members, &c->member_keys, &c->partials, &c->scan_dev, &c->flags_out, &c->s_a, &c->s_b,
-                 &c->s_c, &c->s_d, &c->s_e, &c->s_f, &c->s_g})
+                 &c->s_c, &c->s_d, &c->s_e, &c->s_f, &c->s_g, &c->hs, &c->mag_s, &c->sumsq_s, &c->len_s, &c->ticket,
+                 &c->msum})
     release(*b);
   if (c->h_scan) (void)hipHostFree(c->h_scan);
+  if (c->h_res) (void)hipHostFree(c->h_res);
   for (auto e : c->ev_pool) (void)hipEventDestroy(e);
   (void)hipEventDestroy(c->ev0);
   (void)hipEventDestroy(c->ev1);
@@ -405,37 +408,75 @@ int mc_nw_identity_raw(mc_ctx *c, const uint8_t *a, const uint64_t *a_off, const
 
 static const size_t kFlagPrefix = 4096;  // flagged positions copied back with the result
 
+static bool fused(const mc_ctx *c) { return c->width == 1 || c->width == 2; }
+
 int mc_set_order(mc_ctx *c, const uint32_t *order, uint64_t n) {
   if (!c || !order || n != c->n) return MC_ERR_ARG;
+  if (c->k == 0) return MC_ERR_STATE;
   MCG_CHECK(hipSetDevice(c->device));
   TRY(check_ids(c, order, n));
   c->norder = n;
+  c->h_spos.assign(n, 0);
+  for (uint64_t p = 0; p < n; p++) c->h_spos[order[p]] = p;
   TRY(upload(c->order, order, n, c->stream));
   TRY(ensure(c->alive, n + 16));
   MCG_CHECK(hipMemsetAsync(c->alive.p, 1, n, c->stream));
   TRY(ensure(c->members, (n + 1) * 4));
   TRY(ensure(c->member_keys, (n + 1) * 8));
-  TRY(ensure(c->partials, 4096 * sizeof(ScanPartial)));
+  TRY(ensure(c->partials, ((n + 255) / 256 + 4096) * sizeof(ScanPartial)));
   TRY(ensure(c->scan_dev, sizeof(ScanDev) + std::max<uint64_t>(n + 1, kFlagPrefix) * 4));
   if (!c->h_scan) {
     c->h_scan_cap = sizeof(ScanDev) + kFlagPrefix * 4;
     MCG_CHECK(hipHostMalloc((void **)&c->h_scan, c->h_scan_cap, hipHostMallocDefault));
   }
   MCG_CHECK(hipMemsetAsync(c->scan_dev.p, 0, sizeof(ScanDev), c->stream));
+  c->step = 0;
+  c->pending_kills.clear();
+  c->pending_begin = false;
+  if (fused(c)) {
+    TRY(ensure(c->ticket, 64));
+    MCG_CHECK(hipMemsetAsync(c->ticket.p, 0, 64, c->stream));
+    TRY(ensure(c->msum, (size_t)c->B * 8));
+    const size_t hbytes = sizeof(HostScan) + (n + 16) * 4;
+    if (c->h_res && c->h_res_cap < hbytes) {
+      (void)hipHostFree(c->h_res);
+      c->h_res = nullptr;
+    }
+    if (!c->h_res) {
+      MCG_CHECK(hipHostMalloc((void **)&c->h_res, hbytes, hipHostMallocMapped));
+      MCG_CHECK(hipHostGetDevicePointer((void **)&c->h_res_dev, c->h_res, 0));
+      c->h_res_cap = hbytes;
+    }
+    c->h_res->seq = 0;
+    c->seq = 0;
+    TRY(build_static(c));
+  }
   MCG_CHECK(hipStreamSynchronize(c->stream));
   flush_timers(c);
-  c->step = 0;
   return MC_OK;
 }
 
 int mc_kill(mc_ctx *c, uint64_t pos) {
   if (!c || pos >= c->norder) return MC_ERR_ARG;
+  if (fused(c)) {  // applied by the next scan launch (which also excludes it from its window)
+    if (c->pending_kills.size() == 8) {
+      for (uint64_t p : c->pending_kills) MCG_CHECK(hipMemsetAsync((uint8_t *)c->alive.p + p, 0, 1, c->stream));
+      c->pending_kills.clear();
+    }
+    c->pending_kills.push_back(pos);
+    return MC_OK;
+  }
   MCG_CHECK(hipMemsetAsync((uint8_t *)c->alive.p + pos, 0, 1, c->stream));
   return MC_OK;
 }
 
 int mc_cluster_begin(mc_ctx *c, uint32_t first) {
   if (!c || first >= c->n || c->norder == 0) return MC_ERR_ARG;
+  if (fused(c)) {  // deferred into the next scan launch
+    c->pending_begin = true;
+    c->pending_first_pos = c->h_spos[first];
+    return MC_OK;
+  }
   ScanDev sd;
   memset(&sd, 0, sizeof sd);
   sd.nmembers = 1;
@@ -449,11 +490,51 @@ int mc_cluster_begin(mc_ctx *c, uint32_t first) {
   return MC_OK;
 }
 
+// Spin on the sequence number the fused scan publishes in pinned host memory.
+static int wait_seq(mc_ctx *c, uint32_t seq) {
+  auto t0 = std::chrono::steady_clock::now();
+  for (uint64_t it = 0;; it++) {
+    if (__atomic_load_n(&c->h_res->seq, __ATOMIC_ACQUIRE) == seq) return MC_OK;
+    if ((it & 4095) == 4095) {
+      hipError_t e = hipStreamQuery(c->stream);
+      if (e != hipSuccess && e != hipErrorNotReady) return hip_fail(e, "fused scan kernel");
+      if (e == hipSuccess) {
+        if (__atomic_load_n(&c->h_res->seq, __ATOMIC_ACQUIRE) == seq) return MC_OK;
+        set_error("fused scan finished without publishing its result");
+        return MC_ERR_HIP;
+      }
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(120)) {
+        set_error("fused scan result timeout");
+        return MC_ERR_HIP;
+      }
+    }
+    __builtin_ia32_pause();
+  }
+}
+
 int mc_scan(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, uint32_t *flagged_pos, uint64_t cap,
             mc_scan_result *res) {
   if (!c || !res || !c->has_cls || c->norder == 0) return MC_ERR_STATE;
   if (S > E || E >= c->norder || centre >= c->n) return MC_ERR_ARG;
   c->step++;
+  if (fused(c)) {
+    const uint32_t seq = ++c->seq;
+    TRY(launch_fused_scan(c, centre, S, E, seq));
+    TRY(wait_seq(c, seq));
+    *res = c->h_res->r;
+    const uint64_t nf = res->n_flagged;
+    if (nf > cap) {
+      set_error("flagged buffer too small");
+      return MC_ERR_ARG;
+    }
+    memcpy(flagged_pos, c->h_res->flags, nf * 4);
+    std::sort(flagged_pos, flagged_pos + nf);
+    if (c->ev_pending.size() > 512) {
+      MCG_CHECK(hipStreamSynchronize(c->stream));
+      flush_timers(c);
+    }
+    return MC_OK;
+  }
   int nblocks = 0;
   TRY(launch_scan(c, centre, S, E, &nblocks));
   TRY(launch_finalize(c, nblocks));
@@ -473,7 +554,7 @@ int mc_scan(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, uint32_t *flagge
     MCG_CHECK(hipMemcpyAsync(flagged_pos + first, (char *)c->scan_dev.p + sizeof(ScanDev) + first * 4, (nf - first) * 4,
                              hipMemcpyDeviceToHost, c->stream));
     MCG_CHECK(hipStreamSynchronize(c->stream));
-  flush_timers(c);
+    flush_timers(c);
   }
   std::sort(flagged_pos, flagged_pos + nf);
   return MC_OK;

@@ -250,4 +250,106 @@ __device__ __forceinline__ PS wave_pair_stats(const HistView &H, uint32_t my_a, 
   return mine;
 }
 
+// ---------------------------------------------------------------------------------------
+// get_mean / Trainer::closest for 8/16-bit bins (ClusterFactory.cpp:382-425, Trainer.cpp:351-365).
+// With m_b = S_b / M, (T)m_b = floor(S_b / M) = F_b and the per-bin re-truncated magnitude of
+// distance_d equals sum_b (p_b + F_b) exactly (tests/test_identities.py), so
+//   distance_d(p, mean) = 1e4 * fma(-f, f, 1),  f = 2*sum min(p_b, F_b) / (mag_p + sum F_b)
+// is a SAD reduction of p against the packed integer mean F.
+struct RowRef {  // chunk c of row r = base[r * rstride + c * cstride]
+  const uint4 *base;
+  uint64_t rstride, cstride;
+  __device__ __forceinline__ uint4 chunk(uint64_t r, int c) const { return base[r * rstride + (uint64_t)c * cstride]; }
+};
+
+template <typename T>
+__device__ __forceinline__ uint64_t elem(const RowRef &R, uint64_t r, int b) {
+  constexpr int per = 16 / (int)sizeof(T);
+  uint4 v = R.chunk(r, b / per);
+  return reinterpret_cast<const T *>(&v)[b % per];
+}
+
+// One workgroup.  rows[q] (q < M) are row indices into R with magnitudes mags[rows[q]];
+// keys[q] (or q itself) orders ties like the reference's serial first-min scan.
+// lds_sum: B u64 (may be global), lds_F: nch uint4.  Returns the winning row on thread 0.
+template <typename T, int NTH>
+__device__ uint64_t mean_closest_fast(const RowRef &R, const uint32_t *rows, const uint64_t *keys, uint32_t M,
+                                      const uint64_t *mags, int B, int nch, uint64_t *sum, uint4 *Fl,
+                                      bool sums_ready) {
+  __shared__ double rd[NTH / 64];
+  __shared__ uint64_t rk[NTH / 64];
+  __shared__ uint64_t rr[NTH / 64];
+  __shared__ uint64_t sF;
+  if (!sums_ready) {
+    for (int b = threadIdx.x; b < B; b += NTH) {
+      uint64_t s = 0;
+      for (uint32_t q = 0; q < M; q++) s += elem<T>(R, rows[q], b);
+      sum[b] = s;
+    }
+  }
+  if (threadIdx.x == 0) sF = 0;
+  __syncthreads();
+  constexpr int per = 16 / (int)sizeof(T);
+  uint64_t part = 0;
+  for (int c = threadIdx.x; c < nch; c += NTH) {
+    uint4 v = make_uint4(0, 0, 0, 0);
+    T *pv = reinterpret_cast<T *>(&v);
+    for (int i = 0; i < per; i++) {
+      const int b = c * per + i;
+      const uint64_t F = b < B ? sum[b] / M : 0;
+      pv[i] = (T)F;
+      part += F;
+    }
+    Fl[c] = v;
+  }
+  atomicAdd((unsigned long long *)&sF, (unsigned long long)part);
+  __syncthreads();
+  const uint64_t sumF = sF;
+  double bd = __builtin_inf();
+  uint64_t bk = ~0ull, br = 0;
+  for (uint32_t q = threadIdx.x; q < M; q += NTH) {
+    const uint64_t r = rows[q];
+    Acc<T> acc;
+    for (int c = 0; c < nch; c++) acc.add(R.chunk(r, c), Fl[c]);
+    const uint64_t mp = mags[r];
+    const PS s = acc.finish(mp, sumF);
+    const double frac = (double)(2 * s.smin) / (double)(mp + sumF);
+    const double d = __builtin_fma(-frac, frac, 1.0) * 10000.0;
+    const uint64_t key = keys ? keys[q] : q;
+    if (d < bd || (d == bd && key < bk)) {
+      bd = d;
+      bk = key;
+      br = r;
+    }
+  }
+  for (int o = 32; o >= 1; o >>= 1) {
+    double od = __shfl_xor(bd, o, 64);
+    uint64_t ok = shfl_xor64(bk, o), orr = shfl_xor64(br, o);
+    if (od < bd || (od == bd && ok < bk)) {
+      bd = od;
+      bk = ok;
+      br = orr;
+    }
+  }
+  if ((threadIdx.x & 63) == 0) {
+    rd[threadIdx.x >> 6] = bd;
+    rk[threadIdx.x >> 6] = bk;
+    rr[threadIdx.x >> 6] = br;
+  }
+  __syncthreads();
+  uint64_t win = rr[0];
+  if (threadIdx.x == 0) {
+    double d = rd[0];
+    uint64_t k = rk[0];
+    for (int i = 1; i < NTH / 64; i++)
+      if (rd[i] < d || (rd[i] == d && rk[i] < k)) {
+        d = rd[i];
+        k = rk[i];
+        win = rr[i];
+      }
+  }
+  __syncthreads();
+  return win;
+}
+
 }  // namespace mcg

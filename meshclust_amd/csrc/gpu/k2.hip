@@ -404,11 +404,19 @@ __global__ __launch_bounds__(NT) void mean_shift_kernel(HistView H, DevClassifie
     return;
   }
   double *mbuf = H.B <= 2048 ? mean : gmean + (uint64_t)j * H.B;
-  uint32_t nid = 0;
-  __shared__ uint32_t out_id;
-  mean_closest<T, NT>(H, mine, nullptr, M, mbuf, &out_id);
-  nid = out_id;
-  if (threadIdx.x == 0) newc[j] = nid;
+  if constexpr (sizeof(T) <= 2) {
+    // integer mean + SAD closest (tests/test_identities.py); sums reuse the mean buffer
+    const RowRef R{reinterpret_cast<const uint4 *>(H.hist), H.pitch / 16, 1};
+    uint4 *Fl = clds;  // the centre chunks are no longer needed
+    __syncthreads();
+    const uint64_t win = mean_closest_fast<T, NT>(R, mine, nullptr, M, H.mag, H.B, nch,
+                                                  reinterpret_cast<uint64_t *>(mbuf), Fl, false);
+    if (threadIdx.x == 0) newc[j] = (uint32_t)win;
+  } else {
+    __shared__ uint32_t out_id;
+    mean_closest<T, NT>(H, mine, nullptr, M, mbuf, &out_id);
+    if (threadIdx.x == 0) newc[j] = out_id;
+  }
 }
 
 int grid_for(uint64_t work, int per_block, int cap) {

@@ -58,6 +58,14 @@ struct Buf {
   size_t bytes = 0;
 };
 
+// Pinned, device-mapped record the fused scan publishes (zero-copy; seq written last).
+struct HostScan {
+  mc_scan_result r;
+  uint32_t seq;
+  uint32_t pad;
+  uint32_t flags[1];  // n_flagged static positions follow
+};
+
 }  // namespace mcg
 
 struct mc_ctx {
@@ -78,8 +86,18 @@ struct mc_ctx {
   uint64_t norder = 0;
   mcg::Buf order, alive, members, member_keys, partials, scan_dev, flags_out;
   uint32_t step = 0;
-  mcg::ScanDev *h_scan = nullptr;  // pinned mirror of scan_dev + flagged prefix
+  mcg::ScanDev *h_scan = nullptr;  // pinned mirror of scan_dev + flagged prefix (generic path)
   size_t h_scan_cap = 0;
+  // fused path (8/16-bit bins): static chunk-major layout + zero-copy result
+  mcg::Buf hs, mag_s, sumsq_s, len_s, ticket, msum;
+  uint64_t npad = 0;
+  mcg::HostScan *h_res = nullptr, *h_res_dev = nullptr;
+  size_t h_res_cap = 0;
+  uint32_t seq = 0;
+  std::vector<uint64_t> pending_kills;
+  bool pending_begin = false;
+  uint64_t pending_first_pos = 0;
+  std::vector<uint64_t> h_spos;  // id -> static position
   // scratch
   mcg::Buf s_a, s_b, s_c, s_d, s_e, s_f, s_g;
   std::vector<void *> pinned;
@@ -113,6 +131,8 @@ int launch_scan(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, int *nblocks
 int launch_finalize(mc_ctx *c, int nblocks);
 int launch_mean_shift(mc_ctx *c, const uint32_t *d_cid, uint32_t C, const uint64_t *d_off, const uint64_t *h_off,
                       const uint32_t *d_mem, int delta, uint32_t *d_new);
+int build_static(mc_ctx *c);
+int launch_fused_scan(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, uint32_t seq);
 // NW on byte strings: pair p aligns A[aoff[ai[p]] .. aoff[ai[p]+1]) against B[...] (rows = A).
 int launch_nw(mc_ctx *c, const uint8_t *d_A, const uint64_t *d_aoff, const uint32_t *d_ai, const uint8_t *d_B,
               const uint64_t *d_boff, const uint32_t *d_bi, uint64_t m, const std::vector<uint64_t> &h_alen,

@@ -93,8 +93,18 @@ bool BVec::inner_index_of(uint64_t length, size_t &idx, size_t *pfront, size_t *
 void BVec::insert(uint32_t id) {
   uint64_t len = len_[id];
   size_t front = 0, back = 0;
-  index_of(len, &front, &back);
-  std::vector<size_t> min_sizes;
+  // index_of depends only on the length and the (fixed) bin bounds: memoise it
+  auto it = std::lower_bound(index_memo_.begin(), index_memo_.end(), len,
+                             [](const std::pair<uint64_t, std::pair<size_t, size_t>> &e, uint64_t v) { return e.first < v; });
+  if (it != index_memo_.end() && it->first == len) {
+    front = it->second.first;
+    back = it->second.second;
+  } else {
+    index_of(len, &front, &back);
+    index_memo_.insert(it, {len, {front, back}});
+  }
+  std::vector<size_t> &min_sizes = min_sizes_;
+  min_sizes.clear();
   size_t minimum = std::numeric_limits<size_t>::max();
   for (size_t i = front; i <= back; i++) {
     size_t sz = data_[i].size();
@@ -114,11 +124,13 @@ void BVec::insert_finalize() {
   for (auto &bin : data_)
     std::sort(bin.begin(), bin.end(), [&](uint32_t a, uint32_t b) { return len_[a] < len_[b]; });
   order_.clear();
+  bin_of_.clear();
   spos_.assign(len_.size(), std::numeric_limits<uint64_t>::max());
-  for (const auto &bin : data_)
-    for (uint32_t id : bin) {
+  for (size_t r = 0; r < data_.size(); r++)
+    for (uint32_t id : data_[r]) {
       spos_[id] = order_.size();
       order_.push_back(id);
+      bin_of_.push_back((uint32_t)r);
     }
 }
 
@@ -187,10 +199,13 @@ int64_t BVec::window(const BIdx &b, const BIdx &e, uint64_t *S, uint64_t *E) con
 
 void BVec::remove_positions(const std::vector<uint32_t> &pos_sorted, size_t a, size_t b,
                             std::vector<uint32_t> &available) {
-  if (pos_sorted.empty()) return;
+  // Only the bins holding flagged candidates change; within a bin the survivors keep their
+  // order and the flagged ids leave in bvec order (== ascending static position).
   size_t k = 0;
-  for (size_t i = a; i <= b && k < pos_sorted.size(); i++) {
-    auto &bin = data_[i];
+  while (k < pos_sorted.size()) {
+    const size_t r = bin_of_[pos_sorted[k]];
+    if (r < a || r > b) throw Error("remove_available: flagged candidate outside the window bins", 3);
+    auto &bin = data_[r];
     size_t w = 0;
     for (size_t j = 0; j < bin.size(); j++) {
       uint32_t id = bin[j];
@@ -202,24 +217,17 @@ void BVec::remove_positions(const std::vector<uint32_t> &pos_sorted, size_t a, s
       }
     }
     bin.resize(w);
+    if (k < pos_sorted.size() && bin_of_[pos_sorted[k]] == r)
+      throw Error("remove_available: flagged candidate not alive in its bin", 3);
   }
-  if (k != pos_sorted.size()) throw Error("remove_available: flagged candidate outside the window bins", 3);
 }
 
 std::pair<size_t, size_t> BVec::locate(uint64_t pos) const {
-  uint32_t id = order_[pos];
-  // static positions are bin-major, so the bin is found by the first element's position
-  size_t lo = 0, hi = data_.size();
-  for (size_t r = 0; r < data_.size(); r++) {
-    (void)lo;
-    (void)hi;
-    const auto &bin = data_[r];
-    if (bin.empty()) continue;
-    if (spos_[bin.back()] < pos) continue;
-    for (size_t c = 0; c < bin.size(); c++)
-      if (bin[c] == id) return {r, c};
-    break;
-  }
+  const uint32_t id = order_[pos];
+  const size_t r = bin_of_[pos];
+  const auto &bin = data_[r];
+  for (size_t c = 0; c < bin.size(); c++)
+    if (bin[c] == id) return {r, c};
   throw Error("bvec: static position not alive", 3);
 }
 

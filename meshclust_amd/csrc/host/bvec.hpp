@@ -51,8 +51,11 @@ class BVec {
   const std::vector<uint64_t> &len_;
   std::vector<std::vector<uint32_t>> data_;
   std::vector<uint64_t> begin_bounds_;
-  std::vector<uint32_t> order_;  // static position -> id
-  std::vector<uint64_t> spos_;   // id -> static position
+  std::vector<uint32_t> order_;   // static position -> id
+  std::vector<uint64_t> spos_;    // id -> static position
+  std::vector<uint32_t> bin_of_;  // static position -> bin (bins never change membership)
+  std::vector<std::pair<uint64_t, std::pair<size_t, size_t>>> index_memo_;  // length -> index_of
+  std::vector<size_t> min_sizes_;
 };
 
 }  // namespace mc

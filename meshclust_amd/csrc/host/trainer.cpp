@@ -92,11 +92,14 @@ std::vector<PairId> Trainer::split() {
   {
     Scope s(timer_, "train.sort_keys");
     std::sort(points.begin(), points.end(),
-              [&](uint32_t a, uint32_t b) { return ds_.lengths[a] < ds_.lengths[b]; });
+              [&](uint32_t a, uint32_t b) { return ds_.lengths[a] < ds_.lengths[b]; });  // Trainer.cpp:672-675
     uint32_t begin_pt = points[N / 2];
     std::vector<uint16_t> key0(N);
     check(mc_distance_keys(ctx_, &begin_pt, 1, all_ids.data(), N, key0.data()), "mc_distance_keys");
-    std::sort(points.begin(), points.end(), [&](uint32_t a, uint32_t b) { return key0[a] < key0[b]; });
+    std::vector<uint64_t> w(N);
+    for (size_t t = 0; t < N; t++) w[t] = ((uint64_t)key0[points[t]] << 32) | points[t];
+    std::sort(w.begin(), w.end(), [](uint64_t a, uint64_t b) { return (a >> 32) < (b >> 32); });
+    for (size_t t = 0; t < N; t++) points[t] = (uint32_t)w[t];
   }
   int num_iterations = (int)std::ceil(((double)cfg_.n_points) / cfg_.max_pts_from_one) - 1;
   if (num_iterations <= 0) throw Error("sample size must exceed points per pivot (integer division by zero in Trainer::split)", 1);
@@ -105,7 +108,9 @@ std::vector<PairId> Trainer::split() {
   if (cfg_.verbose) printf("Point pairs: %zu\n", indices.size());
   const size_t to_add_each = cfg_.max_pts_from_one / 2;
   const size_t P = indices.size();
-  // every pivot's distance to every point: one GPU launch
+  // every pivot's distance to every point: one GPU launch.  Each pivot's std::sort runs on
+  // (key << 32 | id) words with a comparator that looks only at the key: the comparison
+  // outcomes -- and so the permutation -- are those of sorting ids by keys[id].
   std::vector<uint16_t> keys(P * N);
   std::vector<std::vector<uint32_t>> sorted(P);
   {
@@ -114,8 +119,11 @@ std::vector<PairId> Trainer::split() {
 #pragma omp parallel for schedule(dynamic) num_threads(cfg_.threads)
     for (size_t i = 0; i < P; i++) {
       const uint16_t *kk = &keys[i * N];
-      sorted[i] = points;
-      std::sort(sorted[i].begin(), sorted[i].end(), [&](uint32_t a, uint32_t b) { return kk[a] < kk[b]; });
+      std::vector<uint64_t> w(N);
+      for (size_t t = 0; t < N; t++) w[t] = ((uint64_t)kk[points[t]] << 32) | points[t];
+      std::sort(w.begin(), w.end(), [](uint64_t a, uint64_t b) { return (a >> 32) < (b >> 32); });
+      sorted[i].resize(N);
+      for (size_t t = 0; t < N; t++) sorted[i][t] = (uint32_t)w[t];
     }
   }
   // binary search with alignment (:703-721): the 150 dependent chains advance together, one

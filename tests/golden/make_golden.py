@@ -43,6 +43,11 @@ E2E = {
     "m2k_id80": (("mixed", 2000, 40, 0.08, 21), ["--id", "0.80"]),
     "m2k_id95": (("mixed", 2000, 40, 0.02, 22), ["--id", "0.95", "--delta", "3", "--iterations", "5"]),
     "s1k_k5": ((1200, 400, 60, 0.05, 23), ["--id", "0.85", "--kmer", "5"]),
+    # 16-bit histograms (k = 1: per-base counts > 255) through the whole pipeline
+    "w16_k1": ((800, 1200, 20, 0.05, 24), ["--id", "0.90", "--kmer", "1"]),
+    # related templates (families): ambiguous pairs, many merges
+    "fam2k": (("family", 2000, 50, 10, 0.10, 0.03, 25), ["--id", "0.90"]),
+    "fam2k_id85": (("family", 2000, 40, 8, 0.12, 0.04, 26), ["--id", "0.85", "--delta", "8"]),
 }
 TRAIN = {"a1k": ("a1k", 3, 0.90)}
 
@@ -80,7 +85,39 @@ def mixed_reads(n, n_templates, mut, seed):
         yield b"read%d template_%d" % (i, t), alpha[base].tobytes()
 
 
+def family_reads(n, n_templates, n_families, tmut, mut, seed, length=1000):
+    """Templates derived from a few family roots (tmut divergence), reads mutated by mut."""
+    rng = np.random.default_rng(seed)
+    alpha = np.frombuffer(b"ACGT", dtype=np.uint8)
+    roots = rng.integers(0, 4, size=(n_families, length), dtype=np.uint8)
+
+    def mutate(s, m):
+        p = m / 3.0
+        r = rng.random(len(s))
+        sub = r < p
+        dele = (r >= p) & (r < 2 * p)
+        ins = (r >= 2 * p) & (r < m)
+        s2 = s.copy()
+        s2[sub] = rng.integers(0, 4, size=int(sub.sum()), dtype=np.uint8)
+        keep = ~dele
+        reps = np.where(ins, 2, 1)[keep]
+        base = np.repeat(s2[keep], reps)
+        idx = np.cumsum(reps) - 1
+        insm = reps == 2
+        base[idx[insm]] = rng.integers(0, 4, size=int(insm.sum()), dtype=np.uint8)
+        return base
+
+    temps = [mutate(roots[t % n_families], tmut) for t in range(n_templates)]
+    for i in range(n):
+        t = i % n_templates
+        yield b"read%d family_%d template_%d" % (i, t % n_families, t), alpha[mutate(temps[t], mut)].tobytes()
+
+
 def make_input(spec, path):
+    if spec[0] == "family":
+        _, n, t, f, tmut, mut, seed = spec
+        synth.write_fasta(path, family_reads(n, t, f, tmut, mut, seed))
+        return sha256(path)
     if spec[0] == "mixed":
         _, n, t, mut, seed = spec
         synth.write_fasta(path, mixed_reads(n, t, mut, seed))
