@@ -269,24 +269,34 @@ __device__ __forceinline__ uint64_t elem(const RowRef &R, uint64_t r, int b) {
   return reinterpret_cast<const T *>(&v)[b % per];
 }
 
+// Adds the histograms of rows[0..M) into sum[0..B) (u64; LDS or global).  Work items are
+// (row, chunk) pairs so every thread issues independent 16-byte loads, then folds its chunk
+// into the sums with LDS/global atomics -- no per-thread serial walk over the rows.
+template <typename T, int NTH>
+__device__ __forceinline__ void add_rows(const RowRef &R, const uint32_t *rows, uint32_t M, int nch, uint64_t *sum) {
+  constexpr int per = 16 / (int)sizeof(T);
+  const uint64_t items = (uint64_t)M * nch;
+  for (uint64_t it = threadIdx.x; it < items; it += NTH) {
+    const uint32_t q = (uint32_t)(it / nch);
+    const int c = (int)(it % nch);
+    const uint4 v = R.chunk(rows[q], c);
+    const T *pv = reinterpret_cast<const T *>(&v);
+#pragma unroll
+    for (int e = 0; e < per; e++)
+      if (pv[e]) atomicAdd((unsigned long long *)&sum[c * per + e], (unsigned long long)pv[e]);
+  }
+}
+
 // One workgroup.  rows[q] (q < M) are row indices into R with magnitudes mags[rows[q]];
 // keys[q] (or q itself) orders ties like the reference's serial first-min scan.
-// lds_sum: B u64 (may be global), lds_F: nch uint4.  Returns the winning row on thread 0.
+// sum: B u64 holding the column sums of the M rows.  Fl: nch uint4 (LDS).  Returns the winner.
 template <typename T, int NTH>
 __device__ uint64_t mean_closest_fast(const RowRef &R, const uint32_t *rows, const uint64_t *keys, uint32_t M,
-                                      const uint64_t *mags, int B, int nch, uint64_t *sum, uint4 *Fl,
-                                      bool sums_ready) {
+                                      const uint64_t *mags, int B, int nch, const uint64_t *sum, uint4 *Fl) {
   __shared__ double rd[NTH / 64];
   __shared__ uint64_t rk[NTH / 64];
   __shared__ uint64_t rr[NTH / 64];
   __shared__ uint64_t sF;
-  if (!sums_ready) {
-    for (int b = threadIdx.x; b < B; b += NTH) {
-      uint64_t s = 0;
-      for (uint32_t q = 0; q < M; q++) s += elem<T>(R, rows[q], b);
-      sum[b] = s;
-    }
-  }
   if (threadIdx.x == 0) sF = 0;
   __syncthreads();
   constexpr int per = 16 / (int)sizeof(T);
@@ -302,7 +312,7 @@ __device__ uint64_t mean_closest_fast(const RowRef &R, const uint32_t *rows, con
     }
     Fl[c] = v;
   }
-  atomicAdd((unsigned long long *)&sF, (unsigned long long)part);
+  if (part) atomicAdd((unsigned long long *)&sF, (unsigned long long)part);
   __syncthreads();
   const uint64_t sumF = sF;
   double bd = __builtin_inf();
@@ -310,6 +320,7 @@ __device__ uint64_t mean_closest_fast(const RowRef &R, const uint32_t *rows, con
   for (uint32_t q = threadIdx.x; q < M; q += NTH) {
     const uint64_t r = rows[q];
     Acc<T> acc;
+#pragma unroll 8
     for (int c = 0; c < nch; c++) acc.add(R.chunk(r, c), Fl[c]);
     const uint64_t mp = mags[r];
     const PS s = acc.finish(mp, sumF);

@@ -408,9 +408,13 @@ __global__ __launch_bounds__(NT) void mean_shift_kernel(HistView H, DevClassifie
     // integer mean + SAD closest (tests/test_identities.py); sums reuse the mean buffer
     const RowRef R{reinterpret_cast<const uint4 *>(H.hist), H.pitch / 16, 1};
     uint4 *Fl = clds;  // the centre chunks are no longer needed
+    uint64_t *sums = reinterpret_cast<uint64_t *>(mbuf);
     __syncthreads();
-    const uint64_t win = mean_closest_fast<T, NT>(R, mine, nullptr, M, H.mag, H.B, nch,
-                                                  reinterpret_cast<uint64_t *>(mbuf), Fl, false);
+    for (int b = threadIdx.x; b < H.B; b += NT) sums[b] = 0;
+    __syncthreads();
+    add_rows<T, NT>(R, mine, M, nch, sums);
+    __syncthreads();
+    const uint64_t win = mean_closest_fast<T, NT>(R, mine, nullptr, M, H.mag, H.B, nch, sums, Fl);
     if (threadIdx.x == 0) newc[j] = (uint32_t)win;
   } else {
     __shared__ uint32_t out_id;

@@ -95,8 +95,16 @@ __global__ __launch_bounds__(ST) void fused_scan_kernel(FusedArgs A, DevClassifi
   if (valid) {
     Acc<T> acc;
     const uint4 *col = A.hs + pos;
-#pragma unroll 4
-    for (int c = 0; c < A.nch; c++) acc.add(col[(uint64_t)c * A.npad], clds[c]);
+    if (A.nch == 16) {
+      uint4 v[16];
+#pragma unroll
+      for (int c = 0; c < 16; c++) v[c] = col[(uint64_t)c * A.npad];
+#pragma unroll
+      for (int c = 0; c < 16; c++) acc.add(v[c], clds[c]);
+    } else {
+#pragma unroll 8
+      for (int c = 0; c < A.nch; c++) acc.add(col[(uint64_t)c * A.npad], clds[c]);
+    }
     const PInfo pi{A.mag_s[pos], A.sumsq_s[pos], A.len_s[pos]};
     const PS s = acc.finish(pi.mag, pc.mag);
     double raw[MC_MAX_SINGLE];
@@ -188,14 +196,16 @@ __global__ __launch_bounds__(ST) void fused_scan_kernel(FusedArgs A, DevClassifi
       }
     }
     const RowRef R{A.hs, 1, A.npad};
-    // running integer sum of the cluster's histograms (the reference re-sums all members)
-    for (int b = threadIdx.x; b < A.B; b += ST) {
-      uint64_t s = A.new_cluster ? elem<T>(R, A.first_pos, b) : A.msum[b];
-      for (uint32_t q = 0; q < nflag; q++) s += elem<T>(R, A.flags_dev[q], b);
-      A.msum[b] = s;
-    }
+    // integer column sums of the cluster: running sum from the previous step (or the new
+    // cluster's first member) + this step's flagged members, folded in LDS
+    uint64_t *lsum = A.B <= 4096 ? reinterpret_cast<uint64_t *>(Fl + A.nch) : A.msum;
+    for (int b = threadIdx.x; b < A.B; b += ST) lsum[b] = A.new_cluster ? elem<T>(R, A.first_pos, b) : A.msum[b];
     __syncthreads();
-    const uint64_t win = mean_closest_fast<T, ST>(R, A.mem_pos, A.mkeys, M, A.mag_s, A.B, A.nch, A.msum, Fl, true);
+    add_rows<T, ST>(R, A.flags_dev, nflag, A.nch, lsum);
+    __syncthreads();
+    if (lsum != A.msum)
+      for (int b = threadIdx.x; b < A.B; b += ST) A.msum[b] = lsum[b];
+    const uint64_t win = mean_closest_fast<T, ST>(R, A.mem_pos, A.mkeys, M, A.mag_s, A.B, A.nch, lsum, Fl);
     new_id = A.order[win];
   }
   if (threadIdx.x == 0) {
@@ -293,7 +303,7 @@ int launch_fused_scan(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, uint32
   A.msum = (uint64_t *)c->msum.p;
   A.hres = c->h_res_dev;
   A.seq = seq;
-  const size_t lds = (size_t)2 * nch * 16;
+  const size_t lds = (size_t)2 * nch * 16 + (c->B <= 4096 ? (size_t)c->B * 8 : 0);
   timed_begin(c);
   if (c->width == 1) fused_scan_kernel<uint8_t><<<grid, ST, lds, c->stream>>>(A, c->cls);
   else fused_scan_kernel<uint16_t><<<grid, ST, lds, c->stream>>>(A, c->cls);
