@@ -20,7 +20,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 LIB_DIR = os.path.join(HERE, "lib")
 BIN = os.path.join(HERE, "bin", "meshclust")
-GPU_LIB = os.path.join(LIB_DIR, "libmcgpu.so")
+GPU_LIB = os.environ.get("MC_GPU_LIB", os.path.join(LIB_DIR, "libmcgpu.so"))
 HOST_LIB = os.path.join(LIB_DIR, "libmeshclust.so")
 HEADER = os.path.join(ROOT, "include", "meshclust_amd.h")
 

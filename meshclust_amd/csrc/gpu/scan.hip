@@ -14,7 +14,9 @@
 // window [S, E] is read as nch perfectly coalesced 1 KiB-per-wave streams and each lane
 // accumulates its own candidate's SAD/dot in registers (no cross-lane reduction).  The
 // centre row sits in LDS and is read as a broadcast.
+#include <cstdio>
 #include <cstring>
+#include <vector>
 
 #include "features.hpp"
 
@@ -68,7 +70,26 @@ struct FusedArgs {
   uint64_t *msum;
   HostScan *hres;
   uint32_t seq;
+  uint64_t *stamps;  // diagnostic build only (MC_STAMPS): s_memrealtime at phase boundaries
 };
+
+#ifdef MC_STAMPS
+#define STAMP(i)                                                                       \
+  do {                                                                                 \
+    if (threadIdx.x == 0) atomicMax((unsigned long long *)&A.stamps[i], __builtin_amdgcn_s_memrealtime()); \
+  } while (0)
+#define STAMP_MIN(i)                                                                   \
+  do {                                                                                 \
+    if (threadIdx.x == 0) atomicMin((unsigned long long *)&A.stamps[i], __builtin_amdgcn_s_memrealtime()); \
+  } while (0)
+#else
+#define STAMP(i) \
+  do {           \
+  } while (0)
+#define STAMP_MIN(i) \
+  do {               \
+  } while (0)
+#endif
 
 __device__ __forceinline__ bool better(double v, uint64_t p, double bv, uint64_t bp) {
   return v > bv || (v == bv && p < bp);
@@ -82,6 +103,7 @@ __global__ __launch_bounds__(ST) void fused_scan_kernel(FusedArgs A, DevClassifi
   __shared__ double rv[ST / 64];
   __shared__ uint64_t rp[ST / 64];
   __shared__ int s_last;
+  STAMP_MIN(0);
   for (int c = threadIdx.x; c < A.nch; c += ST)
     clds[c] = reinterpret_cast<const uint4 *>(A.hist + (uint64_t)A.centre * A.pitch)[c];
   __syncthreads();
@@ -139,6 +161,7 @@ __global__ __launch_bounds__(ST) void fused_scan_kernel(FusedArgs A, DevClassifi
     rp[threadIdx.x >> 6] = best_p;
   }
   __syncthreads();  // also drains every wave's stores before the release below
+  STAMP(1);
   if (threadIdx.x == 0) {
     double v = rv[0];
     uint64_t p = rp[0];
@@ -160,6 +183,7 @@ __global__ __launch_bounds__(ST) void fused_scan_kernel(FusedArgs A, DevClassifi
   }
   __syncthreads();
   if (!s_last) return;
+  STAMP(2);
 
   // ---------------- last workgroup: get_close's reduction + get_mean -------------------
   double bv = -1.0;
@@ -185,6 +209,7 @@ __global__ __launch_bounds__(ST) void fused_scan_kernel(FusedArgs A, DevClassifi
     rp[threadIdx.x >> 6] = bp;
   }
   __syncthreads();
+  STAMP(3);
   const uint32_t nflag = __hip_atomic_load(&A.sd->nflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint32_t M = mbase + nflag;
   uint32_t new_id = 0xffffffffu;
@@ -205,7 +230,9 @@ __global__ __launch_bounds__(ST) void fused_scan_kernel(FusedArgs A, DevClassifi
     __syncthreads();
     if (lsum != A.msum)
       for (int b = threadIdx.x; b < A.B; b += ST) A.msum[b] = lsum[b];
+    STAMP(4);
     const uint64_t win = mean_closest_fast<T, ST>(R, A.mem_pos, A.mkeys, M, A.mag_s, A.B, A.nch, lsum, Fl);
+    STAMP(5);
     new_id = A.order[win];
   }
   if (threadIdx.x == 0) {
@@ -231,6 +258,7 @@ __global__ __launch_bounds__(ST) void fused_scan_kernel(FusedArgs A, DevClassifi
   }
   for (uint32_t q = threadIdx.x; q < nflag; q += ST) A.hres->flags[q] = A.flags_dev[q];
   __syncthreads();
+  STAMP(6);
   if (threadIdx.x == 0) {
     __threadfence_system();
     __hip_atomic_store(&A.hres->seq, A.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -303,6 +331,28 @@ int launch_fused_scan(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, uint32
   A.msum = (uint64_t *)c->msum.p;
   A.hres = c->h_res_dev;
   A.seq = seq;
+#ifdef MC_STAMPS
+  static uint64_t *stamps = nullptr;
+  static std::vector<double> acc(8, 0.0);
+  static uint64_t nacc = 0;
+  if (!stamps) (void)hipMalloc(&stamps, 64);
+  if (nacc) {  // fold the previous launch's stamps (it has completed: its result was consumed)
+    uint64_t h[8];
+    (void)hipMemcpy(h, stamps, 64, hipMemcpyDeviceToHost);
+    for (int i = 1; i < 7; i++) acc[i] += (double)(h[i] - h[0]) / 100.0;  // 100 MHz -> us
+    if (nacc % 500 == 0) {
+      fprintf(stderr, "[stamps] n=%llu avg us from first-wg start:", (unsigned long long)nacc);
+      for (int i = 1; i < 7; i++) fprintf(stderr, " %d:%.2f", i, acc[i] / nacc);
+      fprintf(stderr, "\n");
+    }
+  }
+  {
+    uint64_t init[8] = {~0ull, 0, 0, 0, 0, 0, 0, 0};
+    (void)hipMemcpy(stamps, init, 64, hipMemcpyHostToDevice);
+  }
+  nacc++;
+  A.stamps = stamps;
+#endif
   const size_t lds = (size_t)2 * nch * 16 + (c->B <= 4096 ? (size_t)c->B * 8 : 0);
   timed_begin(c);
   if (c->width == 1) fused_scan_kernel<uint8_t><<<grid, ST, lds, c->stream>>>(A, c->cls);

@@ -12,7 +12,7 @@ namespace {
 // accumulate (ClusterFactory.cpp:637-714): grow one cluster around `last` until get_close
 // finds no similar candidate; returns the next seed through *last_ptr.
 void accumulate(uint32_t *last_ptr, const Dataset &ds, mc_ctx *ctx, BVec &bv, std::vector<Center> &centers,
-                const ClusterConfig &cfg, ClusterStats &stats, std::vector<uint32_t> &flag_buf) {
+                const ClusterConfig &cfg, ClusterStats &stats, std::vector<uint32_t> &flag_buf, PhaseTimer &timer) {
   uint32_t last = *last_ptr;
   std::vector<uint32_t> current = {last};
   check(mc_cluster_begin(ctx, last), "mc_cluster_begin");
@@ -26,6 +26,7 @@ void accumulate(uint32_t *last_ptr, const Dataset &ds, mc_ctx *ctx, BVec &bv, st
     if (count > 0) {
       stats.scan_steps++;
       stats.scan_candidates += (uint64_t)count;
+      Scope sc(timer, "accumulate.mc_scan");
       check(mc_scan(ctx, last, S, E, flag_buf.data(), flag_buf.size(), &res), "mc_scan");
     } else {  // the OpenMP loop runs no iteration: result NULL, is_min stays true
       res.is_min = 1;
@@ -64,7 +65,7 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
     Scope s(timer, "accumulate");
     uint32_t last = bv.pop();
     if (last != BVec::NONE) check(mc_kill(ctx, bv.spos(last)), "mc_kill");
-    while (last != BVec::NONE) accumulate(&last, ds, ctx, bv, part, cfg, stats, flag_buf);
+    while (last != BVec::NONE) accumulate(&last, ds, ctx, bv, part, cfg, stats, flag_buf, timer);
   }
   Scope s(timer, "update+merge");
   for (int it = 0; it < cfg.iterations; it++) {
