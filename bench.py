@@ -164,6 +164,13 @@ def main():
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
                 "bytes_per_eval": eval_bytes, "evals_per_launch": round(scan_evals / fam_n["scan"], 1),
                 "avg_launch_us": round(avg_s * 1e6, 2)}
+        pmc = os.path.join(ROOT, "profiles", "pmc_latest.json")
+        if os.path.exists(pmc):  # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (scripts/pmc_summary.py)
+            e = json.load(open(pmc)).get("fused_scan_kernel<unsigned char>")
+            if e and "hbm_bytes_per_dispatch" in e:
+                roof["traffic"] = round(e["hbm_bytes_per_dispatch"])
+                roof["traffic_unit"] = "bytes/launch (FETCH_SIZE x2 + WRITE_SIZE, profiles/pmc_latest.json)"
+                roof["algorithmic_bytes_per_launch"] = round(per_launch_bytes)
     nw_cells = sum(s["nw_cells"] for s in stats)
     nw_rate = nw_cells / (fam_ms["nw"] / 1e3) if fam_ms["nw"] else None
     cpu = None
