@@ -76,6 +76,8 @@ typedef struct mc_scan_result {
   uint64_t n_flagged;   /* candidates marked similar (removed from the window)         */
   uint32_t new_centre;  /* get_mean's argmin distance_d over the cluster (if !is_min)  */
   uint32_t n_members;   /* cluster size after this step                                */
+  uint64_t nw_pairs;    /* alignment mode: NW alignments run for this step (else 0)    */
+  uint64_t nw_cells;    /* alignment mode: their DP cells, sum of len1 * len2          */
 } mc_scan_result;
 
 typedef struct mc_ctx mc_ctx;
@@ -183,6 +185,37 @@ int mc_scan(mc_ctx *ctx, uint32_t centre_id, uint64_t S, uint64_t E, uint32_t *f
  */
 int mc_mean_shift(mc_ctx *ctx, const uint32_t *centre_ids, uint32_t C, const uint64_t *member_off,
                   const uint32_t *members, int delta, uint32_t *new_centre);
+
+/*
+ * ---- alignment mode (--align, or --id < 0.6: Runner.cpp:32-34, 332) ---------------------
+ * The trainer then installs a classifier whose only feature is MC_FEAT_ALIGN (identity of
+ * utility::GlobAlignE, normalised with min 0 / max 1, weights {-cutoff, 1}; Trainer.cpp:
+ * 570-577, Feature.cpp:90-95).  With such a classifier:
+ *   - mc_scan runs the batched NW kernel of every alive window candidate (seq1) against the
+ *     centre (seq2) -- Feature::align(*pt, *p) inside Trainer::get_close -- and classifies
+ *     the identities; remove_available + get_mean are unchanged (k-mer histograms).
+ *   - mc_classify_pairs / mc_mean_shift are not available (their pairs go through the
+ *     reference's Feature::align memo, which the host replays): use mc_nw_identity +
+ *     mc_classify_values + mc_mean_shift_select instead.
+ */
+
+/*
+ * Classify precomputed single-feature values: raw[i * n_single + f] is feature lookup[f] of
+ * pair i (Feature::compute_all_raw, Feature.cpp:54-84).  Same normalisation, combos, fma GLM
+ * sum and decision as mc_classify_pairs.  Any output pointer may be NULL.
+ */
+int mc_classify_values(mc_ctx *ctx, const double *raw, uint64_t m, uint8_t *similar, double *combo0,
+                       double *sum);
+
+/*
+ * mean_shift_update (ClusterFactory.cpp:289-380) with the Trainer::filter decision supplied
+ * by the caller: for centre j the neighbourhood is members[member_off[b_j] .. member_off[e_j+1])
+ * (b_j = max(0, j-delta), e_j = min(C-1, j+delta)); keep holds one byte per neighbourhood
+ * entry, neighbourhoods concatenated in j order.  new_centre[j] = the first kept member
+ * closest (distance_d) to the kept members' mean, or centre_ids[j] if none is kept.
+ */
+int mc_mean_shift_select(mc_ctx *ctx, const uint32_t *centre_ids, uint32_t C, const uint64_t *member_off,
+                         const uint32_t *members, int delta, const uint8_t *keep, uint32_t *new_centre);
 
 /* Device time (ms) accumulated per kernel family since the last reset (diagnostics). */
 int mc_timers(mc_ctx *ctx, double *ms_out, int n, int reset);

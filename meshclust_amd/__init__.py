@@ -63,6 +63,8 @@ class ScanResult(C.Structure):
         ("n_flagged", C.c_uint64),
         ("new_centre", C.c_uint32),
         ("n_members", C.c_uint32),
+        ("nw_pairs", C.c_uint64),
+        ("nw_cells", C.c_uint64),
     ]
 
 
@@ -86,7 +88,7 @@ def gpu_lib():
         for name in ("mc_load_sequences", "mc_kmer_max", "mc_kmer_build", "mc_get_histograms", "mc_distance_keys",
                      "mc_pair_features", "mc_set_classifier", "mc_classify_pairs", "mc_nw_identity",
                      "mc_nw_identity_raw", "mc_set_order", "mc_kill", "mc_cluster_begin", "mc_scan",
-                     "mc_mean_shift", "mc_timers"):
+                     "mc_mean_shift", "mc_timers", "mc_classify_values", "mc_mean_shift_select"):
             getattr(lib, name).restype = C.c_int
         _gpu = lib
     return _gpu
@@ -194,6 +196,27 @@ class Engine:
         _check(self.lib.mc_classify_pairs(self.ctx, _p(a), _p(b), C.c_uint64(len(a)), _p(sim), _p(c0), _p(s)),
                "mc_classify_pairs")
         return sim, c0, s
+
+    def classify_values(self, raw):
+        """raw: (m, n_single) precomputed single-feature values -> (similar, combo0, sum)."""
+        raw = np.ascontiguousarray(raw, np.float64)
+        m = raw.shape[0]
+        sim = np.zeros(m, np.uint8)
+        c0 = np.zeros(m)
+        s = np.zeros(m)
+        _check(self.lib.mc_classify_values(self.ctx, _p(raw), C.c_uint64(m), _p(sim), _p(c0), _p(s)),
+               "mc_classify_values")
+        return sim, c0, s
+
+    def mean_shift_select(self, centres, member_off, members, delta, keep):
+        centres = np.ascontiguousarray(centres, np.uint32)
+        member_off = np.ascontiguousarray(member_off, np.uint64)
+        members = np.ascontiguousarray(members, np.uint32)
+        keep = np.ascontiguousarray(keep, np.uint8)
+        out = np.zeros(len(centres), np.uint32)
+        _check(self.lib.mc_mean_shift_select(self.ctx, _p(centres), len(centres), _p(member_off), _p(members), delta,
+                                             _p(keep), _p(out)), "mc_mean_shift_select")
+        return out
 
     def nw_identity(self, a, b):
         a = np.ascontiguousarray(a, np.uint32)

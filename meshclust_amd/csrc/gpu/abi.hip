@@ -166,7 +166,7 @@ int mc_ctx_destroy(mc_ctx *c) {
   for (Buf *b : {&c->codes, &c->seq_off, &c->seg, &c->seg_off, &c->hist, &c->mag, &c->sumsq, &c->len, &c->order,
                  &c->alive, &c->members, &c->member_keys, &c->partials, &c->scan_dev, &c->flags_out, &c->s_a, &c->s_b,
                  &c->s_c, &c->s_d, &c->s_e, &c->s_f, &c->s_g, &c->hs, &c->mag_s, &c->sumsq_s, &c->len_s, &c->ticket,
-                 &c->msum})
+                 &c->msum, &c->ident_s, &c->al_a, &c->al_b, &c->al_out})
     release(*b);
   if (c->h_scan) (void)hipHostFree(c->h_scan);
   if (c->h_res) (void)hipHostFree(c->h_res);
@@ -300,19 +300,30 @@ int mc_set_classifier(mc_ctx *c, const mc_classifier *cls) {
   if (!c || !cls) return MC_ERR_ARG;
   if (cls->n_single < 1 || cls->n_single > MC_MAX_SINGLE || cls->n_combo < 1 || cls->n_combo > MC_MAX_COMBO)
     return MC_ERR_ARG;
+  bool align = false;
   for (int i = 0; i < cls->n_single; i++)
-    if (cls->lookup[i] == MC_FEAT_ALIGN) {
-      set_error("alignment-feature classifiers are not supported by the k-mer kernels");
-      return MC_ERR_ARG;
-    }
+    if (cls->lookup[i] == MC_FEAT_ALIGN) align = true;
+  // the reference only ever uses ALIGN alone (Trainer.cpp:570-577)
+  if (align && (cls->n_single != 1 || cls->n_combo != 1 || cls->combo_len[0] != 1)) {
+    set_error("MC_FEAT_ALIGN must be the only feature of an alignment-mode classifier");
+    return MC_ERR_ARG;
+  }
   c->cls.c = *cls;
+  c->cls.align = align ? 1 : 0;
   c->has_cls = true;
   return MC_OK;
+}
+
+static int no_align(mc_ctx *c, const char *what) {
+  if (!c->cls.align) return MC_OK;
+  set_error(std::string(what) + " is not available in alignment mode (see include/meshclust_amd.h)");
+  return MC_ERR_STATE;
 }
 
 int mc_classify_pairs(mc_ctx *c, const uint32_t *a, const uint32_t *b, uint64_t m, uint8_t *similar, double *combo0,
                       double *sum) {
   if (!c || c->k == 0 || !c->has_cls) return MC_ERR_STATE;
+  TRY(no_align(c, "mc_classify_pairs"));
   MCG_CHECK(hipSetDevice(c->device));
   TRY(check_ids(c, a, m));
   TRY(check_ids(c, b, m));
@@ -368,11 +379,7 @@ int mc_nw_identity_raw(mc_ctx *c, const uint8_t *a, const uint64_t *a_off, const
   for (uint64_t i = 0; i < m; i++) {
     la[i] = a_off[i + 1] - a_off[i];
     lb[i] = b_off[i + 1] - b_off[i];
-    idx[i] = (uint32_t)i;
-    if (la[i] == 0 || lb[i] == 0) {
-      set_error("empty sequence in NW pair");
-      return MC_ERR_ARG;
-    }
+    idx[i] = (uint32_t)i;  // empty strings are allowed (GlobAlignE with len1 or len2 == 1)
   }
   // one scratch region: A bytes | B bytes | offsets | indices | outputs
   const size_t abytes = (a_off[m] - a_off[0] + 15) / 16 * 16, bbytes = (b_off[m] - b_off[0] + 15) / 16 * 16;
@@ -418,6 +425,8 @@ int mc_set_order(mc_ctx *c, const uint32_t *order, uint64_t n) {
   c->norder = n;
   c->h_spos.assign(n, 0);
   for (uint64_t p = 0; p < n; p++) c->h_spos[order[p]] = p;
+  c->h_order.assign(order, order + n);
+  c->h_alive.assign(n, 1);
   TRY(upload(c->order, order, n, c->stream));
   TRY(ensure(c->alive, n + 16));
   MCG_CHECK(hipMemsetAsync(c->alive.p, 1, n, c->stream));
@@ -458,6 +467,7 @@ int mc_set_order(mc_ctx *c, const uint32_t *order, uint64_t n) {
 
 int mc_kill(mc_ctx *c, uint64_t pos) {
   if (!c || pos >= c->norder) return MC_ERR_ARG;
+  c->h_alive[pos] = 0;
   if (fused(c)) {  // applied by the next scan launch (which also excludes it from its window)
     if (c->pending_kills.size() == 8) {
       for (uint64_t p : c->pending_kills) MCG_CHECK(hipMemsetAsync((uint8_t *)c->alive.p + p, 0, 1, c->stream));
@@ -512,16 +522,57 @@ static int wait_seq(mc_ctx *c, uint32_t seq) {
   }
 }
 
+// Alignment mode, first half of a get_close step: Feature::align(*pt, *p) (Feature.cpp:
+// 221-243; GlobAlignE with the candidate as seq1 and the centre as seq2) for every alive
+// candidate of the window, written to ident_s[static position].  Within accumulation the
+// reference's memo never changes a value: a centre is never alive again, so a (candidate,
+// centre) pair can only recur in the same orientation (see cluster.cpp, AlignMemo).
+static int align_window(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, uint64_t *pairs, uint64_t *cells) {
+  std::vector<uint32_t> ai, bi, out;
+  std::vector<uint64_t> la, lb;
+  const uint64_t lc = c->h_seq_off[centre + 1] - c->h_seq_off[centre];
+  uint64_t cl = 0;
+  for (uint64_t pos = S; pos <= E; pos++) {
+    if (!c->h_alive[pos]) continue;
+    const uint32_t id = c->h_order[pos];
+    const uint64_t l = c->h_seq_off[id + 1] - c->h_seq_off[id];
+    ai.push_back(id);
+    bi.push_back(centre);
+    out.push_back((uint32_t)pos);
+    la.push_back(l);
+    lb.push_back(lc);
+    cl += l * lc;
+  }
+  *pairs = ai.size();
+  *cells = cl;
+  TRY(ensure(c->ident_s, c->norder * 8 + 16));
+  if (ai.empty()) return MC_OK;
+  TRY(upload(c->al_a, ai.data(), ai.size(), c->stream));
+  TRY(upload(c->al_b, bi.data(), bi.size(), c->stream));
+  TRY(upload(c->al_out, out.data(), out.size(), c->stream));
+  return launch_nw(c, (uint8_t *)c->codes.p, (uint64_t *)c->seq_off.p, (uint32_t *)c->al_a.p, (uint8_t *)c->codes.p,
+                   (uint64_t *)c->seq_off.p, (uint32_t *)c->al_b.p, ai.size(), la, lb, (double *)c->ident_s.p, nullptr,
+                   nullptr, nullptr, (uint32_t *)c->al_out.p);
+}
+
 int mc_scan(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, uint32_t *flagged_pos, uint64_t cap,
             mc_scan_result *res) {
   if (!c || !res || !c->has_cls || c->norder == 0) return MC_ERR_STATE;
   if (S > E || E >= c->norder || centre >= c->n) return MC_ERR_ARG;
   c->step++;
+  uint64_t nw_pairs = 0, nw_cells = 0;
+  const double *d_ident = nullptr;
+  if (c->cls.align) {
+    TRY(align_window(c, centre, S, E, &nw_pairs, &nw_cells));
+    d_ident = (const double *)c->ident_s.p;
+  }
   if (fused(c)) {
     const uint32_t seq = ++c->seq;
-    TRY(launch_fused_scan(c, centre, S, E, seq));
+    TRY(launch_fused_scan(c, centre, S, E, seq, d_ident));
     TRY(wait_seq(c, seq));
     *res = c->h_res->r;
+    res->nw_pairs = nw_pairs;
+    res->nw_cells = nw_cells;
     const uint64_t nf = res->n_flagged;
     if (nf > cap) {
       set_error("flagged buffer too small");
@@ -529,6 +580,7 @@ int mc_scan(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, uint32_t *flagge
     }
     memcpy(flagged_pos, c->h_res->flags, nf * 4);
     std::sort(flagged_pos, flagged_pos + nf);
+    for (uint64_t i = 0; i < nf; i++) c->h_alive[flagged_pos[i]] = 0;
     if (c->ev_pending.size() > 512) {
       MCG_CHECK(hipStreamSynchronize(c->stream));
       flush_timers(c);
@@ -536,12 +588,14 @@ int mc_scan(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, uint32_t *flagge
     return MC_OK;
   }
   int nblocks = 0;
-  TRY(launch_scan(c, centre, S, E, &nblocks));
+  TRY(launch_scan(c, centre, S, E, d_ident, &nblocks));
   TRY(launch_finalize(c, nblocks));
   MCG_CHECK(hipMemcpyAsync(c->h_scan, c->scan_dev.p, c->h_scan_cap, hipMemcpyDeviceToHost, c->stream));
   MCG_CHECK(hipStreamSynchronize(c->stream));
   flush_timers(c);
   *res = c->h_scan->r;
+  res->nw_pairs = nw_pairs;
+  res->nw_cells = nw_cells;
   const uint64_t nf = res->n_flagged;
   if (nf > cap) {
     set_error("flagged buffer too small");
@@ -557,12 +611,33 @@ int mc_scan(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, uint32_t *flagge
     flush_timers(c);
   }
   std::sort(flagged_pos, flagged_pos + nf);
+  for (uint64_t i = 0; i < nf; i++) c->h_alive[flagged_pos[i]] = 0;
   return MC_OK;
 }
 
-int mc_mean_shift(mc_ctx *c, const uint32_t *centre_ids, uint32_t C, const uint64_t *member_off, const uint32_t *members,
-                  int delta, uint32_t *new_centre) {
-  if (!c || !c->has_cls || delta < 0) return MC_ERR_STATE;
+int mc_classify_values(mc_ctx *c, const double *raw, uint64_t m, uint8_t *similar, double *combo0, double *sum) {
+  if (!c || !c->has_cls) return MC_ERR_STATE;
+  if (m == 0) return MC_OK;
+  if (!raw) return MC_ERR_ARG;
+  MCG_CHECK(hipSetDevice(c->device));
+  const int ns = c->cls.c.n_single;
+  TRY(upload(c->s_a, raw, m * ns, c->stream));
+  TRY(ensure(c->s_c, m * 17 + 64));
+  uint8_t *d_sim = (uint8_t *)c->s_c.p;
+  double *d_c0 = (double *)((char *)c->s_c.p + (m + 15) / 16 * 16);
+  double *d_sum = d_c0 + m;
+  TRY(launch_values(c, (const double *)c->s_a.p, m, d_sim, d_c0, d_sum));
+  if (similar) TRY(download(similar, d_sim, m, c->stream));
+  if (combo0) TRY(download(combo0, d_c0, m, c->stream));
+  if (sum) TRY(download(sum, d_sum, m, c->stream));
+  MCG_CHECK(hipStreamSynchronize(c->stream));
+  flush_timers(c);
+  return MC_OK;
+}
+
+static int mean_shift_common(mc_ctx *c, const uint32_t *centre_ids, uint32_t C, const uint64_t *member_off,
+                             const uint32_t *members, int delta, const uint8_t *keep, uint32_t *new_centre) {
+  if (!c || !c->has_cls || c->k == 0 || delta < 0) return MC_ERR_STATE;
   if (C == 0) return MC_OK;
   MCG_CHECK(hipSetDevice(c->device));
   TRY(check_ids(c, centre_ids, C));
@@ -571,14 +646,37 @@ int mc_mean_shift(mc_ctx *c, const uint32_t *centre_ids, uint32_t C, const uint6
   TRY(upload(c->s_a, centre_ids, C, c->stream));
   TRY(upload(c->s_b, member_off, C + 1, c->stream));
   TRY(upload(c->s_c, members, nm, c->stream));
-  // output goes to the tail of s_a
+  const uint8_t *d_keep = nullptr;
+  if (keep) {
+    uint64_t nk = 0;
+    for (uint32_t j = 0; j < C; j++) {
+      const uint32_t b = j >= (uint32_t)delta ? j - delta : 0;
+      const uint32_t e = std::min<uint32_t>(j + delta, C - 1);
+      nk += member_off[e + 1] - member_off[b];
+    }
+    TRY(upload(c->al_out, keep, nk, c->stream));
+    d_keep = (const uint8_t *)c->al_out.p;
+  }
   TRY(ensure(c->flags_out, (size_t)C * 4 + 16));
   TRY(launch_mean_shift(c, (uint32_t *)c->s_a.p, C, (uint64_t *)c->s_b.p, member_off, (uint32_t *)c->s_c.p, delta,
-                        (uint32_t *)c->flags_out.p));
+                        d_keep, (uint32_t *)c->flags_out.p));
   TRY(download(new_centre, c->flags_out.p, C, c->stream));
   MCG_CHECK(hipStreamSynchronize(c->stream));
   flush_timers(c);
   return MC_OK;
+}
+
+int mc_mean_shift(mc_ctx *c, const uint32_t *centre_ids, uint32_t C, const uint64_t *member_off, const uint32_t *members,
+                  int delta, uint32_t *new_centre) {
+  if (!c) return MC_ERR_ARG;
+  TRY(no_align(c, "mc_mean_shift"));
+  return mean_shift_common(c, centre_ids, C, member_off, members, delta, nullptr, new_centre);
+}
+
+int mc_mean_shift_select(mc_ctx *c, const uint32_t *centre_ids, uint32_t C, const uint64_t *member_off,
+                         const uint32_t *members, int delta, const uint8_t *keep, uint32_t *new_centre) {
+  if (!c || !keep) return MC_ERR_ARG;
+  return mean_shift_common(c, centre_ids, C, member_off, members, delta, keep, new_centre);
 }
 
 int mc_timers(mc_ctx *c, double *ms_out, int n, int reset) {

@@ -126,6 +126,24 @@ __global__ __launch_bounds__(NT) void pairs_kernel(HistView H, DevClassifier C, 
   }
 }
 
+// -------------------------------------------------------------------- precomputed values
+// normalize_cache + operator() + GLM decision of pairs whose single-feature values are given
+// (alignment mode: identities looked up through the host's replay of Feature::align's memo).
+__global__ __launch_bounds__(NT) void values_kernel(DevClassifier C, const double *__restrict__ raw_in, uint64_t m,
+                                                    uint8_t *sim, double *c0_out, double *sum_out) {
+  const int ns = C.c.n_single;
+  for (uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x; i < m; i += (uint64_t)gridDim.x * NT) {
+    double raw[MC_MAX_SINGLE];
+#pragma unroll
+    for (int f = 0; f < MC_MAX_SINGLE; f++) raw[f] = f < ns ? raw_in[i * ns + f] : 0.0;
+    double c0, sum;
+    const int d = classify_raw(C, raw, &c0, &sum);
+    if (sim) sim[i] = (uint8_t)d;
+    if (c0_out) c0_out[i] = c0;
+    if (sum_out) sum_out[i] = sum;
+  }
+}
+
 // -------------------------------------------------------------------- accumulation scan
 __device__ __forceinline__ bool better(double v, uint64_t p, double bv, uint64_t bp) {
   return v > bv || (v == bv && p < bp);
@@ -136,7 +154,8 @@ __global__ __launch_bounds__(NT) void scan_kernel(HistView H, DevClassifier C, c
                                                   uint8_t *__restrict__ alive, uint32_t centre, uint64_t S, uint64_t E,
                                                   ScanPartial *__restrict__ partials, ScanDev *__restrict__ sd,
                                                   uint32_t *__restrict__ flags_out, uint32_t *__restrict__ members,
-                                                  uint64_t *__restrict__ mkeys, uint32_t step) {
+                                                  uint64_t *__restrict__ mkeys, uint32_t step,
+                                                  const double *__restrict__ ident) {
   extern __shared__ __attribute__((aligned(16))) uint4 clds[];
   __shared__ double rv[NT / 64];
   __shared__ uint64_t rp[NT / 64];
@@ -152,11 +171,17 @@ __global__ __launch_bounds__(NT) void scan_kernel(HistView H, DevClassifier C, c
     const uint64_t pos = S + base + threadIdx.x;
     const bool valid = (base + threadIdx.x < W) && alive[pos];
     const uint32_t id = valid ? order[pos] : 0;
-    PS s = wave_pair_stats<T>(H, id, centre, valid, clds, pc.mag);
+    PS s{0, 0, 0};
+    if (!ident) s = wave_pair_stats<T>(H, id, centre, valid, clds, pc.mag);  // uniform branch
     if (valid) {
       const PInfo pi = pinfo(H, id);
       double raw[MC_MAX_SINGLE];
-      raw_lookup<T>(H, C.c, s, id, centre, pi, pc, raw);  // feat->compute(*pt, *p): candidate first
+      if (ident) {  // alignment mode: Feature::align(*pt, *p) computed by the NW kernel
+        raw[0] = ident[pos];
+        for (int i = 1; i < MC_MAX_SINGLE; i++) raw[i] = 0;
+      } else {
+        raw_lookup<T>(H, C.c, s, id, centre, pi, pc, raw);  // feat->compute(*pt, *p): candidate first
+      }
       double c0;
       int d = classify_raw(C, raw, &c0, nullptr);
       if (better(c0, pos, best_v, best_p) && c0 > -1.0) {
@@ -349,7 +374,7 @@ __global__ __launch_bounds__(NT) void mean_shift_kernel(HistView H, DevClassifie
                                                         const uint32_t *__restrict__ mem, int delta,
                                                         const uint64_t *__restrict__ soff, uint32_t *__restrict__ kept,
                                                         uint32_t *__restrict__ nkept, double *__restrict__ gmean,
-                                                        uint32_t *__restrict__ newc) {
+                                                        const uint8_t *__restrict__ keep, uint32_t *__restrict__ newc) {
   extern __shared__ __attribute__((aligned(16))) uint4 dyn[];
   __shared__ uint32_t cnt;
   const uint32_t j = blockIdx.x;
@@ -370,14 +395,18 @@ __global__ __launch_bounds__(NT) void mean_shift_kernel(HistView H, DevClassifie
     const uint64_t q = base + threadIdx.x;
     const bool valid = q < hi;
     const uint32_t id = valid ? mem[q] : 0;
-    PS s = wave_pair_stats<T>(H, id, centre, valid, clds, pc.mag);
     int d = 0;
-    if (valid) {
-      const PInfo pi = pinfo(H, id);
-      double raw[MC_MAX_SINGLE];
-      raw_lookup<T>(H, C.c, s, id, centre, pi, pc, raw);
-      double c0;
-      d = classify_raw(C, raw, &c0, nullptr);
+    if (keep) {  // filter decision supplied by the caller (alignment mode)
+      d = valid ? keep[soff[j] + (q - lo)] : 0;
+    } else {
+      PS s = wave_pair_stats<T>(H, id, centre, valid, clds, pc.mag);
+      if (valid) {
+        const PInfo pi = pinfo(H, id);
+        double raw[MC_MAX_SINGLE];
+        raw_lookup<T>(H, C.c, s, id, centre, pi, pc, raw);
+        double c0;
+        d = classify_raw(C, raw, &c0, nullptr);
+      }
     }
     // ordered compaction within the workgroup: wave prefix via ballot, waves in order
     __shared__ uint32_t wcount[NT / 64];
@@ -471,7 +500,17 @@ int launch_pairs(mc_ctx *c, const uint32_t *d_a, const uint32_t *d_b, uint64_t m
   return MC_OK;
 }
 
-int launch_scan(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, int *nblocks) {
+int launch_values(mc_ctx *c, const double *d_raw, uint64_t m, uint8_t *d_sim, double *d_c0, double *d_sum) {
+  if (m == 0) return MC_OK;
+  const int grid = grid_for(m, NT, 4096);
+  timed_begin(c);
+  values_kernel<<<grid, NT, 0, c->stream>>>(c->cls, d_raw, m, d_sim, d_c0, d_sum);
+  MCG_CHECK(hipGetLastError());
+  timed_end(c, F_PAIRS);
+  return MC_OK;
+}
+
+int launch_scan(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, const double *d_ident, int *nblocks) {
   const HistView H = hist_view(c);
   const int nch = (int)((H.B * H.width + 15) / 16);
   const uint64_t W = E - S + 1;
@@ -483,7 +522,7 @@ int launch_scan(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, int *nblocks
   MCG_DISPATCH_T(c->width, (scan_kernel<T><<<grid, NT, (size_t)nch * 16, c->stream>>>(
                                H, c->cls, (const uint32_t *)c->order.p, (uint8_t *)c->alive.p, centre, S, E,
                                (ScanPartial *)c->partials.p, sd, flags, (uint32_t *)c->members.p,
-                               (uint64_t *)c->member_keys.p, c->step)));
+                               (uint64_t *)c->member_keys.p, c->step, d_ident)));
   MCG_CHECK(hipGetLastError());
   timed_end(c, F_SCAN);
   return MC_OK;
@@ -504,7 +543,7 @@ int launch_finalize(mc_ctx *c, int nblocks) {
 }
 
 int launch_mean_shift(mc_ctx *c, const uint32_t *d_cid, uint32_t C, const uint64_t *d_off, const uint64_t *h_off,
-                      const uint32_t *d_mem, int delta, uint32_t *d_new) {
+                      const uint32_t *d_mem, int delta, const uint8_t *d_keep, uint32_t *d_new) {
   if (C == 0) return MC_OK;
   const HistView H = hist_view(c);
   const int nch = (int)((H.B * H.width + 15) / 16);
@@ -524,7 +563,7 @@ int launch_mean_shift(mc_ctx *c, const uint32_t *d_cid, uint32_t C, const uint64
   timed_begin(c);
   MCG_DISPATCH_T(c->width, (mean_shift_kernel<T><<<C, NT, lds, c->stream>>>(
                                H, c->cls, d_cid, C, d_off, d_mem, delta, (const uint64_t *)c->s_d.p,
-                               (uint32_t *)c->s_e.p, (uint32_t *)c->s_f.p, (double *)c->s_g.p, d_new)));
+                               (uint32_t *)c->s_e.p, (uint32_t *)c->s_f.p, (double *)c->s_g.p, d_keep, d_new)));
   MCG_CHECK(hipGetLastError());
   timed_end(c, F_MSHIFT);
   return MC_OK;

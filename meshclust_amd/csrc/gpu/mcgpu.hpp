@@ -26,6 +26,7 @@ enum Family { F_KMER = 0, F_KEYS, F_PAIRS, F_SCAN, F_FINAL, F_MSHIFT, F_NW, F_NF
 struct DevClassifier {
   mc_classifier c;
   double thr;  // round(1/(1+exp(-sum))) == 1  <=>  sum >= thr   (host glibc exp, see abi.hip)
+  int align;   // the only feature is MC_FEAT_ALIGN: raw[0] is an NW identity (Trainer.cpp:570-577)
 };
 
 // Read-only view of the device histogram matrix passed to kernels by value.
@@ -98,6 +99,11 @@ struct mc_ctx {
   bool pending_begin = false;
   uint64_t pending_first_pos = 0;
   std::vector<uint64_t> h_spos;  // id -> static position
+  // alignment mode: host mirror of order/alive (builds the NW pair list of a window) and the
+  // per-static-position identity the scan kernels classify
+  std::vector<uint32_t> h_order;
+  std::vector<uint8_t> h_alive;
+  mcg::Buf ident_s, al_a, al_b, al_out;
   // scratch
   mcg::Buf s_a, s_b, s_c, s_d, s_e, s_f, s_g;
   std::vector<void *> pinned;
@@ -127,17 +133,19 @@ int launch_distance_keys(mc_ctx *c, const uint32_t *d_piv, uint32_t npiv, const 
                          uint16_t *d_keys);
 int launch_pairs(mc_ctx *c, const uint32_t *d_a, const uint32_t *d_b, uint64_t m, const uint16_t *flags, int nflag,
                  double *d_raw, uint8_t *d_sim, double *d_c0, double *d_sum, bool classify);
-int launch_scan(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, int *nblocks);
+int launch_scan(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, const double *d_ident, int *nblocks);
+int launch_values(mc_ctx *c, const double *d_raw, uint64_t m, uint8_t *d_sim, double *d_c0, double *d_sum);
 int launch_finalize(mc_ctx *c, int nblocks);
 int launch_mean_shift(mc_ctx *c, const uint32_t *d_cid, uint32_t C, const uint64_t *d_off, const uint64_t *h_off,
-                      const uint32_t *d_mem, int delta, uint32_t *d_new);
+                      const uint32_t *d_mem, int delta, const uint8_t *d_keep, uint32_t *d_new);
 int build_static(mc_ctx *c);
-int launch_fused_scan(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, uint32_t seq);
+int launch_fused_scan(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, uint32_t seq, const double *d_ident);
 // NW on byte strings: pair p aligns A[aoff[ai[p]] .. aoff[ai[p]+1]) against B[...] (rows = A).
+// Results go to slot p, or to slot d_out[p] when d_out is given.
 int launch_nw(mc_ctx *c, const uint8_t *d_A, const uint64_t *d_aoff, const uint32_t *d_ai, const uint8_t *d_B,
               const uint64_t *d_boff, const uint32_t *d_bi, uint64_t m, const std::vector<uint64_t> &h_alen,
               const std::vector<uint64_t> &h_blen, double *d_ident, int32_t *d_len, int32_t *d_ids,
-              int32_t *d_score);
+              int32_t *d_score, const uint32_t *d_out = nullptr);
 
 }  // namespace mcg
 

@@ -60,6 +60,7 @@ struct NWPairs {
   int32_t *len;
   int32_t *ids;
   int32_t *score;
+  const uint32_t *out;  // optional result slot per pair (else the pair index)
 };
 
 template <int R, typename P>
@@ -252,18 +253,24 @@ __global__ __launch_bounds__(64) void nw_kernel(NWPairs q) {
   const int owner = la == 0 ? 0 : fl / R;
   if (lane == owner) {
     int L, I;
-    if (la == 0) {  // no rows: alignmentScore = max(matches[0], ...) at the initial state
-      L = 0;
+    if (la == 0) {
+      // no rows (len1 == 1): only cell 0 of each state row exists.  With columns
+      // (lb > 0) every j leaves matches[0] = lowerGap[0] = -inf, matchLen[0] = j and
+      // upperGap[0] = -inf untouched, so the final max picks `matches` (GlobAlignE.cpp:
+      // 244-251, 278-283): score -inf, length lb, 0 identities.  Without columns the
+      // initial state (0, 0, 0) is the answer and the identity is 0/0.
+      L = lb;
       I = 0;
-      fin_score = 0;
+      fin_score = lb > 0 ? NINF : 0;
     } else {
       L = (int)(fin_pay >> SH);
       I = (int)(fin_pay & (((P)1 << SH) - 1));
     }
-    q.ident[p] = (double)I / (double)L;
-    if (q.len) q.len[p] = L;
-    if (q.ids) q.ids[p] = I;
-    if (q.score) q.score[p] = fin_score;
+    const uint32_t o = q.out ? q.out[p] : p;
+    q.ident[o] = (double)I / (double)L;
+    if (q.len) q.len[o] = L;
+    if (q.ids) q.ids[o] = I;
+    if (q.score) q.score[o] = fin_score;
   }
 }
 
@@ -280,7 +287,7 @@ int launch_bucket(mc_ctx *c, NWPairs q) {
 int launch_nw(mc_ctx *c, const uint8_t *d_A, const uint64_t *d_aoff, const uint32_t *d_ai, const uint8_t *d_B,
               const uint64_t *d_boff, const uint32_t *d_bi, uint64_t m, const std::vector<uint64_t> &alen,
               const std::vector<uint64_t> &blen, double *d_ident, int32_t *d_len, int32_t *d_ids,
-              int32_t *d_score) {
+              int32_t *d_score, const uint32_t *d_out) {
   if (m == 0) return MC_OK;
   // bucket pairs by rows per lane and payload width; boundary scratch for multi-block pairs
   enum { NB = 8 };
@@ -315,7 +322,7 @@ int launch_nw(mc_ctx *c, const uint8_t *d_A, const uint64_t *d_aoff, const uint3
     MCG_CHECK(hipMemcpyAsync((uint64_t *)c->s_b.p + io, boff[k].data(), boff[k].size() * 8, hipMemcpyHostToDevice,
                              c->stream));
     NWPairs q{d_A, d_aoff, d_ai, d_B, d_boff, d_bi, (uint32_t *)c->s_a.p + io, (uint32_t)bucket[k].size(),
-              (int *)c->s_c.p, (uint64_t *)c->s_b.p + io, d_ident, d_len, d_ids, d_score};
+              (int *)c->s_c.p, (uint64_t *)c->s_b.p + io, d_ident, d_len, d_ids, d_score, d_out};
     int rc = MC_OK;
     switch (k) {
       case 0: rc = launch_bucket<4, uint32_t>(c, q); break;

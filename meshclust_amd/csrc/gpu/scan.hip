@@ -71,6 +71,7 @@ struct FusedArgs {
   HostScan *hres;
   uint32_t seq;
   uint64_t *stamps;  // diagnostic build only (MC_STAMPS): s_memrealtime at phase boundaries
+  const double *ident;  // alignment mode: NW identity per static position (else null)
 };
 
 #ifdef MC_STAMPS
@@ -115,24 +116,30 @@ __global__ __launch_bounds__(ST) void fused_scan_kernel(FusedArgs A, DevClassifi
   double best_v = -1.0;  // get_close's initializer (NULL, -1, 0, 0) with a strict `>`
   uint64_t best_p = ~0ull;
   if (valid) {
-    Acc<T> acc;
-    const uint4 *col = A.hs + pos;
-    if (A.nch == 16) {
-      uint4 v[16];
-#pragma unroll
-      for (int c = 0; c < 16; c++) v[c] = col[(uint64_t)c * A.npad];
-#pragma unroll
-      for (int c = 0; c < 16; c++) acc.add(v[c], clds[c]);
-    } else {
-#pragma unroll 8
-      for (int c = 0; c < A.nch; c++) acc.add(col[(uint64_t)c * A.npad], clds[c]);
-    }
-    const PInfo pi{A.mag_s[pos], A.sumsq_s[pos], A.len_s[pos]};
-    const PS s = acc.finish(pi.mag, pc.mag);
     double raw[MC_MAX_SINGLE];
+    if (A.ident) {  // alignment mode: Feature::align(*pt, *p) computed by the NW kernel
+      raw[0] = A.ident[pos];
 #pragma unroll
-    for (int i = 0; i < MC_MAX_SINGLE; i++)
-      raw[i] = i < C.c.n_single ? raw_fast(C.c.lookup[i], s, pi, pc, A.B) : 0.0;  // compute(*pt, *p)
+      for (int i = 1; i < MC_MAX_SINGLE; i++) raw[i] = 0.0;
+    } else {
+      Acc<T> acc;
+      const uint4 *col = A.hs + pos;
+      if (A.nch == 16) {
+        uint4 v[16];
+#pragma unroll
+        for (int c = 0; c < 16; c++) v[c] = col[(uint64_t)c * A.npad];
+#pragma unroll
+        for (int c = 0; c < 16; c++) acc.add(v[c], clds[c]);
+      } else {
+#pragma unroll 8
+        for (int c = 0; c < A.nch; c++) acc.add(col[(uint64_t)c * A.npad], clds[c]);
+      }
+      const PInfo pi{A.mag_s[pos], A.sumsq_s[pos], A.len_s[pos]};
+      const PS s = acc.finish(pi.mag, pc.mag);
+#pragma unroll
+      for (int i = 0; i < MC_MAX_SINGLE; i++)
+        raw[i] = i < C.c.n_single ? raw_fast(C.c.lookup[i], s, pi, pc, A.B) : 0.0;  // compute(*pt, *p)
+    }
     double c0;
     const int d = classify_raw(C, raw, &c0, nullptr);
     if (c0 > -1.0) {  // NaN never qualifies
@@ -294,7 +301,7 @@ int build_static(mc_ctx *c) {
   return MC_OK;
 }
 
-int launch_fused_scan(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, uint32_t seq) {
+int launch_fused_scan(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, uint32_t seq, const double *d_ident) {
   const int nch = (int)((c->B * c->width + 15) / 16);
   const uint64_t W = E - S + 1;
   const int grid = (int)((W + ST - 1) / ST);
@@ -331,6 +338,7 @@ int launch_fused_scan(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, uint32
   A.msum = (uint64_t *)c->msum.p;
   A.hres = c->h_res_dev;
   A.seq = seq;
+  A.ident = d_ident;
 #ifdef MC_STAMPS
   static uint64_t *stamps = nullptr;
   static std::vector<double> acc(8, 0.0);

@@ -4,19 +4,117 @@
 #include <algorithm>
 #include <cfloat>
 #include <cstdio>
+#include <memory>
+#include <unordered_map>
 
 namespace mc {
 
 namespace {
 
+// Replay of Feature::align's memo table (Feature.cpp:221-243) for alignment mode.
+//
+// The reference memoises every identity by the unordered id pair, keeping the orientation of
+// the first call.  Centres of `part` are Center clones, and DivergencePoint::clone
+// (DivergencePoint.h:37-43) copies histogram, header, id and length but not the data string,
+// so after accumulation every align() against a centre aligns against "" unless the pair is
+// already memoised.  GlobAlignE(x, "") ends in its boundary column: identity 0/|x| (0, or NaN
+// for two empty strings; GlobAlignE.cpp:148-160, 278-291) -- never similar for any --id in
+// (0, 1).  Hence, after accumulation, a pair is similar only if accumulation memoised it:
+//   (m, c) was aligned in accumulation  <=>  some get_close step t had centre c, m alive and
+//   m's static position inside the step's window [S_t, E_t]   (or the same with m, c swapped).
+// Both cannot hold: a centre is never alive again, so the orientation is unique, and a
+// recurring pair recurs in the same orientation (identical value).  The memo is therefore
+// reconstructed from the step windows and each point's removal time instead of storing
+// every accumulation pair; identities are recomputed on the device on first use.
+class AlignMemo {
+ public:
+  AlignMemo(size_t n, const BVec &bv) : kill_(n, NEVER), bv_(bv) {}
+  // get_close step #steps_ starts: centre c over static window [S, E]
+  void begin_step(uint32_t c, uint64_t S, uint64_t E) {
+    win_.push_back({S, E});
+    by_centre_[c].push_back(steps_);
+    steps_++;
+  }
+  // point removed from the bvec now: alive for steps < steps_ (flagged ones were scanned in
+  // the step that just ran, pops/erases happen between steps)
+  void removed(uint32_t id) {
+    if (kill_[id] == NEVER) kill_[id] = steps_;
+  }
+  // 1: memoised as align(m, c); 2: as align(c, m); 0: not memoised in accumulation
+  int orient(uint32_t m, uint32_t c) const {
+    if (scanned(m, c)) return 1;
+    if (scanned(c, m)) return 2;
+    return 0;
+  }
+  static uint64_t key(uint32_t a, uint32_t b) {
+    return a < b ? ((uint64_t)a << 32) | b : ((uint64_t)b << 32) | a;
+  }
+  std::unordered_map<uint64_t, double> ident;  // identities computed so far (device NW)
+
+ private:
+  bool scanned(uint32_t cand, uint32_t centre) const {
+    auto it = by_centre_.find(centre);
+    if (it == by_centre_.end()) return false;
+    const uint64_t sp = bv_.spos(cand);
+    for (uint32_t t : it->second)
+      if (kill_[cand] > t && win_[t].first <= sp && sp <= win_[t].second) return true;
+    return false;
+  }
+  static constexpr uint32_t NEVER = 0xffffffffu;
+  std::vector<uint32_t> kill_;
+  std::vector<std::pair<uint64_t, uint64_t>> win_;
+  std::unordered_map<uint32_t, std::vector<uint32_t>> by_centre_;
+  uint32_t steps_ = 0;
+  const BVec &bv_;
+};
+
+// Identities of the memoised pairs among (a[i], b[i]) in their memo orientation; computes the
+// missing ones in one device NW batch.  val[i] = identity, hit[i] = memoised.
+void memo_lookup(AlignMemo &memo, mc_ctx *ctx, const Dataset &ds, const std::vector<uint32_t> &a,
+                 const std::vector<uint32_t> &b, std::vector<double> &val, std::vector<uint8_t> &hit,
+                 ClusterStats &stats) {
+  const size_t m = a.size();
+  val.assign(m, 0.0);
+  hit.assign(m, 0);
+  std::vector<uint32_t> na, nb;
+  std::vector<uint64_t> nkey;
+  std::unordered_map<uint64_t, size_t> pending;
+  std::vector<int> orient(m);
+  for (size_t i = 0; i < m; i++) {
+    const int o = memo.orient(a[i], b[i]);
+    orient[i] = o;
+    if (!o) continue;
+    hit[i] = 1;
+    const uint64_t k = AlignMemo::key(a[i], b[i]);
+    if (memo.ident.count(k) || pending.count(k)) continue;
+    pending[k] = na.size();
+    na.push_back(o == 1 ? a[i] : b[i]);
+    nb.push_back(o == 1 ? b[i] : a[i]);
+    nkey.push_back(k);
+  }
+  if (!na.empty()) {
+    std::vector<double> id(na.size());
+    check(mc_nw_identity(ctx, na.data(), nb.data(), na.size(), id.data(), nullptr, nullptr), "mc_nw_identity");
+    for (size_t q = 0; q < na.size(); q++) {
+      memo.ident[nkey[q]] = id[q];
+      stats.align_nw_pairs++;
+      stats.align_nw_cells += ds.lengths[na[q]] * ds.lengths[nb[q]];
+    }
+  }
+  for (size_t i = 0; i < m; i++)
+    if (hit[i]) val[i] = memo.ident.at(AlignMemo::key(a[i], b[i]));
+}
+
 // accumulate (ClusterFactory.cpp:637-714): grow one cluster around `last` until get_close
 // finds no similar candidate; returns the next seed through *last_ptr.
 void accumulate(uint32_t *last_ptr, const Dataset &ds, mc_ctx *ctx, BVec &bv, std::vector<Center> &centers,
-                const ClusterConfig &cfg, ClusterStats &stats, std::vector<uint32_t> &flag_buf, PhaseTimer &timer) {
+                const ClusterConfig &cfg, ClusterStats &stats, std::vector<uint32_t> &flag_buf, PhaseTimer &timer,
+                AlignMemo *memo) {
   uint32_t last = *last_ptr;
   std::vector<uint32_t> current = {last};
   check(mc_cluster_begin(ctx, last), "mc_cluster_begin");
   bool is_min = false;
+  const auto &order = bv.static_order();
   while (!is_min) {
     uint64_t len = ds.lengths[last];
     auto bounds = bv.get_range((uint64_t)(len * cfg.sim), (uint64_t)(len / cfg.sim));
@@ -26,8 +124,11 @@ void accumulate(uint32_t *last_ptr, const Dataset &ds, mc_ctx *ctx, BVec &bv, st
     if (count > 0) {
       stats.scan_steps++;
       stats.scan_candidates += (uint64_t)count;
+      if (memo) memo->begin_step(last, S, E);
       Scope sc(timer, "accumulate.mc_scan");
       check(mc_scan(ctx, last, S, E, flag_buf.data(), flag_buf.size(), &res), "mc_scan");
+      stats.align_nw_pairs += res.nw_pairs;
+      stats.align_nw_cells += res.nw_cells;
     } else {  // the OpenMP loop runs no iteration: result NULL, is_min stays true
       res.is_min = 1;
       res.has_best = 0;
@@ -36,21 +137,55 @@ void accumulate(uint32_t *last_ptr, const Dataset &ds, mc_ctx *ctx, BVec &bv, st
     if (is_min) {
       if (!res.has_best) {
         uint32_t p = bv.pop();
-        if (p != BVec::NONE) check(mc_kill(ctx, bv.spos(p)), "mc_kill");
+        if (p != BVec::NONE) {
+          check(mc_kill(ctx, bv.spos(p)), "mc_kill");
+          if (memo) memo->removed(p);
+        }
         *last_ptr = p;
       } else {
         auto rc = bv.locate(res.best_pos);
-        *last_ptr = bv.static_order()[res.best_pos];
+        *last_ptr = order[res.best_pos];
         bv.erase(rc.first, rc.second);
         check(mc_kill(ctx, res.best_pos), "mc_kill");
+        if (memo) memo->removed(order[res.best_pos]);
       }
     } else {
       std::vector<uint32_t> flagged(flag_buf.begin(), flag_buf.begin() + res.n_flagged);
+      if (memo)
+        for (uint32_t pos : flagged) memo->removed(order[pos]);
       bv.remove_positions(flagged, bounds.first.first, bounds.second.first, current);
       last = res.new_centre;
     }
   }
   centers.push_back(Center{last, std::move(current), false});
+}
+
+// merge's cascade (ClusterFactory.cpp:427-493 + Trainer::merge, Trainer.cpp:129-157).
+// Merging only moves member lists, never centres, so every (candidate, current) centre pair is
+// classified in one batch first; sim/c0 are indexed like pa/pb (poff per current centre).
+void merge_cascade(std::vector<Center> &part, const std::vector<uint64_t> &poff, const std::vector<uint8_t> &sim,
+                   const std::vector<double> &c0) {
+  const uint32_t C = (uint32_t)part.size();
+  for (uint32_t i = 0; i < C; i++) {
+    long best_i = 0;
+    double best_v = DBL_MIN;  // std::numeric_limits<double>::min()
+    for (uint64_t q = poff[i]; q < poff[i + 1]; q++) {
+      if (sim[q]) {
+        long t = (long)i + 1 + (long)(q - poff[i]);
+        if (!(best_v > c0[q])) {  // best = best.second > dist ? best : (i, dist): last max wins
+          best_i = t;
+          best_v = c0[q];
+        }
+      }
+    }
+    if (best_i > (long)i) {
+      auto &to_add = part[best_i].points;
+      auto &to_del = part[i].points;
+      to_add.insert(to_add.end(), to_del.begin(), to_del.end());
+      part[i].del = true;
+    }
+  }
+  part.erase(std::remove_if(part.begin(), part.end(), [](const Center &c) { return c.del; }), part.end());
 }
 
 }  // namespace
@@ -61,11 +196,16 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
   const auto &order = bv.static_order();
   check(mc_set_order(ctx, order.data(), order.size()), "mc_set_order");
   std::vector<uint32_t> flag_buf(order.size() + 1);
+  std::unique_ptr<AlignMemo> memo;
+  if (cfg.align) memo.reset(new AlignMemo(ds.size(), bv));
   {
     Scope s(timer, "accumulate");
     uint32_t last = bv.pop();
-    if (last != BVec::NONE) check(mc_kill(ctx, bv.spos(last)), "mc_kill");
-    while (last != BVec::NONE) accumulate(&last, ds, ctx, bv, part, cfg, stats, flag_buf, timer);
+    if (last != BVec::NONE) {
+      check(mc_kill(ctx, bv.spos(last)), "mc_kill");
+      if (memo) memo->removed(last);
+    }
+    while (last != BVec::NONE) accumulate(&last, ds, ctx, bv, part, cfg, stats, flag_buf, timer, memo.get());
   }
   Scope s(timer, "update+merge");
   for (int it = 0; it < cfg.iterations; it++) {
@@ -83,11 +223,37 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
       uint32_t e = std::min<uint32_t>(j + cfg.delta, C - 1);
       stats.update_evals += off[e + 1] - off[b];
     }
-    if (C) check(mc_mean_shift(ctx, cids.data(), C, off.data(), members.data(), cfg.delta, newc.data()), "mc_mean_shift");
+    if (C && !memo) {
+      check(mc_mean_shift(ctx, cids.data(), C, off.data(), members.data(), cfg.delta, newc.data()), "mc_mean_shift");
+    } else if (C) {
+      // Trainer::filter(center clone, good): feat->compute(*member, *clone) (Trainer.cpp:334-349)
+      std::vector<uint32_t> fa, fb;
+      for (uint32_t j = 0; j < C; j++) {
+        uint32_t b = j >= (uint32_t)cfg.delta ? j - cfg.delta : 0;
+        uint32_t e = std::min<uint32_t>(j + cfg.delta, C - 1);
+        for (uint64_t q = off[b]; q < off[e + 1]; q++) {
+          fa.push_back(members[q]);
+          fb.push_back(cids[j]);
+        }
+      }
+      std::vector<double> val;
+      std::vector<uint8_t> hit, keep(fa.size(), 0);
+      memo_lookup(*memo, ctx, ds, fa, fb, val, hit, stats);
+      std::vector<double> raw;
+      std::vector<size_t> idx;
+      for (size_t q = 0; q < fa.size(); q++)
+        if (hit[q]) {
+          raw.push_back(val[q]);
+          idx.push_back(q);
+        }
+      std::vector<uint8_t> sim(raw.size());
+      if (!raw.empty())
+        check(mc_classify_values(ctx, raw.data(), raw.size(), sim.data(), nullptr, nullptr), "mc_classify_values");
+      for (size_t r = 0; r < idx.size(); r++) keep[idx[r]] = sim[r];
+      check(mc_mean_shift_select(ctx, cids.data(), C, off.data(), members.data(), cfg.delta, keep.data(), newc.data()),
+            "mc_mean_shift_select");
+    }
     for (uint32_t j = 0; j < C; j++) part[j].centre = newc[j];
-    // merge (ClusterFactory.cpp:427-493 + Trainer::merge, Trainer.cpp:129-157).  Merging
-    // only moves member lists, never centres, so every (candidate, current) centre pair is
-    // classified in one batch and the sequential cascade is replayed on the host.
     std::vector<uint32_t> pa, pb;
     std::vector<uint64_t> poff(C + 1, 0);
     for (uint32_t i = 0; i < C; i++) {
@@ -99,30 +265,31 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
       poff[i + 1] = pa.size();
     }
     stats.merge_evals += pa.size();
-    std::vector<uint8_t> sim(pa.size());
-    std::vector<double> c0(pa.size());
-    if (!pa.empty())
+    std::vector<uint8_t> sim(pa.size(), 0);
+    std::vector<double> c0(pa.size(), 0.0);
+    if (!pa.empty() && !memo) {
       check(mc_classify_pairs(ctx, pa.data(), pb.data(), pa.size(), sim.data(), c0.data(), nullptr), "mc_classify_pairs");
-    for (uint32_t i = 0; i < C; i++) {
-      long best_i = 0;
-      double best_v = DBL_MIN;  // std::numeric_limits<double>::min()
-      for (uint64_t q = poff[i]; q < poff[i + 1]; q++) {
-        if (sim[q]) {
-          long t = (long)i + 1 + (long)(q - poff[i]);
-          if (!(best_v > c0[q])) {  // best = best.second > dist ? best : (i, dist): last max wins
-            best_i = t;
-            best_v = c0[q];
-          }
+    } else if (!pa.empty()) {  // both centres are clones: only memoised pairs can be similar
+      std::vector<double> val;
+      std::vector<uint8_t> hit;
+      memo_lookup(*memo, ctx, ds, pa, pb, val, hit, stats);
+      std::vector<double> raw;
+      std::vector<size_t> idx;
+      for (size_t q = 0; q < pa.size(); q++)
+        if (hit[q]) {
+          raw.push_back(val[q]);
+          idx.push_back(q);
         }
-      }
-      if (best_i > (long)i) {
-        auto &to_add = part[best_i].points;
-        auto &to_del = part[i].points;
-        to_add.insert(to_add.end(), to_del.begin(), to_del.end());
-        part[i].del = true;
+      std::vector<uint8_t> s2(raw.size());
+      std::vector<double> c2(raw.size());
+      if (!raw.empty())
+        check(mc_classify_values(ctx, raw.data(), raw.size(), s2.data(), c2.data(), nullptr), "mc_classify_values");
+      for (size_t r = 0; r < idx.size(); r++) {
+        sim[idx[r]] = s2[r];
+        c0[idx[r]] = c2[r];
       }
     }
-    part.erase(std::remove_if(part.begin(), part.end(), [](const Center &c) { return c.del; }), part.end());
+    merge_cascade(part, poff, sim, c0);
   }
   return part;
 }

@@ -24,6 +24,7 @@ struct ClusterConfig {
   int iterations = 15;
   int delta = 5;
   bool verbose = true;
+  bool align = false;  // classifier feature is Feature::align (Runner.cpp:32-34, 332)
 };
 
 struct ClusterStats {
@@ -32,6 +33,7 @@ struct ClusterStats {
   uint64_t update_evals = 0;     // filter evaluations in the mean-shift updates
   uint64_t merge_evals = 0;
   uint64_t nw_pairs = 0, nw_cells = 0;  // training alignments
+  uint64_t align_nw_pairs = 0, align_nw_cells = 0;  // alignment mode: classifier alignments
 };
 
 // Runs accumulation + `iterations` rounds of mean-shift update and merge.

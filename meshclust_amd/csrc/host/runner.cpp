@@ -160,7 +160,6 @@ RunResult run_pipeline(const Dataset &ds, mc_ctx *ctx, Options opt, bool upload)
     Scope s(rr.timer, "train");
     tr.train();
   }
-  if (opt.align) throw Error("--align / --id < 0.6 (NW-only classification) is not wired into the GPU scan yet", 2);
   mc_classifier cls = tr.classifier();
   check(mc_set_classifier(ctx, &cls), "mc_set_classifier");
   BVec bv(ds.lengths, 1000);
@@ -174,6 +173,7 @@ RunResult run_pipeline(const Dataset &ds, mc_ctx *ctx, Options opt, bool upload)
   cc.iterations = opt.iterations;
   cc.delta = opt.delta;
   cc.verbose = verbose;
+  cc.align = opt.align;
   rr.part = mean_shift_cluster(ds, ctx, bv, cc, rr.timer, rr.stats);
   rr.stats.nw_pairs = tr.nw_pairs;
   rr.stats.nw_cells = tr.nw_cells;
@@ -190,10 +190,11 @@ std::string stats_json(const RunResult &rr, double parse_ms, double write_ms) {
   o += b;
   snprintf(b, sizeof b,
            ", \"scan_steps\": %llu, \"scan_candidates\": %llu, \"update_evals\": %llu, \"merge_evals\": %llu"
-           ", \"nw_pairs\": %llu, \"nw_cells\": %llu",
+           ", \"nw_pairs\": %llu, \"nw_cells\": %llu, \"align_nw_pairs\": %llu, \"align_nw_cells\": %llu",
            (unsigned long long)rr.stats.scan_steps, (unsigned long long)rr.stats.scan_candidates,
            (unsigned long long)rr.stats.update_evals, (unsigned long long)rr.stats.merge_evals,
-           (unsigned long long)rr.stats.nw_pairs, (unsigned long long)rr.stats.nw_cells);
+           (unsigned long long)rr.stats.nw_pairs, (unsigned long long)rr.stats.nw_cells,
+           (unsigned long long)rr.stats.align_nw_pairs, (unsigned long long)rr.stats.align_nw_cells);
   o += b;
   o += ", \"phases_ms\": {";
   for (size_t i = 0; i < rr.timer.order.size(); i++) {

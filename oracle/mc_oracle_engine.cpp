@@ -25,6 +25,7 @@ struct mc_ctx {
   std::vector<uint64_t> mags;
   mc_classifier cls{};
   bool has_cls = false;
+  bool align = false;  // classifier = Feature::align alone (Trainer.cpp:570-577)
   std::vector<uint32_t> order;
   std::vector<uint8_t> alive;
   std::vector<uint32_t> members;  // current cluster, in `current` order
@@ -142,6 +143,30 @@ int mc_pair_features(mc_ctx *c, const uint32_t *a, const uint32_t *b, uint64_t m
 int mc_set_classifier(mc_ctx *c, const mc_classifier *cls) {
   c->cls = *cls;
   c->has_cls = true;
+  c->align = cls->n_single == 1 && cls->lookup[0] == MC_FEAT_ALIGN;
+  return MC_OK;
+}
+
+// GlobAlignE(a, 0, la-1, b, 0, lb-1, 1, -1, 2, 1).getIdentity() (Feature::align, Feature.cpp:221-243)
+static double nw_ident(mc_ctx *c, uint32_t a, uint32_t b) {
+  int sc, l, d;
+  double id;
+  mco_nw(c->codes.data() + c->seq_off[a], (int)len_of(c, a), c->codes.data() + c->seq_off[b], (int)len_of(c, b), 1,
+         -1, 2, 1, &sc, &l, &d, &id);
+  return id;
+}
+
+int mc_classify_values(mc_ctx *c, const double *raw, uint64_t m, uint8_t *similar, double *combo0, double *sum) {
+  const int ns = c->cls.n_single;
+  for (uint64_t i = 0; i < m; i++) {
+    double r[MC_MAX_SINGLE] = {0};
+    for (int f = 0; f < ns; f++) r[f] = raw[i * ns + f];
+    double s, c0;
+    int d = mco_classify(&c->cls, r, &s, &c0);
+    if (similar) similar[i] = (uint8_t)d;
+    if (combo0) combo0[i] = c0;
+    if (sum) sum[i] = s;
+  }
   return MC_OK;
 }
 
@@ -153,6 +178,7 @@ static int classify(mc_ctx *c, uint32_t a, uint32_t b, double *sum, double *c0) 
 
 int mc_classify_pairs(mc_ctx *c, const uint32_t *a, const uint32_t *b, uint64_t m, uint8_t *similar, double *combo0,
                       double *sum) {
+  if (c->align) return fail(MC_ERR_STATE, "mc_classify_pairs is not available in alignment mode");
   for (uint64_t i = 0; i < m; i++) {
     double s, c0;
     int d = classify(c, a[i], b[i], &s, &c0);
@@ -241,11 +267,26 @@ int mc_scan(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, uint32_t *flagge
   bool has = false;
   uint64_t best_pos = 0, nf = 0;
   bool is_min = true;
+  std::vector<double> ident;
+  if (c->align) {  // Feature::align(*pt, *p) for the whole window, then the serial loop
+    ident.assign(E - S + 1, 0.0);
+#pragma omp parallel for schedule(dynamic)
+    for (uint64_t pos = S; pos <= E; pos++)
+      if (c->alive[pos]) ident[pos - S] = nw_ident(c, c->order[pos], centre);
+  }
   for (uint64_t pos = S; pos <= E; pos++) {
     if (!c->alive[pos]) continue;
     uint32_t id = c->order[pos];
     double s, c0;
-    int d = classify(c, id, centre, &s, &c0);
+    int d;
+    if (c->align) {
+      double r[MC_MAX_SINGLE] = {ident[pos - S]};
+      d = mco_classify(&c->cls, r, &s, &c0);
+      res->nw_pairs++;
+      res->nw_cells += len_of(c, id) * len_of(c, centre);
+    } else {
+      d = classify(c, id, centre, &s, &c0);
+    }
     if (c0 > best_val) {
       best_val = c0;
       best_pos = pos;
@@ -269,8 +310,23 @@ int mc_scan(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, uint32_t *flagge
   return MC_OK;
 }
 
+int mc_mean_shift_select(mc_ctx *c, const uint32_t *cid, uint32_t C, const uint64_t *off, const uint32_t *members,
+                         int delta, const uint8_t *keep, uint32_t *newc) {
+  uint64_t k = 0;
+  for (uint32_t j = 0; j < C; j++) {
+    long b = (long)j - delta < 0 ? 0 : (long)j - delta;
+    long e = (long)j + delta < (long)C - 1 ? (long)j + delta : (long)C - 1;
+    std::vector<uint32_t> good;
+    for (uint64_t q = off[b]; q < off[e + 1]; q++, k++)
+      if (keep[k]) good.push_back(members[q]);
+    newc[j] = good.empty() ? cid[j] : mean_closest(c, good);
+  }
+  return MC_OK;
+}
+
 int mc_mean_shift(mc_ctx *c, const uint32_t *cid, uint32_t C, const uint64_t *off, const uint32_t *members, int delta,
                   uint32_t *newc) {
+  if (c->align) return fail(MC_ERR_STATE, "mc_mean_shift is not available in alignment mode");
 #pragma omp parallel for schedule(dynamic)
   for (uint32_t j = 0; j < C; j++) {
     long b = (long)j - delta < 0 ? 0 : (long)j - delta;

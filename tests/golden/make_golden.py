@@ -48,6 +48,10 @@ E2E = {
     # related templates (families): ambiguous pairs, many merges
     "fam2k": (("family", 2000, 50, 10, 0.10, 0.03, 25), ["--id", "0.90"]),
     "fam2k_id85": (("family", 2000, 40, 8, 0.12, 0.04, 26), ["--id", "0.85", "--delta", "8"]),
+    # alignment mode (Feature::align classifier; --align, or --id < 0.6 switches it on)
+    "al300": ((300, 500, 10, 0.03, 7), ["--align", "--id", "0.9"]),
+    "al_fam400_id55": (("family", 400, 16, 4, 0.25, 0.05, 31), ["--id", "0.55"]),
+    "al_mix300": (("mixed", 300, 10, 0.08, 32), ["--align", "--id", "0.8", "--delta", "3"]),
 }
 TRAIN = {"a1k": ("a1k", 3, 0.90)}
 

@@ -161,3 +161,80 @@ def test_e2e_cli_byte_identical(eng, name, tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     with gzip.open(fixtures.golden("e2e_%s.clstr.gz" % name), "rb") as f:
         assert out.read_bytes() == f.read()
+
+
+# ---------------------------------------------------------------- alignment mode
+def align_classifier(cutoff):
+    """The classifier Trainer::train installs for k == 0 (Trainer.cpp:570-577)."""
+    c = O.Classifier()
+    c.n_single = 1
+    c.lookup[0] = 1  # FEAT_ALIGN
+    c.is_sim[0] = 1
+    c.mins[0], c.maxs[0] = 0.0, 1.0  # Feature::normalize (Feature.cpp:90-95)
+    c.n_combo = 1
+    c.combo_kind[0] = 2  # COMBO_SELF
+    c.combo_len[0] = 1
+    c.combo_idx[0][0] = 0
+    c.weights[0], c.weights[1] = -cutoff, 1.0
+    return c
+
+
+def test_nw_empty_strings_vs_oracle(eng):
+    """GlobAlignE with len1 or len2 == 1 (a Center clone carries no data string)."""
+    rng = np.random.default_rng(4)
+    pairs = [(b"", b""), (b"", bytes([1])), (bytes([2]), b""), (b"", bytes(rng.integers(0, 4, 700, np.uint8))),
+             (bytes(rng.integers(0, 4, 1500, np.uint8)), b""), (bytes([0, 1, 2]), bytes([0, 1, 2]))]
+    a_cat = np.frombuffer(b"".join(a for a, _ in pairs), np.uint8)
+    b_cat = np.frombuffer(b"".join(b for _, b in pairs), np.uint8)
+    a_off = np.cumsum([0] + [len(a) for a, _ in pairs])
+    b_off = np.cumsum([0] + [len(b) for _, b in pairs])
+    ident, ln, ids, sc = eng.nw_identity_raw(a_cat, a_off, b_cat, b_off)
+    for i, (a, b) in enumerate(pairs):
+        wi, wl, wd, ws = O.nw(a, b)
+        assert (ln[i], ids[i], sc[i]) == (wl, wd, ws), i
+        assert ident[i] == wi or (np.isnan(ident[i]) and np.isnan(wi)), i
+
+
+@pytest.mark.parametrize("cutoff", [0.55, 0.8, 0.9])
+def test_align_classify_values_vs_oracle(eng, a1k, cutoff):
+    cls = align_classifier(cutoff)
+    eng.set_classifier(cls)
+    vals = np.array([0.0, 1.0, cutoff, np.nextafter(cutoff, 0), np.nextafter(cutoff, 1), np.nan, 0.5, 0.93, 1e-300])
+    sim, c0, s = eng.classify_values(vals[:, None])
+    for i, v in enumerate(vals):
+        d, ws, wc0 = O.classify(cls, [v])
+        assert sim[i] == d, (v, sim[i], d)
+        assert (s[i] == ws or (np.isnan(s[i]) and np.isnan(ws))) and (c0[i] == wc0 or np.isnan(wc0)), v
+
+
+def _mean_closest_py(h, ids):
+    """get_mean / Trainer::closest restated with the oracle's distance_d (first minimum)."""
+    mean = h[ids].astype(np.float64).sum(axis=0) / len(ids)
+    best, bd = None, None
+    for i in ids:
+        d = O.distance_d(h[i], mean)
+        if best is None or d < bd:
+            best, bd = i, d
+    return best
+
+
+def test_mean_shift_select_vs_oracle(eng, a1k):
+    g, recs = a1k
+    h, _ = eng.histograms()
+    rng = np.random.default_rng(8)
+    C, delta = 12, 2
+    sizes = rng.integers(1, 30, size=C)
+    members = rng.choice(len(recs), size=int(sizes.sum()), replace=False).astype(np.uint32)
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
+    centres = members[off[:-1].astype(np.int64)]
+    keep, want = [], []
+    for j in range(C):
+        b, e = max(0, j - delta), min(C - 1, j + delta)
+        nb = members[int(off[b]):int(off[e + 1])]
+        kj = (rng.random(len(nb)) < (0.0 if j == 3 else 0.4)).astype(np.uint8)
+        keep.append(kj)
+        kept = [int(x) for x, k in zip(nb, kj) if k]
+        want.append(int(centres[j]) if not kept else _mean_closest_py(h, kept))
+    eng.set_classifier(align_classifier(0.9))
+    got = eng.mean_shift_select(centres, off, members, delta, np.concatenate(keep))
+    assert list(got) == want
