@@ -59,11 +59,11 @@ bool BVec::inner_index_of(uint64_t length, size_t &idx, size_t *pfront, size_t *
   const auto &bin = data_[idx];
   size_t front = 0, back = 0;
   size_t low = 0, high = bin.size() - 1;
-  if (length < len_[bin[low]] && pfront != nullptr) *pfront = low;
-  if (length > len_[bin[high]] && pback != nullptr) *pback = high;
+  if (length < plen_[bin[low]] && pfront != nullptr) *pfront = low;
+  if (length > plen_[bin[high]] && pback != nullptr) *pback = high;
   for (; low <= high;) {
     size_t mid = (low + high) / 2;
-    uint64_t d = len_[bin[mid]];
+    uint64_t d = plen_[bin[mid]];
     if (d == length) {
       front = mid;
       back = mid;
@@ -80,11 +80,11 @@ bool BVec::inner_index_of(uint64_t length, size_t &idx, size_t *pfront, size_t *
     }
   }
   if (pfront) {
-    for (long i = (long)front; i >= 0 && len_[bin[i]] == length; i--) front = (size_t)i;
+    for (long i = (long)front; i >= 0 && plen_[bin[i]] == length; i--) front = (size_t)i;
     *pfront = front;
   }
   if (pback) {
-    for (long i = (long)back; i < (long)bin.size() && len_[bin[i]] == length; i++) back = (size_t)i;
+    for (long i = (long)back; i < (long)bin.size() && plen_[bin[i]] == length; i++) back = (size_t)i;
     *pback = back;
   }
   return true;
@@ -125,12 +125,16 @@ void BVec::insert_finalize() {
     std::sort(bin.begin(), bin.end(), [&](uint32_t a, uint32_t b) { return len_[a] < len_[b]; });
   order_.clear();
   bin_of_.clear();
+  plen_.clear();
   spos_.assign(len_.size(), std::numeric_limits<uint64_t>::max());
   for (size_t r = 0; r < data_.size(); r++)
-    for (uint32_t id : data_[r]) {
+    for (uint32_t &e : data_[r]) {  // from here on bins hold static positions (ascending)
+      const uint32_t id = e;
+      e = (uint32_t)order_.size();
       spos_[id] = order_.size();
       order_.push_back(id);
       bin_of_.push_back((uint32_t)r);
+      plen_.push_back(len_[id]);
     }
 }
 
@@ -139,7 +143,7 @@ uint32_t BVec::pop() {
     if (!bin.empty()) {
       uint32_t p = bin[0];
       bin.erase(bin.begin());
-      return p;
+      return order_[p];
     }
   return NONE;
 }
@@ -178,7 +182,7 @@ int64_t BVec::window(const BIdx &b, const BIdx &e, uint64_t *S, uint64_t *E) con
   // the first visited element is istart itself; deref = col->at(r).at(c)
   size_t r = b.first, c = b.second;
   if (r >= data_.size() || c >= data_[r].size()) throw Error("bvec_iterator dereference out of range", 1);
-  *S = spos_[data_[r][c]];
+  *S = data_[r][c];
   int64_t remaining = count - 1;
   while (remaining > 0) {  // operator++ (bvec_iterator.cpp:3-21)
     int64_t avail = (int64_t)data_[r].size() - 1 - (int64_t)c;
@@ -193,28 +197,35 @@ int64_t BVec::window(const BIdx &b, const BIdx &e, uint64_t *S, uint64_t *E) con
     while (r < data_.size() && data_[r].empty()) r++;
     if (r >= data_.size()) throw Error("tried incrementing null iterator", 1);
   }
-  *E = spos_[data_[r][c]];
+  *E = data_[r][c];
   return count;
 }
 
 void BVec::remove_positions(const std::vector<uint32_t> &pos_sorted, size_t a, size_t b,
                             std::vector<uint32_t> &available) {
   // Only the bins holding flagged candidates change; within a bin the survivors keep their
-  // order and the flagged ids leave in bvec order (== ascending static position).
+  // order and the flagged ids leave in bvec order (== ascending static position).  Bins hold
+  // ascending static positions, so each bin is compacted from its first flagged entry on.
   size_t k = 0;
   while (k < pos_sorted.size()) {
     const size_t r = bin_of_[pos_sorted[k]];
     if (r < a || r > b) throw Error("remove_available: flagged candidate outside the window bins", 3);
     auto &bin = data_[r];
-    size_t w = 0;
-    for (size_t j = 0; j < bin.size(); j++) {
-      uint32_t id = bin[j];
-      if (k < pos_sorted.size() && spos_[id] == pos_sorted[k]) {
-        available.push_back(id);
+    size_t j = (size_t)(std::lower_bound(bin.begin(), bin.end(), pos_sorted[k]) - bin.begin());
+    size_t w = j;
+    for (; j < bin.size(); j++) {
+      const uint32_t p = bin[j];
+      if (k < pos_sorted.size() && p == pos_sorted[k]) {
+        available.push_back(order_[p]);
         k++;
-      } else {
-        bin[w++] = id;
+        continue;
       }
+      if (k >= pos_sorted.size() || bin_of_[pos_sorted[k]] != r) {  // no flagged entry left in this bin
+        std::copy(bin.begin() + j, bin.end(), bin.begin() + w);
+        w += bin.size() - j;
+        break;
+      }
+      bin[w++] = p;
     }
     bin.resize(w);
     if (k < pos_sorted.size() && bin_of_[pos_sorted[k]] == r)
@@ -223,12 +234,11 @@ void BVec::remove_positions(const std::vector<uint32_t> &pos_sorted, size_t a, s
 }
 
 std::pair<size_t, size_t> BVec::locate(uint64_t pos) const {
-  const uint32_t id = order_[pos];
   const size_t r = bin_of_[pos];
   const auto &bin = data_[r];
-  for (size_t c = 0; c < bin.size(); c++)
-    if (bin[c] == id) return {r, c};
-  throw Error("bvec: static position not alive", 3);
+  auto it = std::lower_bound(bin.begin(), bin.end(), (uint32_t)pos);
+  if (it == bin.end() || *it != pos) throw Error("bvec: static position not alive", 3);
+  return {r, (size_t)(it - bin.begin())};
 }
 
 size_t BVec::size() const {

@@ -49,11 +49,12 @@ class BVec {
   bool inner_index_of(uint64_t len, size_t &idx, size_t *front, size_t *back) const;
 
   const std::vector<uint64_t> &len_;
-  std::vector<std::vector<uint32_t>> data_;
+  std::vector<std::vector<uint32_t>> data_;  // ids until insert_finalize, static positions after
   std::vector<uint64_t> begin_bounds_;
   std::vector<uint32_t> order_;   // static position -> id
   std::vector<uint64_t> spos_;    // id -> static position
   std::vector<uint32_t> bin_of_;  // static position -> bin (bins never change membership)
+  std::vector<uint64_t> plen_;    // static position -> length
   std::vector<std::pair<uint64_t, std::pair<size_t, size_t>>> index_memo_;  // length -> index_of
   std::vector<size_t> min_sizes_;
 };

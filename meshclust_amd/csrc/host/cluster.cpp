@@ -117,9 +117,14 @@ void accumulate(uint32_t *last_ptr, const Dataset &ds, mc_ctx *ctx, BVec &bv, st
   const auto &order = bv.static_order();
   while (!is_min) {
     uint64_t len = ds.lengths[last];
-    auto bounds = bv.get_range((uint64_t)(len * cfg.sim), (uint64_t)(len / cfg.sim));
+    std::pair<BIdx, BIdx> bounds;
     uint64_t S = 0, E = 0;
-    int64_t count = bv.window(bounds.first, bounds.second, &S, &E);
+    int64_t count;
+    {
+      Scope sr(timer, "accumulate.window");
+      bounds = bv.get_range((uint64_t)(len * cfg.sim), (uint64_t)(len / cfg.sim));
+      count = bv.window(bounds.first, bounds.second, &S, &E);
+    }
     mc_scan_result res{};
     if (count > 0) {
       stats.scan_steps++;
@@ -150,6 +155,7 @@ void accumulate(uint32_t *last_ptr, const Dataset &ds, mc_ctx *ctx, BVec &bv, st
         if (memo) memo->removed(order[res.best_pos]);
       }
     } else {
+      Scope sr(timer, "accumulate.remove");
       std::vector<uint32_t> flagged(flag_buf.begin(), flag_buf.begin() + res.n_flagged);
       if (memo)
         for (uint32_t pos : flagged) memo->removed(order[pos]);

@@ -1,0 +1,131 @@
+// lazysort.hpp -- the permutation std::sort (libstdc++, GCC 11) gives, evaluated lazily.
+//
+// Trainer::split (Trainer.cpp:691-701) sorts all N points by their distance to each of the
+// 150 pivots with std::sort -- an unstable introsort, so the order among equal keys (keys are
+// integers <= 10000: ties are everywhere) is defined only by that algorithm -- and then reads
+// ~35 positions of each sorted array (the alignment binary search and the 20 samples).
+// This class reproduces libstdc++'s std::sort result at any queried position without sorting
+// the whole array: introsort's partitions act on disjoint ranges, so only the ranges that
+// contain a queried position need to be partitioned, recursively, exactly as
+// std::__introsort_loop would (median-of-three to first, unguarded Hoare partition, the
+// depth limit 2*floor(log2 N) with heapsort fallback).  The final insertion sort never moves
+// an element across a partition boundary (every element left of a cut is <= every element
+// right of it and insertion sort moves only strictly smaller elements), so it equals a
+// stable insertion sort of each leaf range.
+//
+// Elements are 64-bit words compared by their upper 32 bits (key << 32 | payload), the
+// split comparator `a->distance(*p) < b->distance(*p)` on (key, id) words.
+#pragma once
+#include <algorithm>
+#include <cstdint>
+#include <vector>
+
+namespace mc {
+
+class LazyIntroSort {
+ public:
+  // Takes the input sequence (the array std::sort would be called on).
+  explicit LazyIntroSort(std::vector<uint64_t> a, int depth_override = -1) : a_(std::move(a)) {
+    const int64_t n = (int64_t)a_.size();
+    int lg = 0;
+    while (n >> (lg + 1)) lg++;
+    nodes_.push_back(Node{0, n, depth_override >= 0 ? depth_override : 2 * lg, -1, 0, false});
+  }
+
+  // Element at position pos of the sorted array.
+  uint64_t at(int64_t pos) {
+    int idx = 0;
+    for (;;) {
+      Node &nd = nodes_[idx];
+      if (nd.final) return a_[pos];
+      if (nd.left < 0) {
+        expand(idx);
+        continue;
+      }
+      idx = pos < nodes_[idx].cut ? nodes_[idx].left : nodes_[idx].left + 1;
+    }
+  }
+
+  size_t size() const { return a_.size(); }
+
+ private:
+  struct Node {
+    int64_t lo, hi;
+    int depth;
+    int left;     // index of the left child (right child = left + 1), -1 if not partitioned
+    int64_t cut;  // partition point
+    bool final;
+  };
+  static bool less(uint64_t x, uint64_t y) { return (x >> 32) < (y >> 32); }
+
+  void expand(int idx) {
+    const int64_t lo = nodes_[idx].lo, hi = nodes_[idx].hi;
+    const int depth = nodes_[idx].depth;
+    uint64_t *f = a_.data() + lo;
+    const int64_t n = hi - lo;
+    if (n <= 16) {  // leaf of __introsort_loop: __final_insertion_sort restricted to it
+      insertion_sort(f, n);
+      nodes_[idx].final = true;
+      return;
+    }
+    if (depth == 0) {  // std::__partial_sort(first, last, last) = make_heap + sort_heap
+      auto cmp = [](uint64_t x, uint64_t y) { return less(x, y); };
+      std::make_heap(f, f + n, cmp);
+      std::sort_heap(f, f + n, cmp);
+      nodes_[idx].final = true;
+      return;
+    }
+    const int64_t cut = lo + partition_pivot(f, n);
+    const int child = (int)nodes_.size();
+    nodes_.push_back(Node{lo, cut, depth - 1, -1, 0, false});
+    nodes_.push_back(Node{cut, hi, depth - 1, -1, 0, false});
+    nodes_[idx].left = child;
+    nodes_[idx].cut = cut;
+  }
+
+  // std::__unguarded_partition_pivot: median of (first+1, mid, last-1) moved to first, then
+  // std::__unguarded_partition(first+1, last, first).  Returns the cut offset.
+  static int64_t partition_pivot(uint64_t *f, int64_t n) {
+    uint64_t *a = f + 1, *b = f + n / 2, *c = f + n - 1;
+    if (less(*a, *b)) {
+      if (less(*b, *c)) std::iter_swap(f, b);
+      else if (less(*a, *c)) std::iter_swap(f, c);
+      else std::iter_swap(f, a);
+    } else if (less(*a, *c)) {
+      std::iter_swap(f, a);
+    } else if (less(*b, *c)) {
+      std::iter_swap(f, c);
+    } else {
+      std::iter_swap(f, b);
+    }
+    uint64_t *first = f + 1, *last = f + n;
+    const uint64_t piv = *f;
+    for (;;) {
+      while (less(*first, piv)) ++first;
+      --last;
+      while (less(piv, *last)) --last;
+      if (!(first < last)) return first - f;
+      std::iter_swap(first, last);
+      ++first;
+    }
+  }
+
+  // stable insertion sort (std::__insertion_sort / __unguarded_linear_insert move only
+  // strictly smaller elements)
+  static void insertion_sort(uint64_t *f, int64_t n) {
+    for (int64_t i = 1; i < n; i++) {
+      const uint64_t v = f[i];
+      int64_t j = i;
+      while (j > 0 && less(v, f[j - 1])) {
+        f[j] = f[j - 1];
+        j--;
+      }
+      f[j] = v;
+    }
+  }
+
+  std::vector<uint64_t> a_;
+  std::vector<Node> nodes_;
+};
+
+}  // namespace mc

@@ -1,6 +1,8 @@
 // trainer.cpp -- see trainer.hpp.  Compiled with -ffp-contract=off.
 #include "trainer.hpp"
 
+#include "lazysort.hpp"
+
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -111,21 +113,25 @@ std::vector<PairId> Trainer::split() {
   // every pivot's distance to every point: one GPU launch.  Each pivot's std::sort runs on
   // (key << 32 | id) words with a comparator that looks only at the key: the comparison
   // outcomes -- and so the permutation -- are those of sorting ids by keys[id].
+  // std::sort(pts, by distance to pivot i) is evaluated lazily (lazysort.hpp): only the
+  // positions the binary search and the sampler read are resolved, with std::sort's exact
+  // tie order.
   std::vector<uint16_t> keys(P * N);
-  std::vector<std::vector<uint32_t>> sorted(P);
+  std::vector<LazyIntroSort> sorted;
+  sorted.reserve(P);
   {
     Scope s(timer_, "train.sort_keys");
     check(mc_distance_keys(ctx_, indices.data(), (uint32_t)P, all_ids.data(), N, keys.data()), "mc_distance_keys");
+    std::vector<std::vector<uint64_t>> w(P);
 #pragma omp parallel for schedule(dynamic) num_threads(cfg_.threads)
     for (size_t i = 0; i < P; i++) {
       const uint16_t *kk = &keys[i * N];
-      std::vector<uint64_t> w(N);
-      for (size_t t = 0; t < N; t++) w[t] = ((uint64_t)kk[points[t]] << 32) | points[t];
-      std::sort(w.begin(), w.end(), [](uint64_t a, uint64_t b) { return (a >> 32) < (b >> 32); });
-      sorted[i].resize(N);
-      for (size_t t = 0; t < N; t++) sorted[i][t] = (uint32_t)w[t];
+      w[i].resize(N);
+      for (size_t t = 0; t < N; t++) w[i][t] = ((uint64_t)kk[points[t]] << 32) | points[t];
     }
+    for (size_t i = 0; i < P; i++) sorted.emplace_back(std::move(w[i]));
   }
+  auto pt_at = [&](size_t i, size_t pos) { return (uint32_t)sorted[i].at((int64_t)pos); };
   // binary search with alignment (:703-721): the 150 dependent chains advance together, one
   // batched NW launch per step.
   std::vector<size_t> offset(P, N / 4), pivot(P, 2 * (N / 4));
@@ -137,11 +143,11 @@ std::vector<PairId> Trainer::split() {
       std::vector<size_t> who;
       for (size_t i = 0; i < P; i++) {
         if (active[i] && offset[i] == 0) active[i] = 0;
-        if (active[i]) {
-          batch.emplace_back(indices[i], sorted[i][pivot[i]]);
-          who.push_back(i);
-        }
+        if (active[i]) who.push_back(i);
       }
+      batch.resize(who.size());
+#pragma omp parallel for schedule(dynamic) num_threads(cfg_.threads)
+      for (size_t t = 0; t < who.size(); t++) batch[t] = PairId(indices[who[t]], pt_at(who[t], pivot[who[t]]));
       if (batch.empty()) break;
       std::vector<double> al;
       nw_batch(batch, al);
@@ -156,28 +162,35 @@ std::vector<PairId> Trainer::split() {
     }
   }
   int aerr = 0;
+  std::vector<std::vector<PairId>> bufs(P);
+  Scope sb(timer_, "train.sample");
+#pragma omp parallel for schedule(dynamic) num_threads(cfg_.threads)
   for (size_t i = 0; i < P; i++) {
-    const auto &pts = sorted[i];
+    const size_t npts = sorted[i].size();
     const uint32_t p = indices[i];
     double before_inc = (double)pivot[i] / to_add_each;
-    double after_inc = ((double)(pts.size() - pivot[i])) / to_add_each;
-    if (before_inc < 1) aerr = 1;
-    else if (after_inc < 1) aerr = -1;
+    double after_inc = ((double)(npts - pivot[i])) / to_add_each;
     double before_start = 0, after_start = (double)pivot[i];
-    std::vector<PairId> buf;
+    std::vector<PairId> &buf = bufs[i];
     for (int t = 0; t < (int)to_add_each; t++) {
       int idx = (int)std::round(before_start);
-      uint32_t q = pts[idx];
+      uint32_t q = pt_at(i, (size_t)idx);
       buf.push_back(hdr_less(p, q) ? PairId(p, q) : PairId(q, p));
       before_start += before_inc;
     }
-    for (int t = 0; t < (int)to_add_each && std::round(after_start) < (double)pts.size(); t++) {
+    for (int t = 0; t < (int)to_add_each && std::round(after_start) < (double)npts; t++) {
       int idx = (int)std::round(after_start);
-      uint32_t q = pts[idx];
+      uint32_t q = pt_at(i, (size_t)idx);
       buf.push_back(hdr_less(p, q) ? PairId(p, q) : PairId(q, p));
       after_start += after_inc;
     }
-    pairs.insert(buf.begin(), buf.end());
+  }
+  for (size_t i = 0; i < P; i++) {  // the warning flag keeps the serial loop's last writer
+    double before_inc = (double)pivot[i] / to_add_each;
+    double after_inc = ((double)(sorted[i].size() - pivot[i])) / to_add_each;
+    if (before_inc < 1) aerr = 1;
+    else if (after_inc < 1) aerr = -1;
+    pairs.insert(bufs[i].begin(), bufs[i].end());
   }
   if (aerr < 0) fprintf(stderr, "Warning: Alignment may be too small for sampling\n");
   else if (aerr > 0) fprintf(stderr, "Warning: Alignment may be too large for sampling\n");
