@@ -33,6 +33,7 @@ extern "C" {
 #define MC_ERR_STATE 3   /* call made in the wrong order (e.g. no sequences yet)  */
 #define MC_ERR_OOM 4     /* device allocation failed                              */
 #define MC_ERR_INPUT 5   /* input the reference would reject (bad nucleotide ...) */
+#define MC_ERR_UNSUPPORTED 6 /* this device path cannot take the request; use the step API  */
 
 /* Feature flags and combo kinds: identical values to src/cluster/src/Feature.h:9-22. */
 #define MC_FEAT_ALIGN (1 << 0)
@@ -175,6 +176,23 @@ int mc_cluster_begin(mc_ctx *ctx, uint32_t first_id);
  */
 int mc_scan(mc_ctx *ctx, uint32_t centre_id, uint64_t S, uint64_t E, uint32_t *flagged_pos,
             uint64_t cap, mc_scan_result *res);
+
+/*
+ * The whole accumulation phase on the device: ClusterFactory::MS's loop
+ * `last = points.pop(); while (last) accumulate(&last, ...)` (ClusterFactory.cpp:717-730,
+ * accumulate :637-714) run by one persistent kernel, bvec included -- no host round trip per
+ * get_close step.  Call after mc_set_order on the fresh bvec: bin b holds the static
+ * positions [bin_lo[b], bin_lo[b+1]) (bin_lo[nbins] = n) and bounds[b] is its begin bound
+ * (bvec.cpp:9-24, 208-218).  sim is --id.  Output: *nclusters clusters in creation order;
+ * cluster c has centre centre_ids[c] and members member_ids[member_off[c] ..
+ * member_off[c+1]) in the reference's `current` order.  stats (may be NULL) receives
+ * {get_close steps, sum of window sizes}.  Returns MC_ERR_UNSUPPORTED when this bvec does not
+ * fit the device controller (alignment mode, 32/64-bit histograms, very large n); the caller
+ * then drives accumulation with mc_scan.
+ */
+int mc_accumulate(mc_ctx *ctx, const uint32_t *bin_lo, const uint64_t *bounds, uint32_t nbins, double sim,
+                  uint32_t *centre_ids, uint64_t *member_off, uint32_t *member_ids, uint64_t *nclusters,
+                  uint64_t *stats);
 
 /*
  * One mean-shift iteration over all centres (the omp parallel for of ClusterFactory.cpp:

@@ -88,7 +88,7 @@ def gpu_lib():
         for name in ("mc_load_sequences", "mc_kmer_max", "mc_kmer_build", "mc_get_histograms", "mc_distance_keys",
                      "mc_pair_features", "mc_set_classifier", "mc_classify_pairs", "mc_nw_identity",
                      "mc_nw_identity_raw", "mc_set_order", "mc_kill", "mc_cluster_begin", "mc_scan",
-                     "mc_mean_shift", "mc_timers", "mc_classify_values", "mc_mean_shift_select"):
+                     "mc_mean_shift", "mc_timers", "mc_classify_values", "mc_mean_shift_select", "mc_accumulate"):
             getattr(lib, name).restype = C.c_int
         _gpu = lib
     return _gpu

@@ -166,7 +166,7 @@ int mc_ctx_destroy(mc_ctx *c) {
   for (Buf *b : {&c->codes, &c->seq_off, &c->seg, &c->seg_off, &c->hist, &c->mag, &c->sumsq, &c->len, &c->order,
                  &c->alive, &c->members, &c->member_keys, &c->partials, &c->scan_dev, &c->flags_out, &c->s_a, &c->s_b,
                  &c->s_c, &c->s_d, &c->s_e, &c->s_f, &c->s_g, &c->hs, &c->mag_s, &c->sumsq_s, &c->len_s, &c->ticket,
-                 &c->msum, &c->ident_s, &c->al_a, &c->al_b, &c->al_out})
+                 &c->msum, &c->ident_s, &c->al_a, &c->al_b, &c->al_out, &c->acc_out})
     release(*b);
   if (c->h_scan) (void)hipHostFree(c->h_scan);
   if (c->h_res) (void)hipHostFree(c->h_res);
@@ -612,6 +612,69 @@ int mc_scan(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, uint32_t *flagge
   }
   std::sort(flagged_pos, flagged_pos + nf);
   for (uint64_t i = 0; i < nf; i++) c->h_alive[flagged_pos[i]] = 0;
+  return MC_OK;
+}
+
+int mc_accumulate(mc_ctx *c, const uint32_t *bin_lo, const uint64_t *bounds, uint32_t nbins, double sim,
+                  uint32_t *centre_ids, uint64_t *member_off, uint32_t *member_ids, uint64_t *nclusters,
+                  uint64_t *stats) {
+  if (!c || !c->has_cls || c->norder == 0) return MC_ERR_STATE;
+  if (!bin_lo || !bounds || nbins == 0 || bin_lo[nbins] != c->norder || !centre_ids || !member_off || !member_ids ||
+      !nclusters)
+    return MC_ERR_ARG;
+  for (uint32_t b = 0; b < nbins; b++)
+    if (bin_lo[b] > bin_lo[b + 1]) return MC_ERR_ARG;
+  if (!fused(c) || !accum_supported(c, nbins)) {
+    set_error("device-resident accumulation does not take this configuration");
+    return MC_ERR_UNSUPPORTED;
+  }
+  MCG_CHECK(hipSetDevice(c->device));
+  const uint64_t n = c->norder;
+  TRY(upload(c->s_d, bin_lo, (size_t)nbins + 1, c->stream));
+  TRY(upload(c->s_e, bounds, nbins, c->stream));
+  TRY(ensure(c->s_f, n * 4 + 16));
+  TRY(ensure(c->s_g, (n + 1) * 8 + 16));
+  TRY(ensure(c->acc_out, 64));
+  MCG_CHECK(hipMemsetAsync(c->acc_out.p, 0, 64, c->stream));
+  TRY(launch_accum(c, (const uint32_t *)c->s_d.p, (const uint64_t *)c->s_e.p, nbins, sim, (uint32_t *)c->members.p,
+                   (uint64_t *)c->member_keys.p, (uint32_t *)c->s_f.p, (uint64_t *)c->s_g.p,
+                   (uint64_t *)c->acc_out.p));
+  uint64_t out[8];
+  MCG_CHECK(hipMemcpyAsync(out, c->acc_out.p, 64, hipMemcpyDeviceToHost, c->stream));
+  MCG_CHECK(hipStreamSynchronize(c->stream));
+  flush_timers(c);
+  if (out[3]) {
+    set_error(out[3] == 99 ? "device accumulation: hand-off timed out"
+              : out[3] == 11 ? "bvec_iterator dereference out of range (the reference throws here)"
+                             : "tried incrementing null iterator (the reference throws here)");
+    return out[3] == 99 ? MC_ERR_HIP : MC_ERR_INPUT;
+  }
+  const uint64_t ncl = out[0], nmem = out[4];
+  if (ncl > n || nmem != n) {
+    set_error("device accumulation produced an inconsistent partition");
+    return MC_ERR_HIP;
+  }
+  std::vector<uint32_t> pos(n);
+  std::vector<uint64_t> keys(n);
+  MCG_CHECK(hipMemcpyAsync(centre_ids, c->s_f.p, ncl * 4, hipMemcpyDeviceToHost, c->stream));
+  MCG_CHECK(hipMemcpyAsync(member_off, c->s_g.p, (ncl + 1) * 8, hipMemcpyDeviceToHost, c->stream));
+  MCG_CHECK(hipMemcpyAsync(pos.data(), c->members.p, n * 4, hipMemcpyDeviceToHost, c->stream));
+  MCG_CHECK(hipMemcpyAsync(keys.data(), c->member_keys.p, n * 8, hipMemcpyDeviceToHost, c->stream));
+  MCG_CHECK(hipStreamSynchronize(c->stream));
+  // `current` order: the seed, then each step's flagged candidates in bvec order
+  std::vector<std::pair<uint64_t, uint32_t>> tmp;
+  for (uint64_t k = 0; k < ncl; k++) {
+    const uint64_t a = member_off[k], b = member_off[k + 1];
+    tmp.clear();
+    for (uint64_t i = a; i < b; i++) tmp.emplace_back(keys[i], pos[i]);
+    std::sort(tmp.begin(), tmp.end());
+    for (uint64_t i = a; i < b; i++) member_ids[i] = c->h_order[tmp[i - a].second];
+  }
+  *nclusters = ncl;
+  if (stats) {
+    stats[0] = out[1];
+    stats[1] = out[2];
+  }
   return MC_OK;
 }
 

@@ -1,0 +1,727 @@
+// accum.hip -- the whole accumulation phase (ClusterFactory::MS's accumulate loop,
+// ClusterFactory.cpp:637-714 and 717-730) as ONE persistent, cooperatively launched kernel.
+//
+// Every step of accumulation depends on the previous one (the next centre is the member
+// closest to the cluster's mean), so the phase is a chain of ~2 steps per cluster, each a
+// scan of the bvec window.  Driving that chain from the host costs a launch and a PCIe round
+// trip per step; here the chain never leaves the GPU:
+//
+//   WG 0 (controller)   keeps the bvec in LDS -- an alive bitmap over static positions plus
+//                       per-bin alive counts -- and runs bvec::get_range / the bvec_iterator
+//                       window (bvec_core.hpp, the closed forms checked against the host
+//                       restatement), pop / erase / remove_available, the cluster's running
+//                       integer column sums, get_mean + Trainer::closest, and the cluster
+//                       bookkeeping; it publishes each step's (centre, S, E) and collects the
+//                       step's result.
+//   all WGs             scan the window: Trainer::get_close (Trainer.cpp:34-114) on the
+//                       chunk-major static layout, one lane per candidate, centre in LDS;
+//                       similar candidates are killed and listed per workgroup, combo-0's
+//                       first maximum is reduced per workgroup.
+//
+// Static chunk c (NT positions) is always scanned by workgroup c mod G, and G is a multiple
+// of 8, so a chunk always lands on the same XCD and its rows stay in that XCD's L2.
+// Hand-offs use the agent-scope release/acquire pattern of cdna_hip_programming.md G16 on
+// two monotonic counters (go: controller -> all, arrive: all -> controller); every spin has
+// a deadline so a fault cannot leave a wave spinning forever.
+#include <algorithm>
+#include <cstring>
+
+#include "bvec_core.hpp"
+#include "features.hpp"
+
+namespace mcg {
+
+namespace {
+
+constexpr int NT = 512;
+constexpr int NW = NT / 64;
+constexpr uint32_t NONE = 0xffffffffu;
+
+struct AccCtl {  // step parameters written by the controller before each `go`
+  uint32_t centre;
+  uint32_t exit;
+  uint64_t S, E;
+  uint32_t step;
+  uint32_t pad;
+};
+
+struct AccPartial {
+  double val;
+  uint64_t pos;
+  uint32_t nflag;
+  uint32_t pad;
+};
+
+struct AccArgs {
+  // chunk-major static layout (scan.hip build_static) and id-major rows (centre)
+  const uint4 *hs;
+  uint64_t npad;
+  int nch, B;
+  const uint64_t *mag_s, *sumsq_s, *len_s;
+  const uint32_t *order;
+  uint8_t *alive;
+  const uint8_t *hist;
+  uint64_t pitch;
+  const uint64_t *mag, *sumsq, *len;
+  // bvec structure
+  uint64_t N;
+  uint32_t nb;
+  const uint32_t *bin_lo;    // nb + 1 static starts
+  const uint64_t *bounds;    // nb begin_bounds
+  double sim;
+  // hand-off
+  AccCtl *ctl;
+  uint32_t *go, *arrive;
+  AccPartial *partials;
+  uint32_t *flist;  // G * fcap
+  uint64_t fcap;
+  // output
+  uint32_t *mem_pos;   // N: member static positions, cluster after cluster
+  uint64_t *mkeys;     // N: (step << 32 | pos), 0 for a cluster's seed
+  uint32_t *cl_centre; // N
+  uint64_t *cl_off;    // N + 1
+  uint64_t *out;       // [0] clusters [1] steps [2] candidates [3] error [4] members
+  uint64_t budget;     // longest wait for one hand-off, s_memrealtime ticks (100 MHz)
+};
+
+struct Red {  // LDS scratch for block-wide reductions and scans
+  uint64_t a[NW], b[NW];
+  double d[NW];
+  uint64_t r0, r1;
+};
+
+__device__ __forceinline__ bool timed_out(const AccArgs &A, uint64_t t0) {
+  return __builtin_amdgcn_s_memrealtime() - t0 > A.budget;
+}
+
+__device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
+  for (int o = 32; o >= 1; o >>= 1) v += shfl_xor64(v, o);
+  return v;
+}
+__device__ __forceinline__ uint64_t wave_min(uint64_t v) {
+  for (int o = 32; o >= 1; o >>= 1) {
+    uint64_t w = shfl_xor64(v, o);
+    v = w < v ? w : v;
+  }
+  return v;
+}
+__device__ __forceinline__ uint64_t wave_max(uint64_t v) {
+  for (int o = 32; o >= 1; o >>= 1) {
+    uint64_t w = shfl_xor64(v, o);
+    v = w > v ? w : v;
+  }
+  return v;
+}
+
+// kind 0 sum, 1 min, 2 max; uniform result
+__device__ uint64_t block_reduce(uint64_t v, int kind, Red &R) {
+  v = kind == 0 ? wave_sum(v) : kind == 1 ? wave_min(v) : wave_max(v);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) R.a[w] = v;
+  __syncthreads();
+  uint64_t r = R.a[0];
+  for (int i = 1; i < NW; i++) {
+    const uint64_t x = R.a[i];
+    r = kind == 0 ? r + x : kind == 1 ? (x < r ? x : r) : (x > r ? x : r);
+  }
+  __syncthreads();
+  return r;
+}
+
+// exclusive prefix of v over threads (thread order); *total = sum
+__device__ uint64_t block_excl_scan(uint64_t v, uint64_t *total, Red &R) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint64_t inc = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t u = shfl64(inc, lane >= o ? lane - o : lane);
+    if (lane >= o) inc += u;
+  }
+  __syncthreads();
+  if (lane == 63) R.b[w] = inc;
+  __syncthreads();
+  uint64_t before = 0, tot = 0;
+  for (int i = 0; i < NW; i++) {
+    if (i < w) before += R.b[i];
+    tot += R.b[i];
+  }
+  __syncthreads();
+  *total = tot;
+  return before + inc - v;
+}
+
+// The bvec held by the controller workgroup: LDS bitmap of alive static positions, per-bin
+// alive counts, bin starts and begin bounds (bvec.cpp's bins after insert_finalize).
+struct DevBvec {
+  uint32_t *bits;
+  uint32_t *cn;
+  const uint32_t *lo;  // LDS copy, nb + 1
+  const uint64_t *bnd; // LDS copy, nb
+  const uint64_t *plen;  // global: length by static position
+  uint64_t nb;
+  Red *R;
+  uint64_t cache_b = ~0ull, cache_L = ~0ull, c_lt = 0, c_le = 0;
+
+  __device__ bool alive(uint64_t p) const { return (bits[p >> 5] >> (p & 31)) & 1u; }
+  __device__ uint64_t nbins() const { return nb; }
+  // accessor interface of bvec_core.hpp
+  __device__ uint64_t cnt(uint64_t b) { return b < nb ? cn[b] : 0; }
+  __device__ uint64_t bound(uint64_t b) { return bnd[b]; }
+  __device__ void index_of(uint64_t point, uint64_t *plow, uint64_t *phigh) {  // bvec.cpp:38-53
+    uint64_t lo_c = nb - 1, hi_c = 0;
+    for (uint64_t i = threadIdx.x; i < nb; i += NT) {
+      const uint64_t prev = i ? bnd[i - 1] : 0, pi = i ? i - 1 : 0;
+      if (point >= prev && point <= bnd[i]) {
+        lo_c = pi < lo_c ? pi : lo_c;
+        hi_c = pi > hi_c ? pi : hi_c;
+      }
+    }
+    uint64_t low = block_reduce(lo_c, 1, *R), high = block_reduce(hi_c, 2, *R);
+    if (point >= bnd[nb - 1]) high = high > nb - 1 ? high : nb - 1;
+    *plow = low;
+    *phigh = high;
+  }
+  __device__ int64_t first_nonempty() {
+    uint64_t v = ~0ull;
+    for (uint64_t i = threadIdx.x; i < nb; i += NT)
+      if (cn[i] && i < v) v = i;
+    v = block_reduce(v, 1, *R);
+    return v == ~0ull ? -1 : (int64_t)v;
+  }
+  __device__ int64_t last_nonempty() {
+    uint64_t v = 0;
+    for (uint64_t i = threadIdx.x; i < nb; i += NT)
+      if (cn[i] && i + 1 > v) v = i + 1;
+    v = block_reduce(v, 2, *R);
+    return (int64_t)v - 1;
+  }
+  __device__ void counts(uint64_t b, uint64_t L) {
+    if (b == cache_b && L == cache_L) return;
+    uint64_t lt = 0, le = 0;
+    for (uint64_t p = lo[b] + threadIdx.x; p < lo[b + 1]; p += NT)
+      if (alive(p)) {
+        const uint64_t l = plen[p];
+        lt += l < L;
+        le += l <= L;
+      }
+    c_lt = block_reduce(lt, 0, *R);
+    c_le = block_reduce(le, 0, *R);
+    cache_b = b;
+    cache_L = L;
+  }
+  __device__ uint64_t count_lt(uint64_t b, uint64_t L) {
+    counts(b, L);
+    return c_lt;
+  }
+  __device__ uint64_t count_le(uint64_t b, uint64_t L) {
+    counts(b, L);
+    return c_le;
+  }
+  __device__ uint64_t prefix(uint64_t b) {
+    uint64_t s = 0;
+    for (uint64_t i = threadIdx.x; i < nb && i < b; i += NT) s += cn[i];
+    return block_reduce(s, 0, *R);
+  }
+  __device__ uint64_t total() { return prefix(nb); }
+  __device__ void locate_rank(uint64_t rank, uint64_t *pb, uint64_t *pc) {
+    // bins split into NT contiguous groups; exclusive scan of group sums
+    const uint64_t per = (nb + NT - 1) / NT;
+    const uint64_t b0 = threadIdx.x * per, b1 = b0 + per < nb ? b0 + per : nb;
+    uint64_t s = 0;
+    for (uint64_t i = b0; i < b1; i++) s += cn[i];
+    uint64_t tot;
+    uint64_t before = block_excl_scan(s, &tot, *R);
+    if (threadIdx.x == 0) {
+      R->r0 = nb;
+      R->r1 = 0;
+    }
+    __syncthreads();
+    if (rank >= before && rank < before + s) {
+      uint64_t r = rank - before;
+      for (uint64_t i = b0; i < b1; i++) {
+        if (r < cn[i]) {
+          R->r0 = i;
+          R->r1 = r;
+          break;
+        }
+        r -= cn[i];
+      }
+    }
+    __syncthreads();
+    *pb = R->r0;
+    *pc = R->r1;
+    __syncthreads();
+  }
+  // static position of the c-th alive element of bin b
+  __device__ uint64_t select(uint64_t b, uint64_t c) {
+    const uint64_t p0 = lo[b], p1 = lo[b + 1];
+    const uint64_t w0 = p0 >> 5, w1 = (p1 + 31) >> 5;
+    uint64_t result = ~0ull;
+    for (uint64_t base = w0; base < w1; base += NT) {
+      const uint64_t w = base + threadIdx.x;
+      uint32_t word = 0;
+      if (w < w1) {
+        word = bits[w];
+        const uint64_t s = w << 5;
+        if (s < p0) word &= ~0u << (p0 - s);
+        if (s + 32 > p1) word &= (p1 - s) >= 32 ? ~0u : ((1u << (p1 - s)) - 1u);
+      }
+      const uint64_t pc = (uint64_t)__popc(word);
+      uint64_t tot;
+      const uint64_t before = block_excl_scan(pc, &tot, *R);
+      if (threadIdx.x == 0) R->r0 = ~0ull;
+      __syncthreads();
+      if (c >= before && c < before + pc) {
+        uint32_t x = word;
+        for (uint64_t k = c - before; k > 0; k--) x &= x - 1;
+        R->r0 = (w << 5) + (uint64_t)__builtin_ctz(x);
+      }
+      __syncthreads();
+      result = R->r0;
+      __syncthreads();
+      if (result != ~0ull) break;
+      c -= tot;
+    }
+    return result;
+  }
+  __device__ uint64_t bin_of(uint64_t p) const {  // single-thread binary search
+    uint64_t a = 0, z = nb;  // lo[a] <= p < lo[z]
+    while (z - a > 1) {
+      const uint64_t m = (a + z) / 2;
+      if (lo[m] <= p) a = m;
+      else z = m;
+    }
+    return a;
+  }
+  // kill one static position (bvec::pop / erase / remove_available)
+  __device__ void kill_one(uint64_t p) {
+    atomicAnd(&bits[p >> 5], ~(1u << (p & 31)));
+    atomicSub(&cn[bin_of(p)], 1u);
+  }
+  __device__ void invalidate() { cache_b = cache_L = ~0ull; }
+};
+
+__device__ __forceinline__ bool better(double v, uint64_t p, double bv, uint64_t bp) {
+  return v > bv || (v == bv && p < bp);
+}
+
+template <typename T>
+__global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
+  extern __shared__ __attribute__((aligned(16))) uint4 dyn[];
+  __shared__ Red R;
+  __shared__ uint32_t s_flag[NT];
+  __shared__ uint32_t s_wcnt[NW];
+  __shared__ double s_bv[NW];
+  __shared__ uint64_t s_bp[NW];
+  __shared__ uint32_t s_go;
+  __shared__ int s_abort;
+  const uint32_t G = gridDim.x, g = blockIdx.x;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint4 *clds = dyn;  // centre chunks
+  const RowRef Rs{A.hs, 1, A.npad};
+
+  // ---------------- controller state (WG 0) ----------------------------------------------
+  uint4 *Fl = dyn + A.nch;
+  uint64_t *msum = reinterpret_cast<uint64_t *>(dyn + 2 * A.nch);
+  uint32_t *cnt = reinterpret_cast<uint32_t *>(msum + A.B);
+  uint32_t *lo = cnt + ((A.nb + 1) & ~1u);
+  uint64_t *bnd = reinterpret_cast<uint64_t *>(lo + ((A.nb + 2) & ~1u));
+  uint32_t *bits = reinterpret_cast<uint32_t *>(bnd + A.nb);
+  DevBvec bv{bits, cnt, lo, bnd, A.len_s, A.nb, &R};
+  const bool ctl = g == 0;
+  // controller registers (uniform within WG 0)
+  uint32_t last = NONE;      // current centre (point id)
+  uint64_t cl_start = 0;     // first member index of the current cluster
+  uint64_t M = 0;            // members of the current cluster
+  uint64_t ncl = 0, nsteps = 0, ncand = 0;
+  uint32_t step = 0;
+  uint64_t err = 0;
+
+  auto finish_cluster = [&]() {
+    if (threadIdx.x == 0) {
+      A.cl_centre[ncl] = last;
+      A.cl_off[ncl + 1] = cl_start + M;
+    }
+    ncl++;
+    cl_start += M;
+    M = 0;
+  };
+  auto new_cluster = [&](uint64_t pos) {  // accumulate's `current = {last}`
+    if (threadIdx.x == 0) {
+      A.mem_pos[cl_start] = (uint32_t)pos;
+      A.mkeys[cl_start] = 0;
+    }
+    for (int b = threadIdx.x; b < A.B; b += NT) msum[b] = elem<T>(Rs, pos, b);
+    M = 1;
+    __syncthreads();
+  };
+  auto pop = [&]() -> uint64_t {  // bvec::pop (bvec.cpp:26-37): static position or ~0
+    const int64_t b = bv.first_nonempty();
+    if (b < 0) return ~0ull;
+    const uint64_t p = bv.select((uint64_t)b, 0);
+    if (threadIdx.x == 0) {
+      bv.kill_one(p);
+      A.alive[p] = 0;
+    }
+    __syncthreads();
+    bv.invalidate();
+    return p;
+  };
+
+  if (ctl) {
+    // bvec after insert_finalize: every static position alive
+    for (uint64_t i = threadIdx.x; i <= A.nb; i += NT) lo[i] = A.bin_lo[i];
+    for (uint64_t i = threadIdx.x; i < A.nb; i += NT) {
+      bnd[i] = A.bounds[i];
+      cnt[i] = A.bin_lo[i + 1] - A.bin_lo[i];
+    }
+    const uint64_t nwords = (A.N + 31) / 32;
+    for (uint64_t w = threadIdx.x; w < nwords; w += NT) {
+      const uint64_t rem = A.N - w * 32;
+      bits[w] = rem >= 32 ? ~0u : ((1u << rem) - 1u);
+    }
+    if (threadIdx.x == 0) A.cl_off[0] = 0;
+    __syncthreads();
+    const uint64_t p = pop();  // MS: Point<T>* last = points.pop()
+    if (p != ~0ull) {
+      last = A.order[p];
+      new_cluster(p);
+    }
+  }
+
+  uint32_t seen = 0;
+  for (;;) {
+    // ============ controller: advance the accumulate loop to the next scan step ============
+    if (ctl) {
+      uint64_t S = 0, E = 0;
+      bool have = false;
+      while (last != NONE && !err) {
+        const uint64_t L = A.len[last];
+        BPos f, b;
+        bv_get_range(bv, (uint64_t)((double)L * A.sim), (uint64_t)((double)L / A.sim), f, b);
+        int e = 0;
+        const int64_t count = bv_window(bv, f, b, &S, &E, &e);
+        if (e) {
+          err = 10 + e;
+          break;
+        }
+        if (count > 0) {
+          ncand += (uint64_t)count;
+          have = true;
+          break;
+        }
+        // the OpenMP loop ran no iteration: is_min with a NULL result -> pop a new seed
+        const uint64_t p = pop();
+        finish_cluster();
+        last = p == ~0ull ? NONE : A.order[p];
+        if (p != ~0ull) new_cluster(p);
+      }
+      step++;
+      if (threadIdx.x == 0) {
+        A.ctl->centre = last;
+        A.ctl->S = S;
+        A.ctl->E = E;
+        A.ctl->step = step;
+        A.ctl->exit = have ? 0 : 1;
+      }
+      if (have) nsteps++;
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(A.go, step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    // ============ everyone: wait for the step ============================================
+    if (threadIdx.x == 0) {
+      s_abort = 0;
+      uint32_t v;
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      while ((v = __hip_atomic_load(A.go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == seen) {
+        if (timed_out(A, t0)) {
+          s_abort = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      s_go = v;
+    }
+    __syncthreads();
+    if (s_abort) {
+      if (threadIdx.x == 0) atomicMax((unsigned long long *)&A.out[3], 99ull);
+      return;
+    }
+    seen = s_go;
+    const AccCtl P = *A.ctl;
+    if (P.exit) break;
+
+    // ============ everyone: scan the owned chunks of the window (Trainer::get_close) =======
+    for (int c = threadIdx.x; c < A.nch; c += NT)
+      clds[c] = reinterpret_cast<const uint4 *>(A.hist + (uint64_t)P.centre * A.pitch)[c];
+    const PInfo pc{A.mag[P.centre], A.sumsq[P.centre], A.len[P.centre]};
+    __syncthreads();
+    double best_v = -1.0;
+    uint64_t best_p = ~0ull;
+    uint32_t nfl = 0;  // this workgroup's flagged count (uniform)
+    const uint64_t c0 = P.S / NT, c1 = P.E / NT;
+    uint64_t cfirst = c0 + ((g + G - (uint32_t)(c0 % G)) % G);
+    for (uint64_t ch = cfirst; ch <= c1; ch += G) {
+      const uint64_t pos = ch * NT + threadIdx.x;
+      const bool valid = pos >= P.S && pos <= P.E && A.alive[pos];
+      int d = 0;
+      if (valid) {
+        Acc<T> acc;
+        const uint4 *col = A.hs + pos;
+        if (A.nch == 16) {
+          uint4 v[16];
+#pragma unroll
+          for (int k = 0; k < 16; k++) v[k] = col[(uint64_t)k * A.npad];
+#pragma unroll
+          for (int k = 0; k < 16; k++) acc.add(v[k], clds[k]);
+        } else {
+#pragma unroll 8
+          for (int k = 0; k < A.nch; k++) acc.add(col[(uint64_t)k * A.npad], clds[k]);
+        }
+        const PInfo pi{A.mag_s[pos], A.sumsq_s[pos], A.len_s[pos]};
+        const PS s = acc.finish(pi.mag, pc.mag);
+        double raw[MC_MAX_SINGLE];
+#pragma unroll
+        for (int i = 0; i < MC_MAX_SINGLE; i++)
+          raw[i] = i < C.c.n_single ? raw_fast(C.c.lookup[i], s, pi, pc, A.B) : 0.0;  // compute(*pt, *p)
+        double cv;
+        d = classify_raw(C, raw, &cv, nullptr);
+        if (cv > -1.0 && better(cv, pos, best_v, best_p)) {
+          best_v = cv;
+          best_p = pos;
+        }
+        if (d) A.alive[pos] = 0;
+      }
+      // ordered compaction of this chunk's flagged positions (ascending position)
+      const uint64_t bal = __ballot(d);
+      if (lane == 0) s_wcnt[wv] = (uint32_t)__popcll(bal);
+      __syncthreads();
+      uint32_t before = nfl;
+      uint32_t tot = 0;
+      for (int i = 0; i < NW; i++) {
+        if (i < wv) before += s_wcnt[i];
+        tot += s_wcnt[i];
+      }
+      if (d) A.flist[(uint64_t)g * A.fcap + before + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull))] = (uint32_t)pos;
+      nfl += tot;
+      __syncthreads();
+    }
+    for (int o = 32; o >= 1; o >>= 1) {
+      const double ov = __shfl_xor(best_v, o, 64);
+      const uint64_t op = shfl_xor64(best_p, o);
+      if (better(ov, op, best_v, best_p)) {
+        best_v = ov;
+        best_p = op;
+      }
+    }
+    if (lane == 0) {
+      s_bv[wv] = best_v;
+      s_bp[wv] = best_p;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double v = s_bv[0];
+      uint64_t p = s_bp[0];
+      for (int i = 1; i < NW; i++)
+        if (better(s_bv[i], s_bp[i], v, p)) {
+          v = s_bv[i];
+          p = s_bp[i];
+        }
+      A.partials[g] = AccPartial{v, p, nfl, 0};
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_fetch_add(A.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (!ctl) continue;
+
+    // ============ controller: collect the step (get_close's reduction + get_mean) =========
+    if (threadIdx.x == 0) {
+      s_abort = 0;
+      const uint32_t want = G * P.step;
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      while (__hip_atomic_load(A.arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want) {
+        if (timed_out(A, t0)) {
+          s_abort = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    if (s_abort) {
+      if (threadIdx.x == 0) atomicMax((unsigned long long *)&A.out[3], 99ull);
+      return;
+    }
+    // first maximum over workgroups, flagged counts and their offsets
+    double bv_ = -1.0;
+    uint64_t bp_ = ~0ull, cnt_w = 0;
+    if (threadIdx.x < G) {
+      const AccPartial q = A.partials[threadIdx.x];
+      bv_ = q.val;
+      bp_ = q.pos;
+      cnt_w = q.nflag;
+    }
+    uint64_t nflag;
+    const uint64_t off_w = block_excl_scan(cnt_w, &nflag, R);
+    if (threadIdx.x < G) s_flag[threadIdx.x] = (uint32_t)off_w;  // G <= NT
+    for (int o = 32; o >= 1; o >>= 1) {
+      const double ov = __shfl_xor(bv_, o, 64);
+      const uint64_t op = shfl_xor64(bp_, o);
+      if (better(ov, op, bv_, bp_)) {
+        bv_ = ov;
+        bp_ = op;
+      }
+    }
+    if (lane == 0) {
+      s_bv[wv] = bv_;
+      s_bp[wv] = bp_;
+    }
+    __syncthreads();
+    double best_val = s_bv[0];
+    uint64_t best_pos = s_bp[0];
+    for (int i = 1; i < NW; i++)
+      if (better(s_bv[i], s_bp[i], best_val, best_pos)) {
+        best_val = s_bv[i];
+        best_pos = s_bp[i];
+      }
+    if (nflag > 0) {
+      // remove_available: the flagged positions join the cluster (keys keep bvec order)
+      const uint64_t mb = cl_start + M;
+      for (uint64_t i = threadIdx.x; i < nflag; i += NT) {
+        uint32_t a = 0, z = G;  // last workgroup with offset <= i
+        while (z - a > 1) {
+          const uint32_t m = (a + z) / 2;
+          if (s_flag[m] <= i) a = m;
+          else z = m;
+        }
+        const uint32_t p = A.flist[(uint64_t)a * A.fcap + (i - s_flag[a])];
+        A.mem_pos[mb + i] = p;
+        A.mkeys[mb + i] = ((uint64_t)P.step << 32) | p;
+        bv.kill_one(p);
+      }
+      __syncthreads();
+      add_rows<T, NT>(Rs, A.mem_pos + mb, (uint32_t)nflag, A.nch, msum);
+      M += nflag;
+      __syncthreads();
+      const uint64_t win = mean_closest_fast<T, NT>(Rs, A.mem_pos + cl_start, A.mkeys + cl_start, (uint32_t)M, A.mag_s,
+                                                    A.B, A.nch, msum, Fl);
+      last = A.order[win];
+      bv.invalidate();
+    } else if (best_pos != ~0ull) {
+      // is_min with a result: the best candidate seeds the next cluster (bvec::erase)
+      if (threadIdx.x == 0) {
+        bv.kill_one(best_pos);
+        A.alive[best_pos] = 0;
+      }
+      __syncthreads();
+      bv.invalidate();
+      finish_cluster();
+      last = A.order[best_pos];
+      new_cluster(best_pos);
+    } else {
+      const uint64_t p = pop();
+      finish_cluster();
+      last = p == ~0ull ? NONE : A.order[p];
+      if (p != ~0ull) new_cluster(p);
+    }
+    __syncthreads();
+  }
+  if (ctl && threadIdx.x == 0) {
+    A.out[0] = ncl;
+    A.out[1] = nsteps;
+    A.out[2] = ncand;
+    if (err) atomicMax((unsigned long long *)&A.out[3], (unsigned long long)err);
+    A.out[4] = cl_start;
+  }
+}
+
+}  // namespace
+
+// LDS bytes of the controller state (all workgroups get the same allocation)
+static size_t accum_lds(const mc_ctx *c, uint32_t nb) {
+  const int nch = (int)((c->B * c->width + 15) / 16);
+  return (size_t)2 * nch * 16 + (size_t)c->B * 8 + (size_t)((nb + 1) & ~1u) * 4 + (size_t)((nb + 2) & ~1u) * 4 +
+         (size_t)nb * 8 + (c->norder + 31) / 32 * 4;
+}
+
+bool accum_supported(const mc_ctx *c, uint32_t nb) {
+  if (c->width != 1 && c->width != 2) return false;
+  if (c->cls.align) return false;
+  if (c->norder >= (1ull << 31)) return false;
+  return accum_lds(c, nb) + 8192 <= 160 * 1024 - 4096;
+}
+
+int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, uint32_t nb, double sim,
+                 uint32_t *d_mem_pos, uint64_t *d_mkeys, uint32_t *d_cl_centre, uint64_t *d_cl_off, uint64_t *d_out) {
+  hipDeviceProp_t prop;
+  MCG_CHECK(hipGetDeviceProperties(&prop, c->device));
+  const size_t lds = accum_lds(c, nb);
+  const void *fn = c->width == 1 ? reinterpret_cast<const void *>(&accum_kernel<uint8_t>)
+                                 : reinterpret_cast<const void *>(&accum_kernel<uint16_t>);
+  MCG_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  int per_cu = 0;
+  MCG_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, NT, lds));
+  if (per_cu < 1) {
+    set_error("accumulation kernel does not fit on a CU");
+    return MC_ERR_HIP;
+  }
+  uint32_t G = (uint32_t)prop.multiProcessorCount / 8 * 8;  // one per CU, a multiple of the 8 XCDs
+  if (G > NT) G = NT;
+  if (G < 8) G = 8;
+  const uint64_t chunks = (c->norder + NT - 1) / NT;
+  const uint64_t fcap = ((chunks + G - 1) / G) * NT;
+  if (ensure(c->s_a, sizeof(AccCtl) + 256) || ensure(c->s_b, (size_t)G * sizeof(AccPartial)) ||
+      ensure(c->s_c, (size_t)G * fcap * 4 + 16))
+    return MC_ERR_OOM;
+  MCG_CHECK(hipMemsetAsync(c->s_a.p, 0, sizeof(AccCtl) + 256, c->stream));
+  MCG_CHECK(hipMemsetAsync(c->alive.p, 1, c->norder, c->stream));
+  AccArgs A;
+  memset(&A, 0, sizeof A);
+  A.hs = (const uint4 *)c->hs.p;
+  A.npad = c->npad;
+  A.nch = (int)((c->B * c->width + 15) / 16);
+  A.B = c->B;
+  A.mag_s = (const uint64_t *)c->mag_s.p;
+  A.sumsq_s = (const uint64_t *)c->sumsq_s.p;
+  A.len_s = (const uint64_t *)c->len_s.p;
+  A.order = (const uint32_t *)c->order.p;
+  A.alive = (uint8_t *)c->alive.p;
+  A.hist = (const uint8_t *)c->hist.p;
+  A.pitch = c->pitch;
+  A.mag = (const uint64_t *)c->mag.p;
+  A.sumsq = (const uint64_t *)c->sumsq.p;
+  A.len = (const uint64_t *)c->len.p;
+  A.N = c->norder;
+  A.nb = nb;
+  A.bin_lo = d_bin_lo;
+  A.bounds = d_bounds;
+  A.sim = sim;
+  A.ctl = (AccCtl *)c->s_a.p;
+  A.go = (uint32_t *)((char *)c->s_a.p + sizeof(AccCtl) + 64);
+  A.arrive = (uint32_t *)((char *)c->s_a.p + sizeof(AccCtl) + 128);
+  A.partials = (AccPartial *)c->s_b.p;
+  A.flist = (uint32_t *)c->s_c.p;
+  A.fcap = fcap;
+  A.mem_pos = d_mem_pos;
+  A.mkeys = d_mkeys;
+  A.cl_centre = d_cl_centre;
+  A.cl_off = d_cl_off;
+  A.out = d_out;
+  A.budget = 20ull * 100000000ull;  // a single hand-off never takes 20 s: give up, report error 99
+  DevClassifier cls = c->cls;
+  void *args[] = {&A, &cls};
+  timed_begin(c);
+  MCG_CHECK(hipLaunchCooperativeKernel(fn, dim3(G), dim3(NT), args, (unsigned)lds, c->stream));
+  timed_end(c, F_SCAN);
+  return MC_OK;
+}
+
+}  // namespace mcg

@@ -1,0 +1,126 @@
+// bvec_core.hpp -- bvec::get_range + the bvec_iterator window of ClusterFactory::accumulate,
+// restated over an "alive set" accessor so the same code runs on the host (checked against
+// meshclust_amd/csrc/host/bvec.cpp in tests/native/bvec_check.cpp) and inside the
+// device-resident accumulation kernel (accum.hip), where the accessor is backed by an LDS
+// bitmap of alive static positions and per-bin alive counts.
+//
+// After insert_finalize a bin is a fixed range of static positions sorted by length; the
+// bvec only ever loses elements, so a bin's content is "its alive positions, in order".
+// The reference's binary search in inner_index_of (bvec.cpp:55-104: `high = mid`, stop at
+// low == high, then widen over equal lengths) has a closed form in terms of
+//   lb = #alive in the bin with length <  L      ub = #alive with length <= L
+//   front = min(lb, size - 1)
+//   back  = ub == size ? size - 1 : (ub > lb ? ub - 1 : ub)
+// (an absent length makes `back` the first longer element: the window then includes one
+// candidate longer than len/sim, exactly as the reference's does).
+//
+// Accessor A (all calls uniform across the calling threads):
+//   uint64_t nbins(); uint64_t cnt(b); uint64_t bound(b)          begin_bounds_[b]
+//   void index_of(point, uint64_t *low, uint64_t *high)           bvec::index_of (bvec.cpp:38-53)
+//   int64_t first_nonempty(); int64_t last_nonempty()             -1 if none
+//   uint64_t count_lt(b, L); uint64_t count_le(b, L)              alive ranks by length
+//   uint64_t prefix(b)                                            sum of cnt over bins < b
+//   uint64_t total()                                              sum of all cnt
+//   void locate_rank(rank, uint64_t *b, uint64_t *c)              rank-th alive in bin order
+//   uint64_t select(b, c)                                          static position of (b, c)
+#pragma once
+#include <cstdint>
+
+#ifdef __HIPCC__
+#define BV_HD __host__ __device__
+#else
+#define BV_HD
+#endif
+
+namespace mcg {
+
+struct BPos {
+  uint64_t first, second;  // (bin, index among the bin's alive elements), size_t semantics
+};
+
+enum BvErr : int { BV_OK = 0, BV_DEREF = 1, BV_NULL_ITER = 2 };
+
+// bvec::inner_index_of (bvec.cpp:55-104)
+template <class A>
+BV_HD inline void bv_inner_index_of(A &a, uint64_t L, uint64_t &idx, uint64_t *pfront, uint64_t *pback) {
+  if (a.cnt(idx) == 0) {
+    if (pfront) {
+      const int64_t i = a.first_nonempty();
+      if (i >= 0) {
+        idx = (uint64_t)i;
+        *pfront = 0;
+      }
+    }
+    if (pback) {
+      const int64_t i = a.last_nonempty();
+      if (i >= 0) {
+        idx = (uint64_t)i;
+        *pback = 0;
+      }
+    }
+    return;
+  }
+  const uint64_t size = a.cnt(idx);
+  if (pfront) {
+    const uint64_t lb = a.count_lt(idx, L);
+    *pfront = lb < size - 1 ? lb : size - 1;
+  }
+  if (pback) {
+    const uint64_t lb = a.count_lt(idx, L), ub = a.count_le(idx, L);
+    *pback = ub == size ? size - 1 : (ub > lb ? ub - 1 : ub);
+  }
+}
+
+// bvec::get_range (bvec.cpp:245-278)
+template <class A>
+BV_HD inline void bv_get_range(A &a, uint64_t begin_len, uint64_t end_len, BPos &front, BPos &back) {
+  const uint64_t nb = a.nbins();
+  front.first = 0;
+  front.second = 0;
+  back.first = nb - 1;
+  back.second = a.cnt(back.first) - 1;  // size_t wrap when empty, as in the reference
+  uint64_t lo, hi;
+  a.index_of(begin_len, &lo, &hi);
+  front.first = lo;
+  a.index_of(end_len, &lo, &hi);
+  back.first = hi;
+  bv_inner_index_of(a, begin_len, front.first, &front.second, nullptr);
+  bv_inner_index_of(a, end_len, back.first, nullptr, &back.second);
+}
+
+// get_close's `for (i = istart; i <= iend; ++i)` (bvec_iterator.h:61-76 operator-, .cpp:3-21
+// operator++): number of iterations and the static positions of the first and last element.
+template <class A>
+BV_HD inline int64_t bv_window(A &a, const BPos &b, const BPos &e, uint64_t *S, uint64_t *E, int *err) {
+  *err = BV_OK;
+  auto less = [](const BPos &x, const BPos &y) {
+    return x.first < y.first || (x.first == y.first && x.second < y.second);
+  };
+  auto minus = [&](const BPos &x, const BPos &y) -> int64_t {  // x - y, x >= y
+    if (x.first == y.first) return (int64_t)(x.second - y.second);
+    uint64_t sum = x.second;
+    sum += a.cnt(y.first) - y.second;
+    sum += a.prefix(x.first) - a.prefix(y.first + 1);  // bins strictly between
+    return (int64_t)sum;
+  };
+  const int64_t diff = less(e, b) ? -minus(b, e) : minus(e, b);
+  const int64_t count = diff + 1;
+  if (count <= 0) return count;
+  if (b.first >= a.nbins() || b.second >= a.cnt(b.first)) {
+    *err = BV_DEREF;
+    return count;
+  }
+  *S = a.select(b.first, b.second);
+  // operator++ walks forward over the alive elements, skipping empty bins
+  const uint64_t rank = a.prefix(b.first) + b.second + (uint64_t)(count - 1);
+  if (rank >= a.total()) {
+    *err = BV_NULL_ITER;
+    return count;
+  }
+  uint64_t r, c;
+  a.locate_rank(rank, &r, &c);
+  *E = a.select(r, c);
+  return count;
+}
+
+}  // namespace mcg

@@ -104,6 +104,7 @@ struct mc_ctx {
   std::vector<uint32_t> h_order;
   std::vector<uint8_t> h_alive;
   mcg::Buf ident_s, al_a, al_b, al_out;
+  mcg::Buf acc_out;  // device-resident accumulation: counters / error word
   // scratch
   mcg::Buf s_a, s_b, s_c, s_d, s_e, s_f, s_g;
   std::vector<void *> pinned;
@@ -139,6 +140,9 @@ int launch_finalize(mc_ctx *c, int nblocks);
 int launch_mean_shift(mc_ctx *c, const uint32_t *d_cid, uint32_t C, const uint64_t *d_off, const uint64_t *h_off,
                       const uint32_t *d_mem, int delta, const uint8_t *d_keep, uint32_t *d_new);
 int build_static(mc_ctx *c);
+bool accum_supported(const mc_ctx *c, uint32_t nb);
+int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, uint32_t nb, double sim,
+                 uint32_t *d_mem_pos, uint64_t *d_mkeys, uint32_t *d_cl_centre, uint64_t *d_cl_off, uint64_t *d_out);
 int launch_fused_scan(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, uint32_t seq, const double *d_ident);
 // NW on byte strings: pair p aligns A[aoff[ai[p]] .. aoff[ai[p]+1]) against B[...] (rows = A).
 // Results go to slot p, or to slot d_out[p] when d_out is given.

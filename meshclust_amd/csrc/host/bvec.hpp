@@ -40,6 +40,10 @@ class BVec {
   std::pair<size_t, size_t> locate(uint64_t pos) const;
 
   const std::vector<uint32_t> &static_order() const { return order_; }
+  // current bins (static positions, after insert_finalize), begin bounds, bin of a position
+  const std::vector<std::vector<uint32_t>> &bins() const { return data_; }
+  const std::vector<uint64_t> &begin_bounds() const { return begin_bounds_; }
+  const std::vector<uint64_t> &static_lengths() const { return plen_; }
   uint64_t spos(uint32_t id) const { return spos_[id]; }
   size_t size() const;
   static const uint32_t NONE = 0xffffffffu;

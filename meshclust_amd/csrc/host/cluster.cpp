@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cstdio>
+#include <cstdlib>
 #include <memory>
 #include <unordered_map>
 
@@ -204,7 +205,31 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
   std::vector<uint32_t> flag_buf(order.size() + 1);
   std::unique_ptr<AlignMemo> memo;
   if (cfg.align) memo.reset(new AlignMemo(ds.size(), bv));
-  {
+  // The device-resident loop (mc_accumulate) unless alignment mode or the configuration
+  // asks for the step API; MC_ACCUM_STEPS=1 forces the host-driven loop (both are GPU paths).
+  bool done = false;
+  if (!memo && !getenv("MC_ACCUM_STEPS")) {
+    Scope s(timer, "accumulate");
+    const auto &bins = bv.bins();
+    std::vector<uint32_t> bin_lo(bins.size() + 1, 0);
+    for (size_t b = 0; b < bins.size(); b++) bin_lo[b + 1] = bin_lo[b] + (uint32_t)bins[b].size();
+    const size_t n = order.size();
+    std::vector<uint32_t> centres(n), ids(n);
+    std::vector<uint64_t> moff(n + 1);
+    uint64_t ncl = 0, st[2] = {0, 0};
+    const int rc = mc_accumulate(ctx, bin_lo.data(), bv.begin_bounds().data(), (uint32_t)bins.size(), cfg.sim,
+                                 centres.data(), moff.data(), ids.data(), &ncl, st);
+    if (rc == MC_OK) {
+      for (uint64_t c = 0; c < ncl; c++)
+        part.push_back(Center{centres[c], std::vector<uint32_t>(ids.begin() + moff[c], ids.begin() + moff[c + 1]), false});
+      stats.scan_steps += st[0];
+      stats.scan_candidates += st[1];
+      done = true;
+    } else if (rc != MC_ERR_UNSUPPORTED) {
+      check(rc, "mc_accumulate");
+    }
+  }
+  if (!done) {
     Scope s(timer, "accumulate");
     uint32_t last = bv.pop();
     if (last != BVec::NONE) {

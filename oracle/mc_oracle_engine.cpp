@@ -341,6 +341,11 @@ int mc_mean_shift(mc_ctx *c, const uint32_t *cid, uint32_t C, const uint64_t *of
   return MC_OK;
 }
 
+int mc_accumulate(mc_ctx *, const uint32_t *, const uint64_t *, uint32_t, double, uint32_t *, uint64_t *, uint32_t *,
+                  uint64_t *, uint64_t *) {
+  return fail(MC_ERR_UNSUPPORTED, "the CPU oracle engine drives accumulation step by step");
+}
+
 int mc_timers(mc_ctx *, double *ms, int n, int) {
   for (int i = 0; i < n; i++) ms[i] = 0;
   return MC_OK;

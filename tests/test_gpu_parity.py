@@ -238,3 +238,37 @@ def test_mean_shift_select_vs_oracle(eng, a1k):
     eng.set_classifier(align_classifier(0.9))
     got = eng.mean_shift_select(centres, off, members, delta, np.concatenate(keep))
     assert list(got) == want
+
+
+# ---------------------------------------------------------------- device-resident accumulation
+ACC_CASES = {
+    "b20k": ((20000, 1000, 200, 0.03, 71), ["--id", "0.90"]),
+    "mixed6k": (("mixed", 6000, 60, 0.06, 72), ["--id", "0.85"]),
+    "fam5k": (("family", 5000, 80, 12, 0.10, 0.03, 73), ["--id", "0.90"]),
+    "short3k_k3": ((3000, 300, 50, 0.05, 74), ["--id", "0.95", "--kmer", "3"]),
+}
+
+
+@pytest.mark.parametrize("name", sorted(ACC_CASES))
+def test_device_accumulate_equals_step_path(eng, name, tmp_path):
+    """mc_accumulate (persistent kernel, bvec on the device) and the host-driven mc_scan loop
+    (whose bvec is the host restatement) give byte-identical .clstr on inputs larger than the
+    reference goldens."""
+    import importlib.util
+    spec, flags = ACC_CASES[name]
+    mg = importlib.util.spec_from_file_location("make_golden", fixtures.golden("make_golden.py"))
+    mod = importlib.util.module_from_spec(mg)
+    mg.loader.exec_module(mod)
+    fa = str(tmp_path / (name + ".fa"))
+    mod.make_input(spec, fa)
+    outs = []
+    for env_steps in (False, True):
+        out = tmp_path / ("%s_%d.clstr" % (name, env_steps))
+        env = dict(os.environ)
+        if env_steps:
+            env["MC_ACCUM_STEPS"] = "1"
+        r = subprocess.run([M.BIN, fa] + flags + ["--output", str(out), "--quiet"], capture_output=True, text=True,
+                           timeout=300, env=env)
+        assert r.returncode == 0, r.stderr[-3000:]
+        outs.append(out.read_bytes())
+    assert outs[0] == outs[1]
