@@ -425,6 +425,7 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
         A.ctl->exit = have ? 0 : 1;
       }
       if (have) nsteps++;
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains before the barrier
       __syncthreads();
       if (threadIdx.x == 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -524,6 +525,7 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
       s_bv[wv] = best_v;
       s_bp[wv] = best_p;
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // flag / alive stores of every wave drained
     __syncthreads();
     if (threadIdx.x == 0) {
       double v = s_bv[0];
@@ -611,8 +613,12 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
       add_rows<T, NT>(Rs, A.mem_pos + mb, (uint32_t)nflag, A.nch, msum);
       M += nflag;
       __syncthreads();
-      const uint64_t win = mean_closest_fast<T, NT>(Rs, A.mem_pos + cl_start, A.mkeys + cl_start, (uint32_t)M, A.mag_s,
-                                                    A.B, A.nch, msum, Fl);
+      const uint64_t win0 = mean_closest_fast<T, NT>(Rs, A.mem_pos + cl_start, A.mkeys + cl_start, (uint32_t)M,
+                                                     A.mag_s, A.B, A.nch, msum, Fl);
+      if (threadIdx.x == 0) R.r0 = win0;  // the winner is thread 0's; make it uniform
+      __syncthreads();
+      const uint64_t win = R.r0;
+      __syncthreads();
       last = A.order[win];
       bv.invalidate();
     } else if (best_pos != ~0ull) {
