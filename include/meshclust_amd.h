@@ -185,8 +185,9 @@ int mc_scan(mc_ctx *ctx, uint32_t centre_id, uint64_t S, uint64_t E, uint32_t *f
  * positions [bin_lo[b], bin_lo[b+1]) (bin_lo[nbins] = n) and bounds[b] is its begin bound
  * (bvec.cpp:9-24, 208-218).  sim is --id.  Output: *nclusters clusters in creation order;
  * cluster c has centre centre_ids[c] and members member_ids[member_off[c] ..
- * member_off[c+1]) in the reference's `current` order.  stats (may be NULL) receives
- * {get_close steps, sum of window sizes}.  Returns MC_ERR_UNSUPPORTED when this bvec does not
+ * member_off[c+1]) in the reference's `current` order.  stats (may be NULL, else 5 entries)
+ * receives {get_close steps, sum of window sizes, then the device controller's time in us:
+ * bvec window + publish, waiting for the scanning workgroups, collect + get_mean}.  Returns MC_ERR_UNSUPPORTED when this bvec does not
  * fit the device controller (alignment mode, 32/64-bit histograms, very large n); the caller
  * then drives accumulation with mc_scan.
  */

@@ -674,6 +674,7 @@ int mc_accumulate(mc_ctx *c, const uint32_t *bin_lo, const uint64_t *bounds, uin
   if (stats) {
     stats[0] = out[1];
     stats[1] = out[2];
+    for (int i = 0; i < 3; i++) stats[2 + i] = out[5 + i] / 100;  // controller phases, 100 MHz ticks -> us
   }
   return MC_OK;
 }

@@ -150,139 +150,100 @@ __device__ uint64_t block_excl_scan(uint64_t v, uint64_t *total, Red &R) {
   return before + inc - v;
 }
 
+__device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
+  for (int o = 32; o >= 1; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o, 64);
+  return v;
+}
+
 // The bvec held by the controller workgroup: LDS bitmap of alive static positions, per-bin
-// alive counts, bin starts and begin bounds (bvec.cpp's bins after insert_finalize).
+// alive counts with a Fenwick tree over them, bin starts and begin bounds (bvec.cpp's bins
+// after insert_finalize).  Every query is answered by each wave on its own from LDS (binary
+// searches, Fenwick walks, one-wave popcount scans), so a query costs no workgroup barrier;
+// callers keep queries uniform and put a barrier between kills and the next query.  The
+// O(log) forms are checked against the host bvec in tests/native/bvec_check.cpp (FastAcc).
 struct DevBvec {
   uint32_t *bits;
   uint32_t *cn;
-  const uint32_t *lo;  // LDS copy, nb + 1
-  const uint64_t *bnd; // LDS copy, nb
-  const uint64_t *plen;  // global: length by static position
-  uint64_t nb;
-  Red *R;
-  uint64_t cache_b = ~0ull, cache_L = ~0ull, c_lt = 0, c_le = 0;
+  uint32_t *fw;          // Fenwick tree, fw[1..nb]
+  const uint32_t *lo;    // LDS copy, nb + 1
+  const uint64_t *bnd;   // LDS copy, nb
+  const uint64_t *plen;  // global: length by static position (non-decreasing inside a bin)
+  uint64_t nb, lg;       // lg: highest power of two <= nb
 
-  __device__ bool alive(uint64_t p) const { return (bits[p >> 5] >> (p & 31)) & 1u; }
   __device__ uint64_t nbins() const { return nb; }
   // accessor interface of bvec_core.hpp
   __device__ uint64_t cnt(uint64_t b) { return b < nb ? cn[b] : 0; }
-  __device__ uint64_t bound(uint64_t b) { return bnd[b]; }
   __device__ void index_of(uint64_t point, uint64_t *plow, uint64_t *phigh) {  // bvec.cpp:38-53
-    uint64_t lo_c = nb - 1, hi_c = 0;
-    for (uint64_t i = threadIdx.x; i < nb; i += NT) {
-      const uint64_t prev = i ? bnd[i - 1] : 0, pi = i ? i - 1 : 0;
-      if (point >= prev && point <= bnd[i]) {
-        lo_c = pi < lo_c ? pi : lo_c;
-        hi_c = pi > hi_c ? pi : hi_c;
-      }
-    }
-    uint64_t low = block_reduce(lo_c, 1, *R), high = block_reduce(hi_c, 2, *R);
-    if (point >= bnd[nb - 1]) high = high > nb - 1 ? high : nb - 1;
-    *plow = low;
-    *phigh = high;
+    bv_index_of_sorted(bnd, nb, point, plow, phigh);
   }
+  __device__ uint64_t prefix(uint64_t b) { return bv_fw_prefix(fw, b < nb ? b : nb); }
+  __device__ uint64_t total() { return prefix(nb); }
+  __device__ void locate_rank(uint64_t rank, uint64_t *pb, uint64_t *pc) { bv_fw_locate(fw, nb, lg, rank, pb, pc); }
   __device__ int64_t first_nonempty() {
-    uint64_t v = ~0ull;
-    for (uint64_t i = threadIdx.x; i < nb; i += NT)
-      if (cn[i] && i < v) v = i;
-    v = block_reduce(v, 1, *R);
-    return v == ~0ull ? -1 : (int64_t)v;
+    if (!total()) return -1;
+    uint64_t b, c;
+    locate_rank(0, &b, &c);
+    return (int64_t)b;
   }
   __device__ int64_t last_nonempty() {
-    uint64_t v = 0;
-    for (uint64_t i = threadIdx.x; i < nb; i += NT)
-      if (cn[i] && i + 1 > v) v = i + 1;
-    v = block_reduce(v, 2, *R);
-    return (int64_t)v - 1;
+    const uint64_t t = total();
+    if (!t) return -1;
+    uint64_t b, c;
+    locate_rank(t - 1, &b, &c);
+    return (int64_t)b;
   }
-  __device__ void counts(uint64_t b, uint64_t L) {
-    if (b == cache_b && L == cache_L) return;
-    uint64_t lt = 0, le = 0;
-    for (uint64_t p = lo[b] + threadIdx.x; p < lo[b + 1]; p += NT)
-      if (alive(p)) {
-        const uint64_t l = plen[p];
-        lt += l < L;
-        le += l <= L;
-      }
-    c_lt = block_reduce(lt, 0, *R);
-    c_le = block_reduce(le, 0, *R);
-    cache_b = b;
-    cache_L = L;
+  __device__ uint32_t masked_word(uint64_t w, uint64_t p0, uint64_t p1) const {
+    uint32_t word = bits[w];
+    const uint64_t s = w << 5;
+    if (s < p0) word &= ~0u << (p0 - s);
+    if (s + 32 > p1) word &= (p1 - s) >= 32 ? ~0u : ((1u << (p1 - s)) - 1u);
+    return word;
   }
-  __device__ uint64_t count_lt(uint64_t b, uint64_t L) {
-    counts(b, L);
-    return c_lt;
+  __device__ uint64_t alive_in(uint64_t p0, uint64_t p1) const {  // alive positions in [p0, p1)
+    if (p0 >= p1) return 0;
+    const uint64_t w0 = p0 >> 5, w1 = (p1 + 31) >> 5;
+    uint32_t n = 0;
+    for (uint64_t w = w0 + (threadIdx.x & 63); w < w1; w += 64) n += (uint32_t)__popc(masked_word(w, p0, p1));
+    return wave_sum32(n);
   }
-  __device__ uint64_t count_le(uint64_t b, uint64_t L) {
-    counts(b, L);
-    return c_le;
-  }
-  __device__ uint64_t prefix(uint64_t b) {
-    uint64_t s = 0;
-    for (uint64_t i = threadIdx.x; i < nb && i < b; i += NT) s += cn[i];
-    return block_reduce(s, 0, *R);
-  }
-  __device__ uint64_t total() { return prefix(nb); }
-  __device__ void locate_rank(uint64_t rank, uint64_t *pb, uint64_t *pc) {
-    // bins split into NT contiguous groups; exclusive scan of group sums
-    const uint64_t per = (nb + NT - 1) / NT;
-    const uint64_t b0 = threadIdx.x * per, b1 = b0 + per < nb ? b0 + per : nb;
-    uint64_t s = 0;
-    for (uint64_t i = b0; i < b1; i++) s += cn[i];
-    uint64_t tot;
-    uint64_t before = block_excl_scan(s, &tot, *R);
-    if (threadIdx.x == 0) {
-      R->r0 = nb;
-      R->r1 = 0;
+  // first position of [a, z) whose length is >= L (strict: > L)
+  __device__ uint64_t len_bound(uint64_t a, uint64_t z, uint64_t L, bool strict) const {
+    while (a < z) {
+      const uint64_t m = (a + z) / 2;
+      const uint64_t l = plen[m];
+      if (strict ? l <= L : l < L) a = m + 1;
+      else z = m;
     }
-    __syncthreads();
-    if (rank >= before && rank < before + s) {
-      uint64_t r = rank - before;
-      for (uint64_t i = b0; i < b1; i++) {
-        if (r < cn[i]) {
-          R->r0 = i;
-          R->r1 = r;
-          break;
-        }
-        r -= cn[i];
-      }
-    }
-    __syncthreads();
-    *pb = R->r0;
-    *pc = R->r1;
-    __syncthreads();
+    return a;
   }
-  // static position of the c-th alive element of bin b
-  __device__ uint64_t select(uint64_t b, uint64_t c) {
+  __device__ uint64_t count_lt(uint64_t b, uint64_t L) { return alive_in(lo[b], len_bound(lo[b], lo[b + 1], L, false)); }
+  __device__ uint64_t count_le(uint64_t b, uint64_t L) { return alive_in(lo[b], len_bound(lo[b], lo[b + 1], L, true)); }
+  // static position of the c-th alive element of bin b (one wave: popcount scan over the words)
+  __device__ uint64_t select(uint64_t b, uint64_t c) const {
+    const int lane = threadIdx.x & 63;
     const uint64_t p0 = lo[b], p1 = lo[b + 1];
     const uint64_t w0 = p0 >> 5, w1 = (p1 + 31) >> 5;
-    uint64_t result = ~0ull;
-    for (uint64_t base = w0; base < w1; base += NT) {
-      const uint64_t w = base + threadIdx.x;
-      uint32_t word = 0;
-      if (w < w1) {
-        word = bits[w];
-        const uint64_t s = w << 5;
-        if (s < p0) word &= ~0u << (p0 - s);
-        if (s + 32 > p1) word &= (p1 - s) >= 32 ? ~0u : ((1u << (p1 - s)) - 1u);
+    for (uint64_t base = w0; base < w1; base += 64) {
+      const uint64_t w = base + lane;
+      const uint32_t word = w < w1 ? masked_word(w, p0, p1) : 0u;
+      const uint32_t pc = (uint32_t)__popc(word);
+      uint32_t inc = pc;
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t u = (uint32_t)__shfl_up((int)inc, o, 64);
+        if (lane >= o) inc += u;
       }
-      const uint64_t pc = (uint64_t)__popc(word);
-      uint64_t tot;
-      const uint64_t before = block_excl_scan(pc, &tot, *R);
-      if (threadIdx.x == 0) R->r0 = ~0ull;
-      __syncthreads();
-      if (c >= before && c < before + pc) {
-        uint32_t x = word;
+      const uint32_t tot = (uint32_t)__shfl((int)inc, 63, 64);
+      if (c < tot) {
+        const uint64_t hit = __ballot(inc > c);
+        const int L = __builtin_ctzll(hit);
+        uint32_t x = (uint32_t)__shfl((int)word, L, 64);
+        const uint32_t before = (uint32_t)__shfl((int)(inc - pc), L, 64);
         for (uint64_t k = c - before; k > 0; k--) x &= x - 1;
-        R->r0 = (w << 5) + (uint64_t)__builtin_ctz(x);
+        return ((base + (uint64_t)L) << 5) + (uint64_t)__builtin_ctz(x);
       }
-      __syncthreads();
-      result = R->r0;
-      __syncthreads();
-      if (result != ~0ull) break;
       c -= tot;
     }
-    return result;
+    return ~0ull;
   }
   __device__ uint64_t bin_of(uint64_t p) const {  // single-thread binary search
     uint64_t a = 0, z = nb;  // lo[a] <= p < lo[z]
@@ -293,12 +254,14 @@ struct DevBvec {
     }
     return a;
   }
-  // kill one static position (bvec::pop / erase / remove_available)
+  // kill one static position (bvec::pop / erase / remove_available); any thread, atomics
   __device__ void kill_one(uint64_t p) {
     atomicAnd(&bits[p >> 5], ~(1u << (p & 31)));
-    atomicSub(&cn[bin_of(p)], 1u);
+    const uint64_t b = bin_of(p);
+    atomicSub(&cn[b], 1u);
+    for (uint64_t i = b + 1; i <= nb; i += i & (~i + 1)) atomicSub(&fw[i], 1u);
   }
-  __device__ void invalidate() { cache_b = cache_L = ~0ull; }
+  __device__ void invalidate() {}
 };
 
 __device__ __forceinline__ bool better(double v, uint64_t p, double bv, uint64_t bp) {
@@ -324,10 +287,13 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
   uint4 *Fl = dyn + A.nch;
   uint64_t *msum = reinterpret_cast<uint64_t *>(dyn + 2 * A.nch);
   uint32_t *cnt = reinterpret_cast<uint32_t *>(msum + A.B);
-  uint32_t *lo = cnt + ((A.nb + 1) & ~1u);
+  uint32_t *fw = cnt + ((A.nb + 1) & ~1u);
+  uint32_t *lo = fw + ((A.nb + 2) & ~1u);
   uint64_t *bnd = reinterpret_cast<uint64_t *>(lo + ((A.nb + 2) & ~1u));
   uint32_t *bits = reinterpret_cast<uint32_t *>(bnd + A.nb);
-  DevBvec bv{bits, cnt, lo, bnd, A.len_s, A.nb, &R};
+  uint64_t lg = 1;
+  while (lg * 2 <= A.nb) lg *= 2;
+  DevBvec bv{bits, cnt, fw, lo, bnd, A.len_s, A.nb, lg};
   const bool ctl = g == 0;
   // controller registers (uniform within WG 0)
   uint32_t last = NONE;      // current centre (point id)
@@ -336,6 +302,8 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
   uint64_t ncl = 0, nsteps = 0, ncand = 0;
   uint32_t step = 0;
   uint64_t err = 0;
+  uint32_t cum = 0;                                  // arrivals expected so far
+  uint64_t t_win = 0, t_wait = 0, t_coll = 0, t_mark = 0;  // controller phase time, 100 MHz ticks
 
   auto finish_cluster = [&]() {
     if (threadIdx.x == 0) {
@@ -375,6 +343,12 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
       bnd[i] = A.bounds[i];
       cnt[i] = A.bin_lo[i + 1] - A.bin_lo[i];
     }
+    __syncthreads();
+    for (uint64_t i = threadIdx.x + 1; i <= A.nb; i += NT) {  // Fenwick node i covers bins (i - lowbit(i), i]
+      uint32_t t = 0;
+      for (uint64_t b = i - (i & (~i + 1)); b < i; b++) t += cnt[b];
+      fw[i] = t;
+    }
     const uint64_t nwords = (A.N + 31) / 32;
     for (uint64_t w = threadIdx.x; w < nwords; w += NT) {
       const uint64_t rem = A.N - w * 32;
@@ -393,6 +367,7 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
   for (;;) {
     // ============ controller: advance the accumulate loop to the next scan step ============
     if (ctl) {
+      if (threadIdx.x == 0) t_mark = __builtin_amdgcn_s_memrealtime();
       uint64_t S = 0, E = 0;
       bool have = false;
       while (last != NONE && !err) {
@@ -431,6 +406,9 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __hip_atomic_store(A.go, step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t t = __builtin_amdgcn_s_memrealtime();
+        t_win += t - t_mark;
+        t_mark = t;
       }
     }
     // ============ everyone: wait for the step ============================================
@@ -458,7 +436,13 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
     const AccCtl P = *A.ctl;
     if (P.exit) break;
 
-    // ============ everyone: scan the owned chunks of the window (Trainer::get_close) =======
+    // ============ workgroups owning chunks of the window: scan them (Trainer::get_close) ===
+    // Chunk c0 + i belongs to workgroup (c0 + i) mod G; only the nact workgroups owning a
+    // chunk of [S, E] take part in the step (and arrive), the others wait for the next go.
+    const uint64_t c0 = P.S / NT, c1 = P.E / NT;
+    const uint32_t nact = (uint32_t)(c1 - c0 + 1 < (uint64_t)G ? c1 - c0 + 1 : (uint64_t)G);
+    const uint32_t mine = (g + G - (uint32_t)(c0 % G)) % G;
+    if (mine < nact) {
     for (int c = threadIdx.x; c < A.nch; c += NT)
       clds[c] = reinterpret_cast<const uint4 *>(A.hist + (uint64_t)P.centre * A.pitch)[c];
     const PInfo pc{A.mag[P.centre], A.sumsq[P.centre], A.len[P.centre]};
@@ -466,9 +450,7 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
     double best_v = -1.0;
     uint64_t best_p = ~0ull;
     uint32_t nfl = 0;  // this workgroup's flagged count (uniform)
-    const uint64_t c0 = P.S / NT, c1 = P.E / NT;
-    uint64_t cfirst = c0 + ((g + G - (uint32_t)(c0 % G)) % G);
-    for (uint64_t ch = cfirst; ch <= c1; ch += G) {
+    for (uint64_t ch = c0 + mine; ch <= c1; ch += G) {
       const uint64_t pos = ch * NT + threadIdx.x;
       const bool valid = pos >= P.S && pos <= P.E && A.alive[pos];
       int d = 0;
@@ -540,12 +522,13 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __hip_atomic_fetch_add(A.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    }  // active workgroup
     if (!ctl) continue;
 
     // ============ controller: collect the step (get_close's reduction + get_mean) =========
     if (threadIdx.x == 0) {
       s_abort = 0;
-      const uint32_t want = G * P.step;
+      const uint32_t want = cum + nact;
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       while (__hip_atomic_load(A.arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want) {
         if (timed_out(A, t0)) {
@@ -556,7 +539,11 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const uint64_t t = __builtin_amdgcn_s_memrealtime();
+      t_wait += t - t_mark;
+      t_mark = t;
     }
+    cum += nact;
     __syncthreads();
     if (s_abort) {
       if (threadIdx.x == 0) atomicMax((unsigned long long *)&A.out[3], 99ull);
@@ -565,15 +552,15 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
     // first maximum over workgroups, flagged counts and their offsets
     double bv_ = -1.0;
     uint64_t bp_ = ~0ull, cnt_w = 0;
-    if (threadIdx.x < G) {
-      const AccPartial q = A.partials[threadIdx.x];
+    if (threadIdx.x < nact) {
+      const AccPartial q = A.partials[(c0 + threadIdx.x) % G];
       bv_ = q.val;
       bp_ = q.pos;
       cnt_w = q.nflag;
     }
     uint64_t nflag;
     const uint64_t off_w = block_excl_scan(cnt_w, &nflag, R);
-    if (threadIdx.x < G) s_flag[threadIdx.x] = (uint32_t)off_w;  // G <= NT
+    if (threadIdx.x < nact) s_flag[threadIdx.x] = (uint32_t)off_w;  // nact <= G <= NT
     for (int o = 32; o >= 1; o >>= 1) {
       const double ov = __shfl_xor(bv_, o, 64);
       const uint64_t op = shfl_xor64(bp_, o);
@@ -598,13 +585,13 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
       // remove_available: the flagged positions join the cluster (keys keep bvec order)
       const uint64_t mb = cl_start + M;
       for (uint64_t i = threadIdx.x; i < nflag; i += NT) {
-        uint32_t a = 0, z = G;  // last workgroup with offset <= i
+        uint32_t a = 0, z = nact;  // last active workgroup with offset <= i
         while (z - a > 1) {
           const uint32_t m = (a + z) / 2;
           if (s_flag[m] <= i) a = m;
           else z = m;
         }
-        const uint32_t p = A.flist[(uint64_t)a * A.fcap + (i - s_flag[a])];
+        const uint32_t p = A.flist[(uint64_t)((c0 + a) % G) * A.fcap + (i - s_flag[a])];
         A.mem_pos[mb + i] = p;
         A.mkeys[mb + i] = ((uint64_t)P.step << 32) | p;
         bv.kill_one(p);
@@ -639,6 +626,10 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
       if (p != ~0ull) new_cluster(p);
     }
     __syncthreads();
+    if (threadIdx.x == 0) {
+      const uint64_t t = __builtin_amdgcn_s_memrealtime();
+      t_coll += t - t_mark;
+    }
   }
   if (ctl && threadIdx.x == 0) {
     A.out[0] = ncl;
@@ -646,6 +637,9 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
     A.out[2] = ncand;
     if (err) atomicMax((unsigned long long *)&A.out[3], (unsigned long long)err);
     A.out[4] = cl_start;
+    A.out[5] = t_win;
+    A.out[6] = t_wait;
+    A.out[7] = t_coll;
   }
 }
 
@@ -654,7 +648,7 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
 // LDS bytes of the controller state (all workgroups get the same allocation)
 static size_t accum_lds(const mc_ctx *c, uint32_t nb) {
   const int nch = (int)((c->B * c->width + 15) / 16);
-  return (size_t)2 * nch * 16 + (size_t)c->B * 8 + (size_t)((nb + 1) & ~1u) * 4 + (size_t)((nb + 2) & ~1u) * 4 +
+  return (size_t)2 * nch * 16 + (size_t)c->B * 8 + (size_t)((nb + 1) & ~1u) * 4 + (size_t)((nb + 2) & ~1u) * 8 +
          (size_t)nb * 8 + (c->norder + 31) / 32 * 4;
 }
 

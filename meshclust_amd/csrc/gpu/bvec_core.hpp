@@ -40,6 +40,58 @@ struct BPos {
 
 enum BvErr : int { BV_OK = 0, BV_DEREF = 1, BV_NULL_ITER = 2 };
 
+// bvec::index_of (bvec.cpp:38-53) in O(log nb).  The begin bounds are sorted lengths sampled
+// every bin_size (bvec.cpp:9-24), so they never decrease and the bins i with
+// bnd[i-1] <= point <= bnd[i] (bnd[-1] = 0) form one run [i0, i1]: i0 is the first bin whose
+// bound reaches `point`, i1 the last one whose predecessor's bound does not exceed it.
+template <class Bnd>
+BV_HD inline void bv_index_of_sorted(const Bnd &bnd, uint64_t nb, uint64_t point, uint64_t *plow, uint64_t *phigh) {
+  uint64_t a = 0, z = nb;
+  while (a < z) {
+    const uint64_t m = (a + z) / 2;
+    if (bnd[m] < point) a = m + 1;
+    else z = m;
+  }
+  const uint64_t i0 = a;
+  a = 0;
+  z = nb;
+  while (a < z) {
+    const uint64_t m = (a + z) / 2;
+    if (bnd[m] <= point) a = m + 1;
+    else z = m;
+  }
+  const uint64_t i1 = a < nb - 1 ? a : nb - 1;
+  uint64_t low = nb - 1, high = 0;
+  if (i0 <= i1) {
+    low = i0 ? i0 - 1 : 0;
+    high = i1 ? i1 - 1 : 0;
+  }
+  if (point >= bnd[nb - 1]) high = high > nb - 1 ? high : nb - 1;
+  *plow = low;
+  *phigh = high;
+}
+
+// Fenwick tree over the per-bin alive counts: t[1..nb], t[i] = sum of cnt over
+// (i - lowbit(i), i].  prefix(b) = sum of cnt[0..b); locate finds the bin holding the
+// rank-th alive element (bvec_iterator's walk over bins) in log2(nb) steps.
+template <class Tr>
+BV_HD inline uint64_t bv_fw_prefix(const Tr &t, uint64_t b) {
+  uint64_t s = 0;
+  for (uint64_t i = b; i > 0; i -= i & (~i + 1)) s += t[i];
+  return s;
+}
+template <class Tr>
+BV_HD inline void bv_fw_locate(const Tr &t, uint64_t nb, uint64_t lg, uint64_t rank, uint64_t *pb, uint64_t *pc) {
+  uint64_t pos = 0;
+  for (uint64_t step = lg; step; step >>= 1)
+    if (pos + step <= nb && t[pos + step] <= rank) {
+      pos += step;
+      rank -= t[pos];
+    }
+  *pb = pos;  // nb when rank >= total
+  *pc = rank;
+}
+
 // bvec::inner_index_of (bvec.cpp:55-104)
 template <class A>
 BV_HD inline void bv_inner_index_of(A &a, uint64_t L, uint64_t &idx, uint64_t *pfront, uint64_t *pback) {

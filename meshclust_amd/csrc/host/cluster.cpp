@@ -216,7 +216,7 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
     const size_t n = order.size();
     std::vector<uint32_t> centres(n), ids(n);
     std::vector<uint64_t> moff(n + 1);
-    uint64_t ncl = 0, st[2] = {0, 0};
+    uint64_t ncl = 0, st[5] = {0, 0, 0, 0, 0};
     const int rc = mc_accumulate(ctx, bin_lo.data(), bv.begin_bounds().data(), (uint32_t)bins.size(), cfg.sim,
                                  centres.data(), moff.data(), ids.data(), &ncl, st);
     if (rc == MC_OK) {
@@ -224,6 +224,9 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
         part.push_back(Center{centres[c], std::vector<uint32_t>(ids.begin() + moff[c], ids.begin() + moff[c + 1]), false});
       stats.scan_steps += st[0];
       stats.scan_candidates += st[1];
+      timer.add("accumulate.dev_window", st[2] / 1000.0);
+      timer.add("accumulate.dev_wait", st[3] / 1000.0);
+      timer.add("accumulate.dev_collect", st[4] / 1000.0);
       done = true;
     } else if (rc != MC_ERR_UNSUPPORTED) {
       check(rc, "mc_accumulate");

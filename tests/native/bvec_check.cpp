@@ -74,6 +74,69 @@ struct NaiveAcc {
   uint64_t select(uint64_t b, uint64_t c) { return bv.bins()[b][c]; }
 };
 
+
+// The O(log) forms the device controller uses: index_of by two binary searches over the
+// sorted begin bounds, a Fenwick tree over the per-bin alive counts, and per-bin rank counts
+// from a binary search over the (length-sorted) static positions of the bin.
+struct FastAcc {
+  const BVec &bv;
+  std::vector<uint64_t> lo;
+  std::vector<uint8_t> alive;
+  std::vector<uint64_t> fw;
+  uint64_t lg = 1;
+  FastAcc(const BVec &b, const std::vector<uint64_t> &lo_) : bv(b), lo(lo_) {
+    const uint64_t nb = lo.size() - 1;
+    alive.assign(lo[nb], 0);
+    for (const auto &bin : bv.bins())
+      for (uint32_t p : bin) alive[p] = 1;
+    fw.assign(nb + 1, 0);
+    for (uint64_t bi = 0; bi < nb; bi++)
+      for (uint64_t i = bi + 1; i <= nb; i += i & (~i + 1)) fw[i] += bv.bins()[bi].size();
+    while (lg * 2 <= nb) lg *= 2;
+  }
+  uint64_t nbins() { return lo.size() - 1; }
+  uint64_t cnt(uint64_t b) { return b < nbins() ? bv.bins().at(b).size() : 0; }
+  void index_of(uint64_t point, uint64_t *l, uint64_t *h) {
+    mcg::bv_index_of_sorted(bv.begin_bounds(), nbins(), point, l, h);
+  }
+  uint64_t prefix(uint64_t b) { return mcg::bv_fw_prefix(fw, std::min(b, nbins())); }
+  uint64_t total() { return prefix(nbins()); }
+  void locate_rank(uint64_t rank, uint64_t *b, uint64_t *c) { mcg::bv_fw_locate(fw, nbins(), lg, rank, b, c); }
+  int64_t first_nonempty() {
+    if (!total()) return -1;
+    uint64_t b, c;
+    locate_rank(0, &b, &c);
+    return (int64_t)b;
+  }
+  int64_t last_nonempty() {
+    const uint64_t t = total();
+    if (!t) return -1;
+    uint64_t b, c;
+    locate_rank(t - 1, &b, &c);
+    return (int64_t)b;
+  }
+  uint64_t alive_in(uint64_t a, uint64_t z) {
+    uint64_t n = 0;
+    for (uint64_t p = a; p < z; p++) n += alive[p];
+    return n;
+  }
+  uint64_t count_lt(uint64_t b, uint64_t L) {
+    const auto &sl = bv.static_lengths();
+    const uint64_t k = std::lower_bound(sl.begin() + lo[b], sl.begin() + lo[b + 1], L) - sl.begin();
+    return alive_in(lo[b], k);
+  }
+  uint64_t count_le(uint64_t b, uint64_t L) {
+    const auto &sl = bv.static_lengths();
+    const uint64_t k = std::upper_bound(sl.begin() + lo[b], sl.begin() + lo[b + 1], L) - sl.begin();
+    return alive_in(lo[b], k);
+  }
+  uint64_t select(uint64_t b, uint64_t c) {
+    for (uint64_t p = lo[b]; p < lo[b + 1]; p++)
+      if (alive[p] && c-- == 0) return p;
+    return ~0ull;
+  }
+};
+
 int main() {
   std::mt19937_64 rng(777);
   long checks = 0;
@@ -91,6 +154,8 @@ int main() {
     BVec bv(len, bin_size);
     for (uint32_t i = 0; i < n; i++) bv.insert(i);
     bv.insert_finalize();
+    std::vector<uint64_t> blo(1, 0);
+    for (const auto &bin : bv.bins()) blo.push_back(blo.back() + bin.size());
     const double sims[] = {0.9, 0.55, 0.8, 0.95, 0.99};
     for (int it = 0; it < 4000 && bv.size() > 0; it++) {
       // query
@@ -123,6 +188,17 @@ int main() {
           printf("WINDOW MISMATCH t=%d it=%d: host err %d count %lld S %llu E %llu / core err %d count %lld S %llu E %llu\n",
                  t, it, herr, (long long)c1, (unsigned long long)S1, (unsigned long long)E1, derr, (long long)c2,
                  (unsigned long long)S2, (unsigned long long)E2);
+          return 1;
+        }
+        FastAcc fa(bv, blo);
+        mcg::BPos f2, b2;
+        mcg::bv_get_range(fa, bl, el, f2, b2);
+        uint64_t S3 = 0, E3 = 0;
+        int ferr = 0;
+        int64_t c3 = mcg::bv_window(fa, f2, b2, &S3, &E3, &ferr);
+        if (f2.first != f.first || f2.second != f.second || b2.first != b.first || b2.second != b.second ||
+            ferr != derr || c3 != c2 || (!ferr && c3 > 0 && (S3 != S2 || E3 != E2))) {
+          printf("FAST MISMATCH t=%d it=%d\n", t, it);
           return 1;
         }
         checks++;
