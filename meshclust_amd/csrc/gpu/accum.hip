@@ -52,6 +52,17 @@ struct AccPartial {
   uint32_t pad;
 };
 
+// Static part of a centre's bvec window (bvec::get_range, bvec.cpp:245-278), per point id:
+// the window lengths, the bins index_of picks, and how many static positions of those bins
+// are shorter than (or not longer than) the window lengths.  Only alive counts change during
+// accumulation, so the controller turns these into inner_index_of's ranks with LDS popcounts.
+struct WinTab {
+  uint64_t bl, el;          // (uint64_t)(len * sim), (uint64_t)(len / sim)
+  uint32_t fb, bb;          // index_of(bl).low, index_of(el).high
+  uint32_t kf, kblt, kble;  // static positions of bin fb with length < bl; of bin bb < el, <= el
+  uint32_t pad;
+};
+
 struct AccArgs {
   // chunk-major static layout (scan.hip build_static) and id-major rows (centre)
   const uint4 *hs;
@@ -69,6 +80,7 @@ struct AccArgs {
   const uint32_t *bin_lo;    // nb + 1 static starts
   const uint64_t *bounds;    // nb begin_bounds
   double sim;
+  const WinTab *wtab;        // per point id
   // hand-off
   AccCtl *ctl;
   uint32_t *go, *arrive;
@@ -169,6 +181,7 @@ struct DevBvec {
   const uint64_t *bnd;   // LDS copy, nb
   const uint64_t *plen;  // global: length by static position (non-decreasing inside a bin)
   uint64_t nb, lg;       // lg: highest power of two <= nb
+  WinTab h{~0ull, ~0ull, ~0u, ~0u, 0, 0, 0, 0};  // the current centre's static window data
 
   __device__ uint64_t nbins() const { return nb; }
   // accessor interface of bvec_core.hpp
@@ -216,8 +229,17 @@ struct DevBvec {
     }
     return a;
   }
-  __device__ uint64_t count_lt(uint64_t b, uint64_t L) { return alive_in(lo[b], len_bound(lo[b], lo[b + 1], L, false)); }
-  __device__ uint64_t count_le(uint64_t b, uint64_t L) { return alive_in(lo[b], len_bound(lo[b], lo[b + 1], L, true)); }
+  __device__ uint64_t count_lt(uint64_t b, uint64_t L) {
+    uint64_t k;
+    if (b == h.fb && L == h.bl) k = lo[b] + h.kf;
+    else if (b == h.bb && L == h.el) k = lo[b] + h.kblt;
+    else k = len_bound(lo[b], lo[b + 1], L, false);
+    return alive_in(lo[b], k);
+  }
+  __device__ uint64_t count_le(uint64_t b, uint64_t L) {
+    const uint64_t k = b == h.bb && L == h.el ? lo[b] + h.kble : len_bound(lo[b], lo[b + 1], L, true);
+    return alive_in(lo[b], k);
+  }
   // static position of the c-th alive element of bin b (one wave: popcount scan over the words)
   __device__ uint64_t select(uint64_t b, uint64_t c) const {
     const int lane = threadIdx.x & 63;
@@ -266,6 +288,38 @@ struct DevBvec {
 
 __device__ __forceinline__ bool better(double v, uint64_t p, double bv, uint64_t bp) {
   return v > bv || (v == bv && p < bp);
+}
+
+__device__ uint64_t lower_len(const uint64_t *len_s, uint64_t a, uint64_t z, uint64_t L, bool strict) {
+  while (a < z) {
+    const uint64_t m = (a + z) / 2;
+    if (strict ? len_s[m] <= L : len_s[m] < L) a = m + 1;
+    else z = m;
+  }
+  return a;
+}
+
+__global__ __launch_bounds__(256) void wintab_kernel(const uint64_t *__restrict__ len, uint64_t n,
+                                                     const uint64_t *__restrict__ len_s,
+                                                     const uint32_t *__restrict__ bin_lo,
+                                                     const uint64_t *__restrict__ bnd, uint32_t nb, double sim,
+                                                     WinTab *__restrict__ out) {
+  for (uint64_t id = (uint64_t)blockIdx.x * 256 + threadIdx.x; id < n; id += (uint64_t)gridDim.x * 256) {
+    const uint64_t L = len[id];
+    WinTab w;
+    w.bl = (uint64_t)((double)L * sim);  // get_range(len * sim, len / sim), ClusterFactory.cpp:650
+    w.el = (uint64_t)((double)L / sim);
+    uint64_t lo_, hi_;
+    bv_index_of_sorted(bnd, nb, w.bl, &lo_, &hi_);
+    w.fb = (uint32_t)lo_;
+    bv_index_of_sorted(bnd, nb, w.el, &lo_, &hi_);
+    w.bb = (uint32_t)hi_;
+    w.kf = (uint32_t)(lower_len(len_s, bin_lo[w.fb], bin_lo[w.fb + 1], w.bl, false) - bin_lo[w.fb]);
+    w.kblt = (uint32_t)(lower_len(len_s, bin_lo[w.bb], bin_lo[w.bb + 1], w.el, false) - bin_lo[w.bb]);
+    w.kble = (uint32_t)(lower_len(len_s, bin_lo[w.bb], bin_lo[w.bb + 1], w.el, true) - bin_lo[w.bb]);
+    w.pad = 0;
+    out[id] = w;
+  }
 }
 
 template <typename T>
@@ -371,9 +425,9 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
       uint64_t S = 0, E = 0;
       bool have = false;
       while (last != NONE && !err) {
-        const uint64_t L = A.len[last];
+        bv.h = A.wtab[last];
         BPos f, b;
-        bv_get_range(bv, (uint64_t)((double)L * A.sim), (uint64_t)((double)L / A.sim), f, b);
+        bv_get_range(bv, bv.h.bl, bv.h.el, f, b);
         int e = 0;
         const int64_t count = bv_window(bv, f, b, &S, &E, &e);
         if (e) {
@@ -678,9 +732,16 @@ int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, 
   if (G < 8) G = 8;
   const uint64_t chunks = (c->norder + NT - 1) / NT;
   const uint64_t fcap = ((chunks + G - 1) / G) * NT;
-  if (ensure(c->s_a, sizeof(AccCtl) + 256) || ensure(c->s_b, (size_t)G * sizeof(AccPartial)) ||
+  const size_t part_bytes = ((size_t)G * sizeof(AccPartial) + 255) / 256 * 256;
+  if (ensure(c->s_a, sizeof(AccCtl) + 256) || ensure(c->s_b, part_bytes + c->n * sizeof(WinTab)) ||
       ensure(c->s_c, (size_t)G * fcap * 4 + 16))
     return MC_ERR_OOM;
+  WinTab *d_wtab = (WinTab *)((char *)c->s_b.p + part_bytes);
+  timed_begin(c);
+  wintab_kernel<<<(int)std::min<uint64_t>((c->n + 255) / 256, 2048), 256, 0, c->stream>>>(
+      (const uint64_t *)c->len.p, c->n, (const uint64_t *)c->len_s.p, d_bin_lo, d_bounds, nb, sim, d_wtab);
+  MCG_CHECK(hipGetLastError());
+  timed_end(c, F_FINAL);
   MCG_CHECK(hipMemsetAsync(c->s_a.p, 0, sizeof(AccCtl) + 256, c->stream));
   MCG_CHECK(hipMemsetAsync(c->alive.p, 1, c->norder, c->stream));
   AccArgs A;
@@ -704,6 +765,7 @@ int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, 
   A.bin_lo = d_bin_lo;
   A.bounds = d_bounds;
   A.sim = sim;
+  A.wtab = d_wtab;
   A.ctl = (AccCtl *)c->s_a.p;
   A.go = (uint32_t *)((char *)c->s_a.p + sizeof(AccCtl) + 64);
   A.arrive = (uint32_t *)((char *)c->s_a.p + sizeof(AccCtl) + 128);
