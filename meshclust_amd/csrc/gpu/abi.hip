@@ -7,6 +7,8 @@
 #include <chrono>
 #include <cfloat>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -634,13 +636,13 @@ int mc_accumulate(mc_ctx *c, const uint32_t *bin_lo, const uint64_t *bounds, uin
   TRY(upload(c->s_e, bounds, nbins, c->stream));
   TRY(ensure(c->s_f, n * 4 + 16));
   TRY(ensure(c->s_g, (n + 1) * 8 + 16));
-  TRY(ensure(c->acc_out, 64));
-  MCG_CHECK(hipMemsetAsync(c->acc_out.p, 0, 64, c->stream));
+  TRY(ensure(c->acc_out, 128));
+  MCG_CHECK(hipMemsetAsync(c->acc_out.p, 0, 128, c->stream));
   TRY(launch_accum(c, (const uint32_t *)c->s_d.p, (const uint64_t *)c->s_e.p, nbins, sim, (uint32_t *)c->members.p,
                    (uint64_t *)c->member_keys.p, (uint32_t *)c->s_f.p, (uint64_t *)c->s_g.p,
                    (uint64_t *)c->acc_out.p));
-  uint64_t out[8];
-  MCG_CHECK(hipMemcpyAsync(out, c->acc_out.p, 64, hipMemcpyDeviceToHost, c->stream));
+  uint64_t out[16];
+  MCG_CHECK(hipMemcpyAsync(out, c->acc_out.p, 128, hipMemcpyDeviceToHost, c->stream));
   MCG_CHECK(hipStreamSynchronize(c->stream));
   flush_timers(c);
   if (out[3]) {
@@ -670,12 +672,17 @@ int mc_accumulate(mc_ctx *c, const uint32_t *bin_lo, const uint64_t *bounds, uin
     std::sort(tmp.begin(), tmp.end());
     for (uint64_t i = a; i < b; i++) member_ids[i] = c->h_order[tmp[i - a].second];
   }
+  for (uint64_t k = 0; k < ncl; k++) centre_ids[k] = c->h_order[centre_ids[k]];  // static positions -> ids
   *nclusters = ncl;
   if (stats) {
     stats[0] = out[1];
     stats[1] = out[2];
     for (int i = 0; i < 3; i++) stats[2 + i] = out[5 + i] / 100;  // controller phases, 100 MHz ticks -> us
   }
+  if (getenv("MC_ACCUM_PROFILE"))
+    fprintf(stderr, "[accum] steps %llu window %.3f wait %.3f collect %.3f (reduce %.3f gather+kill %.3f sums %.3f closest %.3f) ms\n",
+            (unsigned long long)out[1], out[5] / 1e5, out[6] / 1e5, out[7] / 1e5, out[8] / 1e5, out[9] / 1e5, out[10] / 1e5,
+            out[11] / 1e5);
   return MC_OK;
 }
 

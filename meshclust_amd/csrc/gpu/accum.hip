@@ -38,7 +38,7 @@ constexpr int NW = NT / 64;
 constexpr uint32_t NONE = 0xffffffffu;
 
 struct AccCtl {  // step parameters written by the controller before each `go`
-  uint32_t centre;
+  uint32_t centre;  // static position of the centre
   uint32_t exit;
   uint64_t S, E;
   uint32_t step;
@@ -80,7 +80,7 @@ struct AccArgs {
   const uint32_t *bin_lo;    // nb + 1 static starts
   const uint64_t *bounds;    // nb begin_bounds
   double sim;
-  const WinTab *wtab;        // per point id
+  const WinTab *wtab;        // per static position
   // hand-off
   AccCtl *ctl;
   uint32_t *go, *arrive;
@@ -90,7 +90,7 @@ struct AccArgs {
   // output
   uint32_t *mem_pos;   // N: member static positions, cluster after cluster
   uint64_t *mkeys;     // N: (step << 32 | pos), 0 for a cluster's seed
-  uint32_t *cl_centre; // N
+  uint32_t *cl_centre; // N: static position of each cluster's centre
   uint64_t *cl_off;    // N + 1
   uint64_t *out;       // [0] clusters [1] steps [2] candidates [3] error [4] members
   uint64_t budget;     // longest wait for one hand-off, s_memrealtime ticks (100 MHz)
@@ -299,13 +299,12 @@ __device__ uint64_t lower_len(const uint64_t *len_s, uint64_t a, uint64_t z, uin
   return a;
 }
 
-__global__ __launch_bounds__(256) void wintab_kernel(const uint64_t *__restrict__ len, uint64_t n,
-                                                     const uint64_t *__restrict__ len_s,
+__global__ __launch_bounds__(256) void wintab_kernel(uint64_t n, const uint64_t *__restrict__ len_s,
                                                      const uint32_t *__restrict__ bin_lo,
                                                      const uint64_t *__restrict__ bnd, uint32_t nb, double sim,
                                                      WinTab *__restrict__ out) {
   for (uint64_t id = (uint64_t)blockIdx.x * 256 + threadIdx.x; id < n; id += (uint64_t)gridDim.x * 256) {
-    const uint64_t L = len[id];
+    const uint64_t L = len_s[id];  // id = static position
     WinTab w;
     w.bl = (uint64_t)((double)L * sim);  // get_range(len * sim, len / sim), ClusterFactory.cpp:650
     w.el = (uint64_t)((double)L / sim);
@@ -350,7 +349,7 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
   DevBvec bv{bits, cnt, fw, lo, bnd, A.len_s, A.nb, lg};
   const bool ctl = g == 0;
   // controller registers (uniform within WG 0)
-  uint32_t last = NONE;      // current centre (point id)
+  uint32_t last = NONE;      // current centre (static position)
   uint64_t cl_start = 0;     // first member index of the current cluster
   uint64_t M = 0;            // members of the current cluster
   uint64_t ncl = 0, nsteps = 0, ncand = 0;
@@ -358,6 +357,7 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
   uint64_t err = 0;
   uint32_t cum = 0;                                  // arrivals expected so far
   uint64_t t_win = 0, t_wait = 0, t_coll = 0, t_mark = 0;  // controller phase time, 100 MHz ticks
+  uint64_t t_sub[4] = {0, 0, 0, 0};  // collect: reduce, gather+kill, column sums, closest
 
   auto finish_cluster = [&]() {
     if (threadIdx.x == 0) {
@@ -412,7 +412,7 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
     __syncthreads();
     const uint64_t p = pop();  // MS: Point<T>* last = points.pop()
     if (p != ~0ull) {
-      last = A.order[p];
+      last = (uint32_t)p;
       new_cluster(p);
     }
   }
@@ -442,7 +442,7 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
         // the OpenMP loop ran no iteration: is_min with a NULL result -> pop a new seed
         const uint64_t p = pop();
         finish_cluster();
-        last = p == ~0ull ? NONE : A.order[p];
+        last = p == ~0ull ? NONE : (uint32_t)p;
         if (p != ~0ull) new_cluster(p);
       }
       step++;
@@ -498,8 +498,8 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
     const uint32_t mine = (g + G - (uint32_t)(c0 % G)) % G;
     if (mine < nact) {
     for (int c = threadIdx.x; c < A.nch; c += NT)
-      clds[c] = reinterpret_cast<const uint4 *>(A.hist + (uint64_t)P.centre * A.pitch)[c];
-    const PInfo pc{A.mag[P.centre], A.sumsq[P.centre], A.len[P.centre]};
+      clds[c] = Rs.chunk(P.centre, c);
+    const PInfo pc{A.mag_s[P.centre], A.sumsq_s[P.centre], A.len_s[P.centre]};
     __syncthreads();
     double best_v = -1.0;
     uint64_t best_p = ~0ull;
@@ -635,6 +635,11 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
         best_val = s_bv[i];
         best_pos = s_bp[i];
       }
+    uint64_t tq = 0;
+    if (threadIdx.x == 0) {
+      tq = __builtin_amdgcn_s_memrealtime();
+      t_sub[0] += tq - t_mark;
+    }
     if (nflag > 0) {
       // remove_available: the flagged positions join the cluster (keys keep bvec order)
       const uint64_t mb = cl_start + M;
@@ -651,16 +656,27 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
         bv.kill_one(p);
       }
       __syncthreads();
+      if (threadIdx.x == 0) {
+        const uint64_t t = __builtin_amdgcn_s_memrealtime();
+        t_sub[1] += t - tq;
+        tq = t;
+      }
       add_rows<T, NT>(Rs, A.mem_pos + mb, (uint32_t)nflag, A.nch, msum);
       M += nflag;
       __syncthreads();
+      if (threadIdx.x == 0) {
+        const uint64_t t = __builtin_amdgcn_s_memrealtime();
+        t_sub[2] += t - tq;
+        tq = t;
+      }
       const uint64_t win0 = mean_closest_fast<T, NT>(Rs, A.mem_pos + cl_start, A.mkeys + cl_start, (uint32_t)M,
                                                      A.mag_s, A.B, A.nch, msum, Fl);
       if (threadIdx.x == 0) R.r0 = win0;  // the winner is thread 0's; make it uniform
       __syncthreads();
       const uint64_t win = R.r0;
       __syncthreads();
-      last = A.order[win];
+      if (threadIdx.x == 0) t_sub[3] += __builtin_amdgcn_s_memrealtime() - tq;
+      last = (uint32_t)win;
       bv.invalidate();
     } else if (best_pos != ~0ull) {
       // is_min with a result: the best candidate seeds the next cluster (bvec::erase)
@@ -671,12 +687,12 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
       __syncthreads();
       bv.invalidate();
       finish_cluster();
-      last = A.order[best_pos];
+      last = (uint32_t)best_pos;
       new_cluster(best_pos);
     } else {
       const uint64_t p = pop();
       finish_cluster();
-      last = p == ~0ull ? NONE : A.order[p];
+      last = p == ~0ull ? NONE : (uint32_t)p;
       if (p != ~0ull) new_cluster(p);
     }
     __syncthreads();
@@ -694,6 +710,7 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
     A.out[5] = t_win;
     A.out[6] = t_wait;
     A.out[7] = t_coll;
+    for (int i = 0; i < 4; i++) A.out[8 + i] = t_sub[i];
   }
 }
 
@@ -739,7 +756,7 @@ int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, 
   WinTab *d_wtab = (WinTab *)((char *)c->s_b.p + part_bytes);
   timed_begin(c);
   wintab_kernel<<<(int)std::min<uint64_t>((c->n + 255) / 256, 2048), 256, 0, c->stream>>>(
-      (const uint64_t *)c->len.p, c->n, (const uint64_t *)c->len_s.p, d_bin_lo, d_bounds, nb, sim, d_wtab);
+      c->norder, (const uint64_t *)c->len_s.p, d_bin_lo, d_bounds, nb, sim, d_wtab);
   MCG_CHECK(hipGetLastError());
   timed_end(c, F_FINAL);
   MCG_CHECK(hipMemsetAsync(c->s_a.p, 0, sizeof(AccCtl) + 256, c->stream));
