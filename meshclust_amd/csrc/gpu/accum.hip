@@ -286,6 +286,31 @@ struct DevBvec {
   __device__ void invalidate() {}
 };
 
+// Column sums of rows[0..M) (static positions) added into sum[0..B) (LDS).  Thread (chunk c,
+// row group g) accumulates chunk c of rows g, g + ng, ... in registers and adds its totals once,
+// so the LDS atomics per step do not grow with the number of new members.
+template <typename T>
+__device__ void add_rows_acc(const RowRef &R, const uint32_t *rows, uint32_t M, int nch, uint64_t *sum) {
+  constexpr int per = 16 / (int)sizeof(T);
+  const int ng = nch < NT ? NT / nch : 1;
+  for (int item = threadIdx.x; item < nch * ng; item += NT) {
+    const int c = item % nch, grp = item / nch;
+    uint64_t a[per];
+#pragma unroll
+    for (int e = 0; e < per; e++) a[e] = 0;
+#pragma unroll 4
+    for (uint32_t q = (uint32_t)grp; q < M; q += (uint32_t)ng) {
+      const uint4 v = R.chunk(rows[q], c);
+      const T *pv = reinterpret_cast<const T *>(&v);
+#pragma unroll
+      for (int e = 0; e < per; e++) a[e] += pv[e];
+    }
+#pragma unroll
+    for (int e = 0; e < per; e++)
+      if (a[e]) atomicAdd((unsigned long long *)&sum[c * per + e], (unsigned long long)a[e]);
+  }
+}
+
 __device__ __forceinline__ bool better(double v, uint64_t p, double bv, uint64_t bp) {
   return v > bv || (v == bv && p < bp);
 }
@@ -661,7 +686,7 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
         t_sub[1] += t - tq;
         tq = t;
       }
-      add_rows<T, NT>(Rs, A.mem_pos + mb, (uint32_t)nflag, A.nch, msum);
+      add_rows_acc<T>(Rs, A.mem_pos + mb, (uint32_t)nflag, A.nch, msum);
       M += nflag;
       __syncthreads();
       if (threadIdx.x == 0) {

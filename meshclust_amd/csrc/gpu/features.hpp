@@ -306,7 +306,8 @@ __device__ uint64_t mean_closest_fast(const RowRef &R, const uint32_t *rows, con
     T *pv = reinterpret_cast<T *>(&v);
     for (int i = 0; i < per; i++) {
       const int b = c * per + i;
-      const uint64_t F = b < B ? sum[b] / M : 0;
+      const uint64_t S = b < B ? sum[b] : 0;
+      const uint64_t F = (S >> 32) == 0 ? (uint64_t)((uint32_t)S / M) : S / M;  // 32-bit divide when it fits
       pv[i] = (T)F;
       part += F;
     }
@@ -320,8 +321,16 @@ __device__ uint64_t mean_closest_fast(const RowRef &R, const uint32_t *rows, con
   for (uint32_t q = threadIdx.x; q < M; q += NTH) {
     const uint64_t r = rows[q];
     Acc<T> acc;
+    if (nch == 16) {  // k = 4 at 8 bits (or k = 3 at 16): all loads in flight at once
+      uint4 v[16];
+#pragma unroll
+      for (int c = 0; c < 16; c++) v[c] = R.chunk(r, c);
+#pragma unroll
+      for (int c = 0; c < 16; c++) acc.add(v[c], Fl[c]);
+    } else {
 #pragma unroll 8
-    for (int c = 0; c < nch; c++) acc.add(R.chunk(r, c), Fl[c]);
+      for (int c = 0; c < nch; c++) acc.add(R.chunk(r, c), Fl[c]);
+    }
     const uint64_t mp = mags[r];
     const PS s = acc.finish(mp, sumF);
     const double frac = (double)(2 * s.smin) / (double)(mp + sumF);
