@@ -36,6 +36,7 @@ namespace {
 constexpr int NT = 512;
 constexpr int NW = NT / 64;
 constexpr uint32_t NONE = 0xffffffffu;
+constexpr uint32_t MCAP = 1024;  // members of the current cluster mirrored in LDS
 
 struct AccCtl {  // step parameters written by the controller before each `go`
   uint32_t centre;  // static position of the centre
@@ -351,6 +352,8 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
   extern __shared__ __attribute__((aligned(16))) uint4 dyn[];
   __shared__ Red R;
   __shared__ uint32_t s_flag[NT];
+  __shared__ uint32_t s_mpos[MCAP];  // current cluster: static positions and tie keys (first MCAP)
+  __shared__ uint64_t s_mkey[MCAP];
   __shared__ uint32_t s_wcnt[NW];
   __shared__ double s_bv[NW];
   __shared__ uint64_t s_bp[NW];
@@ -397,6 +400,8 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
     if (threadIdx.x == 0) {
       A.mem_pos[cl_start] = (uint32_t)pos;
       A.mkeys[cl_start] = 0;
+      s_mpos[0] = (uint32_t)pos;
+      s_mkey[0] = 0;
     }
     for (int b = threadIdx.x; b < A.B; b += NT) msum[b] = elem<T>(Rs, pos, b);
     M = 1;
@@ -676,8 +681,13 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
           else z = m;
         }
         const uint32_t p = A.flist[(uint64_t)((c0 + a) % G) * A.fcap + (i - s_flag[a])];
+        const uint64_t key = ((uint64_t)P.step << 32) | p;
         A.mem_pos[mb + i] = p;
-        A.mkeys[mb + i] = ((uint64_t)P.step << 32) | p;
+        A.mkeys[mb + i] = key;
+        if (M + i < MCAP) {
+          s_mpos[M + i] = p;
+          s_mkey[M + i] = key;
+        }
         bv.kill_one(p);
       }
       __syncthreads();
@@ -686,7 +696,10 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
         t_sub[1] += t - tq;
         tq = t;
       }
-      add_rows_acc<T>(Rs, A.mem_pos + mb, (uint32_t)nflag, A.nch, msum);
+      // row indices from LDS when the cluster fits there: the chunk loads are then the only
+      // global round trip
+      const bool in_lds = M + nflag <= MCAP;
+      add_rows_acc<T>(Rs, in_lds ? s_mpos + M : A.mem_pos + mb, (uint32_t)nflag, A.nch, msum);
       M += nflag;
       __syncthreads();
       if (threadIdx.x == 0) {
@@ -694,7 +707,8 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
         t_sub[2] += t - tq;
         tq = t;
       }
-      const uint64_t win0 = mean_closest_fast<T, NT>(Rs, A.mem_pos + cl_start, A.mkeys + cl_start, (uint32_t)M,
+      const uint64_t win0 = mean_closest_fast<T, NT>(Rs, in_lds ? s_mpos : A.mem_pos + cl_start,
+                                                     in_lds ? s_mkey : A.mkeys + cl_start, (uint32_t)M,
                                                      A.mag_s, A.B, A.nch, msum, Fl);
       if (threadIdx.x == 0) R.r0 = win0;  // the winner is thread 0's; make it uniform
       __syncthreads();
