@@ -19,10 +19,19 @@
 //                       first maximum is reduced per workgroup.
 //
 // Static chunk c (NT positions) is always scanned by workgroup c mod G, and G is a multiple
-// of 8, so a chunk always lands on the same XCD and its rows stay in that XCD's L2.
-// Hand-offs use the agent-scope release/acquire pattern of cdna_hip_programming.md G16 on
-// two monotonic counters (go: controller -> all, arrive: all -> controller); every spin has
-// a deadline so a fault cannot leave a wave spinning forever.
+// of 8, so a chunk always lands on the same XCD and its rows stay in that XCD's L2; the alive
+// flags of a workgroup's chunks live in its own LDS.
+//
+// Hand-offs carry only a few words, so they use sc1 stores and loads (relaxed agent-scope
+// atomics: L1 bypassed, coherent across XCDs) with a drain before each signal instead of
+// release/acquire fences (MI355X_MICROARCH.md hand-off table, first row):
+//   controller -> workers   a step record in a ring {step|centre, S, E, step|kill-log length}
+//                           written seqlock-style, then `go` = step; pops / erases are appended
+//                           to a kill log that owners apply before their next scan
+//   workers -> controller   flagged positions + {max, position, count} partial, then one
+//                           arrival per workgroup on `arrive`
+// Only the workgroups owning a chunk of the window take part in a step.  Every spin has a
+// deadline, so a fault cannot leave a wave spinning forever (error 99).
 #include <algorithm>
 #include <cstring>
 
@@ -37,14 +46,8 @@ constexpr int NT = 512;
 constexpr int NW = NT / 64;
 constexpr uint32_t NONE = 0xffffffffu;
 constexpr uint32_t MCAP = 1024;  // members of the current cluster mirrored in LDS
+constexpr uint32_t RING = 64;    // step records kept for workgroups that read them late
 
-struct AccCtl {  // step parameters written by the controller before each `go`
-  uint32_t centre;  // static position of the centre
-  uint32_t exit;
-  uint64_t S, E;
-  uint32_t step;
-  uint32_t pad;
-};
 
 struct AccPartial {
   double val;
@@ -70,11 +73,6 @@ struct AccArgs {
   uint64_t npad;
   int nch, B;
   const uint64_t *mag_s, *sumsq_s, *len_s;
-  const uint32_t *order;
-  uint8_t *alive;
-  const uint8_t *hist;
-  uint64_t pitch;
-  const uint64_t *mag, *sumsq, *len;
   // bvec structure
   uint64_t N;
   uint32_t nb;
@@ -82,8 +80,9 @@ struct AccArgs {
   const uint64_t *bounds;    // nb begin_bounds
   double sim;
   const WinTab *wtab;        // per static position
-  // hand-off
-  AccCtl *ctl;
+  // hand-off (every handed-off word is stored and loaded with sc1 accesses, see below)
+  uint64_t *ring;   // RING step records of 4 words
+  uint32_t *klog;   // static positions killed by the controller (pop / erase), append-only
   uint32_t *go, *arrive;
   AccPartial *partials;
   uint32_t *flist;  // G * fcap
@@ -107,40 +106,24 @@ __device__ __forceinline__ bool timed_out(const AccArgs &A, uint64_t t0) {
   return __builtin_amdgcn_s_memrealtime() - t0 > A.budget;
 }
 
-__device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
-  for (int o = 32; o >= 1; o >>= 1) v += shfl_xor64(v, o);
-  return v;
+// Hand-off primitives.  Relaxed agent-scope atomics lower to global loads/stores with sc1:
+// they bypass the CU's L1 and are coherent across XCDs without release/acquire fences when
+// every handed-off word is written this way, each storing wave drains (vmcnt(0)) before
+// the signal and every load of the words is also sc1 (MI355X_MICROARCH.md, hand-off table,
+// first row).  The drain is inline asm so the compiler cannot drop it.
+__device__ __forceinline__ void st64(uint64_t *p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ uint64_t wave_min(uint64_t v) {
-  for (int o = 32; o >= 1; o >>= 1) {
-    uint64_t w = shfl_xor64(v, o);
-    v = w < v ? w : v;
-  }
-  return v;
+__device__ __forceinline__ void st32(uint32_t *p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ uint64_t wave_max(uint64_t v) {
-  for (int o = 32; o >= 1; o >>= 1) {
-    uint64_t w = shfl_xor64(v, o);
-    v = w > v ? w : v;
-  }
-  return v;
+__device__ __forceinline__ uint64_t ld64(const uint64_t *p) {
+  return __hip_atomic_load(const_cast<uint64_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-
-// kind 0 sum, 1 min, 2 max; uniform result
-__device__ uint64_t block_reduce(uint64_t v, int kind, Red &R) {
-  v = kind == 0 ? wave_sum(v) : kind == 1 ? wave_min(v) : wave_max(v);
-  const int w = threadIdx.x >> 6;
-  __syncthreads();
-  if ((threadIdx.x & 63) == 0) R.a[w] = v;
-  __syncthreads();
-  uint64_t r = R.a[0];
-  for (int i = 1; i < NW; i++) {
-    const uint64_t x = R.a[i];
-    r = kind == 0 ? r + x : kind == 1 ? (x < r ? x : r) : (x > r ? x : r);
-  }
-  __syncthreads();
-  return r;
+__device__ __forceinline__ uint32_t ld32(const uint32_t *p) {
+  return __hip_atomic_load(const_cast<uint32_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+__device__ __forceinline__ void drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // exclusive prefix of v over threads (thread order); *total = sum
 __device__ uint64_t block_excl_scan(uint64_t v, uint64_t *total, Red &R) {
@@ -358,6 +341,7 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
   __shared__ double s_bv[NW];
   __shared__ uint64_t s_bp[NW];
   __shared__ uint32_t s_go;
+  __shared__ uint64_t s_rec[4];
   __shared__ int s_abort;
   const uint32_t G = gridDim.x, g = blockIdx.x;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -372,6 +356,12 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
   uint32_t *lo = fw + ((A.nb + 2) & ~1u);
   uint64_t *bnd = reinterpret_cast<uint64_t *>(lo + ((A.nb + 2) & ~1u));
   uint32_t *bits = reinterpret_cast<uint32_t *>(bnd + A.nb);
+  // every workgroup: alive flags of the positions it owns (chunks g, g + G, ...), local index
+  // (chunk / G) * NT + offset.  Flagged candidates are cleared by the owner; the controller's
+  // pops and erases arrive through the kill log.
+  uint8_t *lal = reinterpret_cast<uint8_t *>(bits + (A.N + 31) / 32);
+  for (uint64_t i = threadIdx.x; i < A.fcap; i += NT) lal[i] = 1;
+  uint32_t kcur = 0;  // kill-log entries applied so far
   uint64_t lg = 1;
   while (lg * 2 <= A.nb) lg *= 2;
   DevBvec bv{bits, cnt, fw, lo, bnd, A.len_s, A.nb, lg};
@@ -384,6 +374,7 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
   uint32_t step = 0;
   uint64_t err = 0;
   uint32_t cum = 0;                                  // arrivals expected so far
+  uint32_t kn = 0;                                   // kill-log length
   uint64_t t_win = 0, t_wait = 0, t_coll = 0, t_mark = 0;  // controller phase time, 100 MHz ticks
   uint64_t t_sub[4] = {0, 0, 0, 0};  // collect: reduce, gather+kill, column sums, closest
 
@@ -413,8 +404,9 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
     const uint64_t p = bv.select((uint64_t)b, 0);
     if (threadIdx.x == 0) {
       bv.kill_one(p);
-      A.alive[p] = 0;
+      st32(A.klog + kn, (uint32_t)p);
     }
+    kn++;
     __syncthreads();
     bv.invalidate();
     return p;
@@ -476,20 +468,20 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
         if (p != ~0ull) new_cluster(p);
       }
       step++;
-      if (threadIdx.x == 0) {
-        A.ctl->centre = last;
-        A.ctl->S = S;
-        A.ctl->E = E;
-        A.ctl->step = step;
-        A.ctl->exit = have ? 0 : 1;
-      }
       if (have) nsteps++;
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains before the barrier
-      __syncthreads();
       if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(A.go, step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // step record {step|centre, S, E, step|kill-log length}: the tagged first and last words
+        // are written before and after the body, so a reader that sees both tags equal to the
+        // step it was signalled read an untorn record (seqlock order; readers go in reverse)
+        uint64_t *r = A.ring + (uint64_t)(step % RING) * 4;
+        st64(r + 0, ((uint64_t)step << 32) | (have ? last : NONE));
+        drain();
+        st64(r + 1, S);
+        st64(r + 2, E);
+        drain();
+        st64(r + 3, ((uint64_t)step << 32) | kn);
+        drain();  // record and kill-log entries (all stored by this lane) complete
+        st32(A.go, step);
         const uint64_t t = __builtin_amdgcn_s_memrealtime();
         t_win += t - t_mark;
         t_mark = t;
@@ -498,18 +490,33 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
     // ============ everyone: wait for the step ============================================
     if (threadIdx.x == 0) {
       s_abort = 0;
-      uint32_t v;
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      while ((v = __hip_atomic_load(A.go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == seen) {
-        if (timed_out(A, t0)) {
+      for (;;) {
+        uint32_t v;
+        while ((v = ld32(A.go)) == seen) {
+          if (timed_out(A, t0)) break;
+          __builtin_amdgcn_s_sleep(1);
+        }
+        if (v == seen) {
           s_abort = 1;
           break;
         }
-        __builtin_amdgcn_s_sleep(1);
+        const uint64_t *r = A.ring + (uint64_t)(v % RING) * 4;
+        const uint64_t w3 = ld64(r + 3);
+        drain();
+        const uint64_t w1 = ld64(r + 1), w2 = ld64(r + 2);
+        drain();
+        const uint64_t w0 = ld64(r + 0);
+        if ((w0 >> 32) == v && (w3 >> 32) == v) {
+          s_rec[0] = w0;
+          s_rec[1] = w1;
+          s_rec[2] = w2;
+          s_rec[3] = w3;
+          s_go = v;
+          break;
+        }
+        // that slot is being rewritten for a later step: read `go` again
       }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      s_go = v;
     }
     __syncthreads();
     if (s_abort) {
@@ -517,8 +524,13 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
       return;
     }
     seen = s_go;
-    const AccCtl P = *A.ctl;
-    if (P.exit) break;
+    struct {
+      uint32_t centre;
+      uint64_t S, E;
+      uint32_t step;
+    } P{(uint32_t)s_rec[0], s_rec[1], s_rec[2], seen};
+    const uint32_t kend = (uint32_t)s_rec[3];
+    if (P.centre == NONE) break;
 
     // ============ workgroups owning chunks of the window: scan them (Trainer::get_close) ===
     // Chunk c0 + i belongs to workgroup (c0 + i) mod G; only the nact workgroups owning a
@@ -527,6 +539,12 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
     const uint32_t nact = (uint32_t)(c1 - c0 + 1 < (uint64_t)G ? c1 - c0 + 1 : (uint64_t)G);
     const uint32_t mine = (g + G - (uint32_t)(c0 % G)) % G;
     if (mine < nact) {
+    for (uint64_t i = kcur + threadIdx.x; i < kend; i += NT) {  // controller kills since last time
+      const uint32_t p = ld32(A.klog + i);
+      const uint64_t ch = p / NT;
+      if (ch % G == g) lal[(ch / G) * NT + p % NT] = 0;
+    }
+    kcur = kend;
     for (int c = threadIdx.x; c < A.nch; c += NT)
       clds[c] = Rs.chunk(P.centre, c);
     const PInfo pc{A.mag_s[P.centre], A.sumsq_s[P.centre], A.len_s[P.centre]};
@@ -536,7 +554,8 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
     uint32_t nfl = 0;  // this workgroup's flagged count (uniform)
     for (uint64_t ch = c0 + mine; ch <= c1; ch += G) {
       const uint64_t pos = ch * NT + threadIdx.x;
-      const bool valid = pos >= P.S && pos <= P.E && A.alive[pos];
+      uint8_t *la = lal + (ch / G) * NT + threadIdx.x;
+      const bool valid = pos >= P.S && pos <= P.E && *la;
       int d = 0;
       if (valid) {
         Acc<T> acc;
@@ -563,7 +582,7 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
           best_v = cv;
           best_p = pos;
         }
-        if (d) A.alive[pos] = 0;
+        if (d) *la = 0;
       }
       // ordered compaction of this chunk's flagged positions (ascending position)
       const uint64_t bal = __ballot(d);
@@ -575,7 +594,7 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
         if (i < wv) before += s_wcnt[i];
         tot += s_wcnt[i];
       }
-      if (d) A.flist[(uint64_t)g * A.fcap + before + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull))] = (uint32_t)pos;
+      if (d) st32(A.flist + (uint64_t)g * A.fcap + before + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull)), (uint32_t)pos);
       nfl += tot;
       __syncthreads();
     }
@@ -601,9 +620,11 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
           v = s_bv[i];
           p = s_bp[i];
         }
-      A.partials[g] = AccPartial{v, p, nfl, 0};
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      uint64_t *q = reinterpret_cast<uint64_t *>(A.partials + g);
+      st64(q + 0, (uint64_t)__double_as_longlong(v));
+      st64(q + 1, p);
+      st64(q + 2, nfl);
+      drain();  // this lane's partial; the other waves' list stores drained before the barrier
       __hip_atomic_fetch_add(A.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     }  // active workgroup
@@ -614,15 +635,13 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
       s_abort = 0;
       const uint32_t want = cum + nact;
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      while (__hip_atomic_load(A.arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want) {
+      while (ld32(A.arrive) != want) {
         if (timed_out(A, t0)) {
           s_abort = 1;
           break;
         }
         __builtin_amdgcn_s_sleep(1);
       }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const uint64_t t = __builtin_amdgcn_s_memrealtime();
       t_wait += t - t_mark;
       t_mark = t;
@@ -637,10 +656,10 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
     double bv_ = -1.0;
     uint64_t bp_ = ~0ull, cnt_w = 0;
     if (threadIdx.x < nact) {
-      const AccPartial q = A.partials[(c0 + threadIdx.x) % G];
-      bv_ = q.val;
-      bp_ = q.pos;
-      cnt_w = q.nflag;
+      const uint64_t *q = reinterpret_cast<const uint64_t *>(A.partials + (c0 + threadIdx.x) % G);
+      bv_ = __longlong_as_double((long long)ld64(q + 0));
+      bp_ = ld64(q + 1);
+      cnt_w = ld64(q + 2);
     }
     uint64_t nflag;
     const uint64_t off_w = block_excl_scan(cnt_w, &nflag, R);
@@ -680,7 +699,7 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
           if (s_flag[m] <= i) a = m;
           else z = m;
         }
-        const uint32_t p = A.flist[(uint64_t)((c0 + a) % G) * A.fcap + (i - s_flag[a])];
+        const uint32_t p = ld32(A.flist + (uint64_t)((c0 + a) % G) * A.fcap + (i - s_flag[a]));
         const uint64_t key = ((uint64_t)P.step << 32) | p;
         A.mem_pos[mb + i] = p;
         A.mkeys[mb + i] = key;
@@ -721,8 +740,9 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
       // is_min with a result: the best candidate seeds the next cluster (bvec::erase)
       if (threadIdx.x == 0) {
         bv.kill_one(best_pos);
-        A.alive[best_pos] = 0;
+        st32(A.klog + kn, (uint32_t)best_pos);
       }
+      kn++;
       __syncthreads();
       bv.invalidate();
       finish_cluster();
@@ -755,25 +775,41 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
 
 }  // namespace
 
-// LDS bytes of the controller state (all workgroups get the same allocation)
-static size_t accum_lds(const mc_ctx *c, uint32_t nb) {
+// Grid: one workgroup per CU, a multiple of the 8 XCDs.
+static uint32_t accum_grid(const mc_ctx *c) {
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess) cus = 256;
+  uint32_t G = (uint32_t)cus / 8 * 8;
+  if (G > (uint32_t)NT) G = NT;
+  if (G < 8) G = 8;
+  return G;
+}
+// positions owned by one workgroup (its chunks g, g + G, ...)
+static uint64_t accum_fcap(const mc_ctx *c, uint32_t G) {
+  const uint64_t chunks = (c->norder + NT - 1) / NT;
+  return ((chunks + G - 1) / G) * NT;
+}
+
+// LDS bytes: controller state + the per-workgroup alive flags (all workgroups get the same
+// allocation)
+static size_t accum_lds(const mc_ctx *c, uint32_t nb, uint32_t G) {
   const int nch = (int)((c->B * c->width + 15) / 16);
   return (size_t)2 * nch * 16 + (size_t)c->B * 8 + (size_t)((nb + 1) & ~1u) * 4 + (size_t)((nb + 2) & ~1u) * 8 +
-         (size_t)nb * 8 + (c->norder + 31) / 32 * 4;
+         (size_t)nb * 8 + (c->norder + 31) / 32 * 4 + accum_fcap(c, G);
 }
 
 bool accum_supported(const mc_ctx *c, uint32_t nb) {
   if (c->width != 1 && c->width != 2) return false;
   if (c->cls.align) return false;
   if (c->norder >= (1ull << 31)) return false;
-  return accum_lds(c, nb) + 8192 <= 160 * 1024 - 4096;
+  // + static LDS (reductions, member mirror) and headroom
+  return accum_lds(c, nb, accum_grid(c)) + 24 * 1024 <= 160 * 1024;
 }
 
 int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, uint32_t nb, double sim,
                  uint32_t *d_mem_pos, uint64_t *d_mkeys, uint32_t *d_cl_centre, uint64_t *d_cl_off, uint64_t *d_out) {
-  hipDeviceProp_t prop;
-  MCG_CHECK(hipGetDeviceProperties(&prop, c->device));
-  const size_t lds = accum_lds(c, nb);
+  const uint32_t G = accum_grid(c);
+  const size_t lds = accum_lds(c, nb, G);
   const void *fn = c->width == 1 ? reinterpret_cast<const void *>(&accum_kernel<uint8_t>)
                                  : reinterpret_cast<const void *>(&accum_kernel<uint16_t>);
   MCG_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -783,14 +819,12 @@ int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, 
     set_error("accumulation kernel does not fit on a CU");
     return MC_ERR_HIP;
   }
-  uint32_t G = (uint32_t)prop.multiProcessorCount / 8 * 8;  // one per CU, a multiple of the 8 XCDs
-  if (G > NT) G = NT;
-  if (G < 8) G = 8;
-  const uint64_t chunks = (c->norder + NT - 1) / NT;
-  const uint64_t fcap = ((chunks + G - 1) / G) * NT;
+  const uint64_t fcap = accum_fcap(c, G);
+  const size_t hand = 256 + (size_t)RING * 32;  // go, arrive, step ring
   const size_t part_bytes = ((size_t)G * sizeof(AccPartial) + 255) / 256 * 256;
-  if (ensure(c->s_a, sizeof(AccCtl) + 256) || ensure(c->s_b, part_bytes + c->n * sizeof(WinTab)) ||
-      ensure(c->s_c, (size_t)G * fcap * 4 + 16))
+  const size_t flist_bytes = ((size_t)G * fcap * 4 + 255) / 256 * 256;
+  if (ensure(c->s_a, hand) || ensure(c->s_b, part_bytes + c->n * sizeof(WinTab)) ||
+      ensure(c->s_c, flist_bytes + c->norder * 4 + 16))
     return MC_ERR_OOM;
   WinTab *d_wtab = (WinTab *)((char *)c->s_b.p + part_bytes);
   timed_begin(c);
@@ -798,8 +832,7 @@ int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, 
       c->norder, (const uint64_t *)c->len_s.p, d_bin_lo, d_bounds, nb, sim, d_wtab);
   MCG_CHECK(hipGetLastError());
   timed_end(c, F_FINAL);
-  MCG_CHECK(hipMemsetAsync(c->s_a.p, 0, sizeof(AccCtl) + 256, c->stream));
-  MCG_CHECK(hipMemsetAsync(c->alive.p, 1, c->norder, c->stream));
+  MCG_CHECK(hipMemsetAsync(c->s_a.p, 0, hand, c->stream));
   AccArgs A;
   memset(&A, 0, sizeof A);
   A.hs = (const uint4 *)c->hs.p;
@@ -809,24 +842,18 @@ int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, 
   A.mag_s = (const uint64_t *)c->mag_s.p;
   A.sumsq_s = (const uint64_t *)c->sumsq_s.p;
   A.len_s = (const uint64_t *)c->len_s.p;
-  A.order = (const uint32_t *)c->order.p;
-  A.alive = (uint8_t *)c->alive.p;
-  A.hist = (const uint8_t *)c->hist.p;
-  A.pitch = c->pitch;
-  A.mag = (const uint64_t *)c->mag.p;
-  A.sumsq = (const uint64_t *)c->sumsq.p;
-  A.len = (const uint64_t *)c->len.p;
   A.N = c->norder;
   A.nb = nb;
   A.bin_lo = d_bin_lo;
   A.bounds = d_bounds;
   A.sim = sim;
   A.wtab = d_wtab;
-  A.ctl = (AccCtl *)c->s_a.p;
-  A.go = (uint32_t *)((char *)c->s_a.p + sizeof(AccCtl) + 64);
-  A.arrive = (uint32_t *)((char *)c->s_a.p + sizeof(AccCtl) + 128);
+  A.go = (uint32_t *)c->s_a.p;
+  A.arrive = (uint32_t *)((char *)c->s_a.p + 128);
+  A.ring = (uint64_t *)((char *)c->s_a.p + 256);
   A.partials = (AccPartial *)c->s_b.p;
   A.flist = (uint32_t *)c->s_c.p;
+  A.klog = (uint32_t *)((char *)c->s_c.p + flist_bytes);
   A.fcap = fcap;
   A.mem_pos = d_mem_pos;
   A.mkeys = d_mkeys;
