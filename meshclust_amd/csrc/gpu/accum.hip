@@ -25,8 +25,8 @@
 // Hand-offs carry only a few words, so they use sc1 stores and loads (relaxed agent-scope
 // atomics: L1 bypassed, coherent across XCDs) with a drain before each signal instead of
 // release/acquire fences (MI355X_MICROARCH.md hand-off table, first row):
-//   controller -> workers   a step record in a ring {step|centre, S, E, step|kill-log length}
-//                           written seqlock-style, then `go` = step; pops / erases are appended
+//   controller -> workers   a step record in a ring {centre, S, E, kill-log length}, each word
+//                           tagged with the step, then `go` = step; pops / erases are appended
 //                           to a kill log that owners apply before their next scan
 //   workers -> controller   flagged positions + {max, position, count} partial, then one
 //                           arrival per workgroup on `arrive`
@@ -470,16 +470,15 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
       step++;
       if (have) nsteps++;
       if (threadIdx.x == 0) {
-        // step record {step|centre, S, E, step|kill-log length}: the tagged first and last words
-        // are written before and after the body, so a reader that sees both tags equal to the
-        // step it was signalled read an untorn record (seqlock order; readers go in reverse)
+        // step record: every word carries the step in its upper half (positions < 2^31), so a
+        // reader that finds all four tags equal to the step it was signalled holds an untorn
+        // record even if the slot is being reused
         uint64_t *r = A.ring + (uint64_t)(step % RING) * 4;
-        st64(r + 0, ((uint64_t)step << 32) | (have ? last : NONE));
-        drain();
-        st64(r + 1, S);
-        st64(r + 2, E);
-        drain();
-        st64(r + 3, ((uint64_t)step << 32) | kn);
+        const uint64_t tag = (uint64_t)step << 32;
+        st64(r + 0, tag | (have ? last : NONE));
+        st64(r + 1, tag | S);
+        st64(r + 2, tag | E);
+        st64(r + 3, tag | kn);
         drain();  // record and kill-log entries (all stored by this lane) complete
         st32(A.go, step);
         const uint64_t t = __builtin_amdgcn_s_memrealtime();
@@ -502,15 +501,11 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
           break;
         }
         const uint64_t *r = A.ring + (uint64_t)(v % RING) * 4;
-        const uint64_t w3 = ld64(r + 3);
-        drain();
-        const uint64_t w1 = ld64(r + 1), w2 = ld64(r + 2);
-        drain();
-        const uint64_t w0 = ld64(r + 0);
-        if ((w0 >> 32) == v && (w3 >> 32) == v) {
+        const uint64_t w0 = ld64(r + 0), w1 = ld64(r + 1), w2 = ld64(r + 2), w3 = ld64(r + 3);
+        if ((w0 >> 32) == v && (w1 >> 32) == v && (w2 >> 32) == v && (w3 >> 32) == v) {
           s_rec[0] = w0;
-          s_rec[1] = w1;
-          s_rec[2] = w2;
+          s_rec[1] = (uint32_t)w1;
+          s_rec[2] = (uint32_t)w2;
           s_rec[3] = w3;
           s_go = v;
           break;
