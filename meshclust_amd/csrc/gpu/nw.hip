@@ -282,6 +282,257 @@ int launch_bucket(mc_ctx *c, NWPairs q) {
   return MC_OK;
 }
 
+
+// ---------------------------------------------------------------------------------------
+// Latency form for small batches (the training sampler's dependent alignment rounds): one
+// pair per workgroup of W waves.  Wave w owns rows [w*64*R, (w+1)*64*R) of each row block and
+// runs 64 + KLAG steps behind wave w-1; lane 63 of wave w-1 leaves its bottom row for column
+// j in an LDS ring that lane 0 of wave w reads KLAG + 1 steps later.  A workgroup barrier
+// every KLAG steps orders those writes and reads (a slot is rewritten RING_C columns later,
+// with a barrier in between).  Inside a wave the bottom row moves down by one lane per step
+// with DPP wave_shr:1 (a VALU move, no LDS round trip).
+constexpr int KLAG = 16, RING_C = 64;
+
+__device__ __forceinline__ int dpp_shr1(int v) { return __builtin_amdgcn_mov_dpp(v, 0x138, 0xf, 0xf, false); }
+template <typename P>
+__device__ __forceinline__ P dshr(P v) {
+  if constexpr (sizeof(P) == 4) {
+    return (P)(uint32_t)dpp_shr1((int)v);
+  } else {
+    const uint32_t lo = (uint32_t)dpp_shr1((int)(uint32_t)v), hi = (uint32_t)dpp_shr1((int)(uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+  }
+}
+
+template <int R, typename P, int W>
+__global__ __launch_bounds__(64 * W) void nw_mw_kernel(NWPairs q) {
+  constexpr int SH = Pack<P>::SH;
+  constexpr P LEN1 = (P)1 << SH;
+  constexpr int ROWS = 64 * R * W;  // rows per block
+  __shared__ int rM[RING_C][W], rX[RING_C][W], rY[RING_C][W];
+  __shared__ P rMP[RING_C][W], rXP[RING_C][W], rYP[RING_C][W];
+  const uint32_t slot = blockIdx.x;
+  if (slot >= q.npairs) return;
+  const uint32_t p = q.pidx[slot];
+  const uint8_t *a = q.A + q.aoff[q.ai[p]];
+  const int la = (int)(q.aoff[q.ai[p] + 1] - q.aoff[q.ai[p]]);
+  const uint8_t *b = q.Bq + q.boff[q.bi[p]];
+  const int lb = (int)(q.boff[q.bi[p] + 1] - q.boff[q.bi[p]]);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, gl = threadIdx.x;
+  const int len1 = la + 1, len2 = lb + 1;
+  const int shorter = (len2 < len1 ? len2 : len1) - 1;
+  const int lenDiff = len2 > len1 ? len2 - len1 : len1 - len2;
+  int maxDiff = 0;
+  if (lenDiff >= 1) maxDiff += -GO - lenDiff * GE;
+  maxDiff += MISMATCH * shorter - 1;
+  const int NINF = maxDiff;
+  int *bnd = q.bnd ? q.bnd + q.bnd_off[slot] : nullptr;  // 6 ints per column, columns 0..lb
+  const int nblk = (la + ROWS - 1) / ROWS;
+  int fin_score = 0;
+  P fin_pay = 0;
+  for (int blk = 0; blk < (nblk > 0 ? nblk : 1); blk++) {
+    const int itop = blk * ROWS + gl * R + 1;  // first row of this lane
+    uint8_t ac[R];
+    int M[R], X[R], Y[R];
+    P MP[R], XP[R], YP[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      const int i = itop + r;
+      ac[r] = i <= la ? a[i - 1] : (uint8_t)0xFF;
+      M[r] = NINF;  // column 0 (GlobAlignE.cpp:140-160)
+      Y[r] = NINF;
+      X[r] = -GO - i * GE;
+      MP[r] = XP[r] = YP[r] = (P)i << SH;
+    }
+    int dM, dX, dY;
+    P dMP, dXP, dYP;
+    {
+      const int i = itop - 1;
+      if (i == 0) {
+        dM = 0;
+        dX = NINF;
+        dY = -GO;
+        dMP = dXP = dYP = 0;
+      } else {
+        dM = NINF;
+        dX = -GO - i * GE;
+        dY = NINF;
+        dMP = dXP = dYP = (P)i << SH;
+      }
+    }
+    int oM = NINF, oX = NINF, oY = NINF;
+    P oMP = 0, oXP = 0, oYP = 0;
+    int ob = 0;
+    const int lagw = w * (64 + KLAG);
+    const int steps = lb + 63 + (W - 1) * (64 + KLAG);
+    for (int t = 0; t < steps; t++) {
+      const int j = t - lane - lagw + 1;  // column of this lane at this step
+      int uM = dpp_shr1(oM), uX = dpp_shr1(oX), uY = dpp_shr1(oY);
+      P uMP = dshr<P>(oMP), uXP = dshr<P>(oXP), uYP = dshr<P>(oYP);
+      int bc = dpp_shr1(ob);
+      if (lane == 0) {
+        bc = (j >= 1 && j <= lb) ? b[j - 1] : 0;
+        if (j >= 1 && j <= lb) {
+          if (w > 0) {  // bottom row of wave w-1 at column j
+            const int sl = j % RING_C;
+            uM = rM[sl][w];
+            uX = rX[sl][w];
+            uY = rY[sl][w];
+            uMP = rMP[sl][w];
+            uXP = rXP[sl][w];
+            uYP = rYP[sl][w];
+          } else if (blk == 0) {  // row 0: M = X = -inf, Y = -o - j*e, lengths j
+            uM = NINF;
+            uX = NINF;
+            uY = -GO - j * GE;
+            uMP = uXP = uYP = (P)j << SH;
+          } else {
+            const int *sb = bnd + 6 * j;
+            uM = sb[0];
+            uX = sb[1];
+            uY = sb[2];
+            uMP = (P)(uint32_t)sb[3];
+            uXP = (P)(uint32_t)sb[4];
+            uYP = (P)(uint32_t)sb[5];
+            if constexpr (sizeof(P) == 8) {
+              const int *s2 = bnd + 6 * (lb + 1) + 6 * j;
+              uMP |= (P)(uint32_t)s2[3] << 32;
+              uXP |= (P)(uint32_t)s2[4] << 32;
+              uYP |= (P)(uint32_t)s2[5] << 32;
+            }
+          }
+        }
+      }
+      if (j >= 1 && j <= lb) {
+        int aM = uM, aX = uX;
+        P aMP = uMP, aXP = uXP;
+        int gM = dM, gX = dX, gY = dY;
+        P gMP = dMP, gXP = dXP, gYP = dYP;
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+          const int pM = M[r], pX = X[r], pY = Y[r];
+          const P pMP = MP[r], pXP = XP[r], pYP = YP[r];
+          const int yb = pM - (GO + GE), yc = pY - GE;  // upperGap (GlobAlignE.cpp:233-251)
+          const bool yFromM = yb >= yc;
+          Y[r] = yFromM ? yb : yc;
+          YP[r] = (yFromM ? pMP : pYP) + LEN1;
+          const bool hit = ac[r] == (uint8_t)bc;  // matches (:255-299)
+          const int sc = hit ? MATCH : MISMATCH;
+          const bool fromM = gM >= gX && gM >= gY;
+          const bool fromX = !fromM && gX >= gY;
+          const int best = fromM ? gM : (fromX ? gX : gY);
+          const P bestP = fromM ? gMP : (fromX ? gXP : gYP);
+          M[r] = best + sc;
+          MP[r] = bestP + LEN1 + (hit ? (P)1 : (P)0);
+          const int xb = aM - (GO + GE), xc = aX - GE;  // lowerGap (:316-330)
+          const bool xFromM = xb >= xc;
+          X[r] = xFromM ? xb : xc;
+          XP[r] = (xFromM ? aMP : aXP) + LEN1;
+          aM = M[r];
+          aX = X[r];
+          aMP = MP[r];
+          aXP = XP[r];
+          gM = pM;
+          gX = pX;
+          gY = pY;
+          gMP = pMP;
+          gXP = pXP;
+          gYP = pYP;
+        }
+        dM = uM;
+        dX = uX;
+        dY = uY;
+        dMP = uMP;
+        dXP = uXP;
+        dYP = uYP;
+        oM = M[R - 1];
+        oX = X[R - 1];
+        oY = Y[R - 1];
+        oMP = MP[R - 1];
+        oXP = XP[R - 1];
+        oYP = YP[R - 1];
+        ob = bc;
+        if (lane == 63) {
+          if (w + 1 < W) {
+            const int sl = j % RING_C;
+            rM[sl][w + 1] = oM;
+            rX[sl][w + 1] = oX;
+            rY[sl][w + 1] = oY;
+            rMP[sl][w + 1] = oMP;
+            rXP[sl][w + 1] = oXP;
+            rYP[sl][w + 1] = oYP;
+          } else if (blk + 1 < nblk) {
+            int *sb = bnd + 6 * j;
+            sb[0] = oM;
+            sb[1] = oX;
+            sb[2] = oY;
+            sb[3] = (int)(uint32_t)oMP;
+            sb[4] = (int)(uint32_t)oXP;
+            sb[5] = (int)(uint32_t)oYP;
+            if constexpr (sizeof(P) == 8) {
+              int *s2 = bnd + 6 * (lb + 1) + 6 * j;
+              s2[3] = (int)(uint32_t)(oMP >> 32);
+              s2[4] = (int)(uint32_t)(oXP >> 32);
+              s2[5] = (int)(uint32_t)(oYP >> 32);
+            }
+          }
+        }
+      } else {
+        ob = bc;
+      }
+      if (W > 1 && (t % KLAG) == KLAG - 1) __syncthreads();
+    }
+    const int fl = la - blk * ROWS - 1;
+    if (fl >= 0 && fl < ROWS && gl == fl / R) {
+      const int r = fl % R;
+      int mM = 0, mX = 0, mY = 0;
+      P pM = 0, pX = 0, pY = 0;
+#pragma unroll
+      for (int rr = 0; rr < R; rr++)
+        if (rr == r) {
+          mM = M[rr];
+          mX = X[rr];
+          mY = Y[rr];
+          pM = MP[rr];
+          pX = XP[rr];
+          pY = YP[rr];
+        }
+      int sc = mM > mX ? mM : mX;  // GlobAlignE.cpp:278-291
+      sc = sc > mY ? sc : mY;
+      fin_score = sc;
+      fin_pay = sc == mM ? pM : (sc == mX ? pX : pY);
+    }
+    __threadfence_block();
+    __syncthreads();
+  }
+  const int fl = la - (nblk - 1) * ROWS - 1;
+  const int owner = la == 0 ? 0 : fl / R;
+  if (gl == owner) {
+    int L, I;
+    if (la == 0) {  // see nw_kernel
+      L = lb;
+      I = 0;
+      fin_score = lb > 0 ? NINF : 0;
+    } else {
+      L = (int)(fin_pay >> SH);
+      I = (int)(fin_pay & (((P)1 << SH) - 1));
+    }
+    const uint32_t o = q.out ? q.out[p] : p;
+    q.ident[o] = (double)I / (double)L;
+    if (q.len) q.len[o] = L;
+    if (q.ids) q.ids[o] = I;
+    if (q.score) q.score[o] = fin_score;
+  }
+}
+
+template <int R, typename P>
+int launch_bucket_mw(mc_ctx *c, NWPairs q) {
+  if (q.npairs == 0) return MC_OK;
+  nw_mw_kernel<R, P, 4><<<q.npairs, 256, 0, c->stream>>>(q);
+  MCG_CHECK(hipGetLastError());
+  return MC_OK;
+}
+
 }  // namespace
 
 int launch_nw(mc_ctx *c, const uint8_t *d_A, const uint64_t *d_aoff, const uint32_t *d_ai, const uint8_t *d_B,
@@ -289,7 +540,10 @@ int launch_nw(mc_ctx *c, const uint8_t *d_A, const uint64_t *d_aoff, const uint3
               const std::vector<uint64_t> &blen, double *d_ident, int32_t *d_len, int32_t *d_ids,
               int32_t *d_score, const uint32_t *d_out) {
   if (m == 0) return MC_OK;
-  // bucket pairs by rows per lane and payload width; boundary scratch for multi-block pairs
+  // bucket pairs by rows per lane and payload width; boundary scratch for multi-block pairs.
+  // Few pairs (fewer than the chip's SIMDs) are latency-bound: one 4-wave workgroup per pair;
+  // many pairs: one wavefront per pair.
+  const bool mw = m < 1024;
   enum { NB = 8 };
   std::vector<uint32_t> bucket[NB];
   std::vector<uint64_t> boff[NB];
@@ -297,11 +551,19 @@ int launch_nw(mc_ctx *c, const uint8_t *d_A, const uint64_t *d_aoff, const uint3
   for (uint64_t i = 0; i < m; i++) {
     const uint64_t la = alen[i], lb = blen[i];
     const bool wide = la + lb >= 65535;
-    int r = la <= 256 ? 0 : la <= 512 ? 1 : 2;  // R = 4, 8, 16
-    int bk = r + (wide ? 3 : 0);
+    int r, bk;
+    uint64_t rows;
+    if (mw) {
+      r = la <= 256 ? 0 : la <= 512 ? 1 : la <= 1024 ? 2 : 3;  // R = 1, 2, 4, 8 over 4 waves
+      bk = r + (wide ? 4 : 0);
+      rows = 256ull << r;
+    } else {
+      r = la <= 256 ? 0 : la <= 512 ? 1 : 2;  // R = 4, 8, 16
+      bk = r + (wide ? 3 : 0);
+      rows = 64ull * (r == 0 ? 4 : r == 1 ? 8 : 16);
+    }
     bucket[bk].push_back((uint32_t)i);
     boff[bk].push_back(scratch[bk]);
-    const uint64_t rows = 64ull * (r == 0 ? 4 : r == 1 ? 8 : 16);
     if (la > rows) scratch[bk] += 12 * (lb + 1);
   }
   timed_begin(c);
@@ -324,7 +586,18 @@ int launch_nw(mc_ctx *c, const uint8_t *d_A, const uint64_t *d_aoff, const uint3
     NWPairs q{d_A, d_aoff, d_ai, d_B, d_boff, d_bi, (uint32_t *)c->s_a.p + io, (uint32_t)bucket[k].size(),
               (int *)c->s_c.p, (uint64_t *)c->s_b.p + io, d_ident, d_len, d_ids, d_score, d_out};
     int rc = MC_OK;
-    switch (k) {
+    if (mw) {
+      switch (k) {
+        case 0: rc = launch_bucket_mw<1, uint32_t>(c, q); break;
+        case 1: rc = launch_bucket_mw<2, uint32_t>(c, q); break;
+        case 2: rc = launch_bucket_mw<4, uint32_t>(c, q); break;
+        case 3: rc = launch_bucket_mw<8, uint32_t>(c, q); break;
+        case 4: rc = launch_bucket_mw<1, uint64_t>(c, q); break;
+        case 5: rc = launch_bucket_mw<2, uint64_t>(c, q); break;
+        case 6: rc = launch_bucket_mw<4, uint64_t>(c, q); break;
+        default: rc = launch_bucket_mw<8, uint64_t>(c, q); break;
+      }
+    } else switch (k) {
       case 0: rc = launch_bucket<4, uint32_t>(c, q); break;
       case 1: rc = launch_bucket<8, uint32_t>(c, q); break;
       case 2: rc = launch_bucket<16, uint32_t>(c, q); break;

@@ -76,6 +76,25 @@ def test_nw_golden(eng):
     assert np.array_equal(ident, g["identity"])
 
 
+def test_nw_golden_batch_paths(eng):
+    """The golden pairs through both launch forms: a small batch (one 4-wave workgroup per
+    pair, DPP lane shifts, LDS ring between waves) and a batch of >= 1024 pairs (one wavefront
+    per pair)."""
+    g = np.load(fixtures.golden("nw.npz"))
+    n = len(g["a_off"]) - 1
+    for reps in (1, (1024 + n - 1) // n + 1):
+        la = np.diff(g["a_off"])
+        lb = np.diff(g["b_off"])
+        a = np.tile(g["a"], reps)
+        b = np.tile(g["b"], reps)
+        a_off = np.concatenate([[0], np.cumsum(np.tile(la, reps))])
+        b_off = np.concatenate([[0], np.cumsum(np.tile(lb, reps))])
+        ident, ln, ids, sc = eng.nw_identity_raw(a, a_off, b, b_off)
+        assert np.array_equal(ln, np.tile(g["length"], reps)), reps
+        assert np.array_equal(ids, np.tile(g["ids"], reps)), reps
+        assert np.array_equal(sc, np.tile(g["score"], reps)), reps
+
+
 def test_nw_long_multiblock_vs_oracle(eng):
     """Pairs longer than one 1024-row block (boundary row in scratch) and >64k total length."""
     rng = np.random.default_rng(9)
@@ -94,6 +113,14 @@ def test_nw_long_multiblock_vs_oracle(eng):
     for i, (a, b) in enumerate(pairs):
         w = O.nw(a.tobytes(), b.tobytes())
         assert (ident[i], ln[i], ids[i], sc[i]) == w, i
+    # the same pairs in a batch of >= 1024 (one wavefront per pair, 1024-row blocks)
+    reps = 1024 // len(pairs) + 1
+    la = np.diff(a_off)
+    lb = np.diff(b_off)
+    big = eng.nw_identity_raw(np.tile(a_cat, reps), np.concatenate([[0], np.cumsum(np.tile(la, reps))]),
+                              np.tile(b_cat, reps), np.concatenate([[0], np.cumsum(np.tile(lb, reps))]))
+    for got, want in zip(big, (ident, ln, ids, sc)):
+        assert np.array_equal(got, np.tile(want, reps))
 
 
 @pytest.fixture(scope="module")
