@@ -122,14 +122,23 @@ __global__ __launch_bounds__(64) void nw_kernel(NWPairs q) {
     P oMP = 0, oXP = 0, oYP = 0;
     uint8_t ob = 0;
     const int steps = lb + 63;
+    // seq2 codes for lane 0 (column t + 1 at step t): one 64-byte block per 64 steps, lane l
+    // holding byte l, loaded a block ahead and read with a uniform readlane
+    int bcur = 0, bnext = lane < lb ? b[lane] : 0;
     for (int t = 0; t < steps; t++) {
       const int j = t - lane + 1;  // column of this lane at this step
+      if ((t & 63) == 0) {
+        bcur = bnext;
+        const int nx = t + 64 + lane;
+        bnext = nx < lb ? b[nx] : 0;
+      }
       // hand-off from lane-1: its bottom row at column j (computed at step t-1) + seq2 code
       int uM = shup<int>(oM), uX = shup<int>(oX), uY = shup<int>(oY);
       P uMP = shup<P>(oMP), uXP = shup<P>(oXP), uYP = shup<P>(oYP);
       uint8_t bc = (uint8_t)__shfl_up((int)ob, 1, 64);
+      const int b0 = __builtin_amdgcn_readlane(bcur, t & 63);
       if (lane == 0) {
-        bc = (j >= 1 && j <= lb) ? b[j - 1] : 0;
+        bc = (j >= 1 && j <= lb) ? (uint8_t)b0 : 0;
         if (blk == 0) {  // row 0 at column j: M = X = -inf, Y = -o - j*e, lengths j
           uM = NINF;
           uX = NINF;
@@ -365,13 +374,21 @@ __global__ __launch_bounds__(64 * W) void nw_mw_kernel(NWPairs q) {
     int ob = 0;
     const int lagw = w * (64 + KLAG);
     const int steps = lb + 63 + (W - 1) * (64 + KLAG);
+    int bcur = 0, bnext = lane < lb ? b[lane] : 0;  // seq2 blocks for lane 0, as in nw_kernel
     for (int t = 0; t < steps; t++) {
       const int j = t - lane - lagw + 1;  // column of this lane at this step
+      const int idx = t - lagw;           // lane 0 reads seq2[idx]
+      if (idx >= 0 && (idx & 63) == 0) {
+        bcur = bnext;
+        const int nx = idx + 64 + lane;
+        bnext = nx < lb ? b[nx] : 0;
+      }
+      const int b0 = __builtin_amdgcn_readlane(bcur, idx & 63);
       int uM = dpp_shr1(oM), uX = dpp_shr1(oX), uY = dpp_shr1(oY);
       P uMP = dshr<P>(oMP), uXP = dshr<P>(oXP), uYP = dshr<P>(oYP);
       int bc = dpp_shr1(ob);
       if (lane == 0) {
-        bc = (j >= 1 && j <= lb) ? b[j - 1] : 0;
+        bc = (j >= 1 && j <= lb) ? b0 : 0;
         if (j >= 1 && j <= lb) {
           if (w > 0) {  // bottom row of wave w-1 at column j
             const int sl = j % RING_C;
