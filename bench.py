@@ -160,13 +160,20 @@ def main():
         per_launch_bytes = scan_evals * eval_bytes / fam_n["scan"]
         avg_s = fam_ms["scan"] / fam_n["scan"] / 1e3
         ach = per_launch_bytes / avg_s / 1e9
-        roof = {"kernel": "scan_kernel (Trainer::get_close)", "bound": "hbm", "achieved": round(ach, 1),
+        # one launch per clustering = the device-resident accumulation (accum.hip); otherwise
+        # one fused scan launch per get_close step (scan.hip)
+        device_loop = fam_n["scan"] <= a.steps
+        kname = "accum_kernel<unsigned char>" if device_loop else "fused_scan_kernel<unsigned char>"
+        roof = {"kernel": ("accum_kernel (whole accumulation phase, %d dependent get_close steps per launch)"
+                           % s0["scan_steps"]) if device_loop else "fused_scan_kernel (Trainer::get_close step)",
+                "bound": "hbm", "achieved": round(ach, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
                 "bytes_per_eval": eval_bytes, "evals_per_launch": round(scan_evals / fam_n["scan"], 1),
-                "avg_launch_us": round(avg_s * 1e6, 2)}
+                "avg_launch_us": round(avg_s * 1e6, 2),
+                "us_per_step": round(fam_ms["scan"] * 1e3 / sum(s["scan_steps"] for s in stats), 2)}
         pmc = os.path.join(ROOT, "profiles", "pmc_latest.json")
         if os.path.exists(pmc):  # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (scripts/pmc_summary.py)
-            e = json.load(open(pmc)).get("fused_scan_kernel<unsigned char>")
+            e = json.load(open(pmc)).get(kname)
             if e and "hbm_bytes_per_dispatch" in e:
                 roof["traffic"] = round(e["hbm_bytes_per_dispatch"])
                 roof["traffic_unit"] = "bytes/launch (FETCH_SIZE x2 + WRITE_SIZE, profiles/pmc_latest.json)"
