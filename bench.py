@@ -10,7 +10,10 @@ HBM (FASTA parse and the one-time upload are outside the timed region; their cos
 reported separately in "extra").
 
 With --gpus N (torch.distributed, one rank per GPU) every rank clusters its own batch
-(seed 41 + rank): replicas, weak scaling; no collective is on the data path.
+(seed 41 + rank): replicas, weak scaling; no collective is on the data path.  With --shard the
+ranks instead share ONE clustering of the seed-41 batch (meshclust_amd.dist): each runs the
+accumulation chain, computes its share of every mean-shift iteration and the ranks all-gather
+the new centres over RCCL (strong scaling).
 
 Prints ONE JSON line on rank 0.
 """
@@ -87,6 +90,7 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=10000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--stats-out", default=None)
+    ap.add_argument("--shard", action="store_true", help="ranks share one clustering (strong scaling)")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -102,21 +106,31 @@ def main():
         M.build()
     if dist:
         dist.barrier()
-    fasta = ensure_fasta(a.n, a.len, a.templates, a.mut, a.seed + rank)
+    shard = dist is not None and a.shard
+    fasta = ensure_fasta(a.n, a.len, a.templates, a.mut, a.seed + (0 if shard else rank))
     t0 = time.perf_counter()
     ds = M.Dataset([fasta], threads=16)
     parse_s = time.perf_counter() - t0
     eng = M.Engine(local)
     args = ["--id", a.id, "--threads", "16"]
+    comm = None
+    if shard:
+        import torch
+        from meshclust_amd.dist import TorchShardComm
+        if torch.cuda.is_available():
+            torch.cuda.set_device(local)
+            comm = TorchShardComm(dist.new_group(backend="nccl"))  # RCCL for the centre exchange
+        else:
+            comm = TorchShardComm()
 
     import torch
     sync = torch.cuda.synchronize if torch.cuda.is_available() else (lambda: None)
 
     t0 = time.perf_counter()
-    st = ds.run(eng, args, upload=True)  # one-time upload (+ first warm-up pass)
+    st = ds.run(eng, args, upload=True, comm=comm)  # one-time upload (+ first warm-up pass)
     first_s = time.perf_counter() - t0
     for _ in range(max(0, a.warmup - 1)):
-        ds.run(eng, args, upload=False)
+        ds.run(eng, args, upload=False, comm=comm)
     eng.timers(reset=True)
 
     if dist:
@@ -125,7 +139,7 @@ def main():
     t0 = time.perf_counter()
     stats = []
     for _ in range(a.steps):
-        stats.append(ds.run(eng, args, upload=False))
+        stats.append(ds.run(eng, args, upload=False, comm=comm))
     sync()
     if dist:
         dist.barrier()
@@ -143,7 +157,7 @@ def main():
             dist.destroy_process_group()
         return
     s0 = stats[-1]
-    n_total = a.n * a.steps * world
+    n_total = a.n * a.steps * (1 if shard else world)
     value = n_total / elapsed
     ms_step = elapsed / a.steps * 1000.0
 
@@ -192,14 +206,15 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": round(ms_step, 2),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if shard else "weak",
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (meshclust_amd.synth: %d reads x %d bp, %d templates, mut %.2f, seed %d+rank)"
                 % (a.n, a.len, a.templates, a.mut, a.seed),
         "config": {"workload": "config B: 100k synthetic 1kb reads, --id %s k-mer mean-shift" % a.id,
                    "reads_per_gpu": a.n, "read_len": a.len, "k": s0["k"], "histogram_bits": 8 * width,
-                   "parallelism": "replicas x%d" % world},
+                   "parallelism": ("one clustering sharded x%d (centre all-gather over RCCL)" % world) if shard
+                   else "replicas x%d" % world},
         "roofline": roof,
         "cpu_baseline": cpu,
         "extra": {"nw_cell_updates_per_s": nw_rate, "clusters": s0["clusters"], "dominant_family": dominant,

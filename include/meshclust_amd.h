@@ -206,6 +206,14 @@ int mc_mean_shift(mc_ctx *ctx, const uint32_t *centre_ids, uint32_t C, const uin
                   const uint32_t *members, int delta, uint32_t *new_centre);
 
 /*
+ * The same for centres j0 <= j < j1 only (new_centre holds j1 - j0 entries): the per-rank
+ * share of one iteration when the update is sharded over GPUs by centre; the ranks then
+ * all-gather the new centres (the centre-reassignment exchange).
+ */
+int mc_mean_shift_range(mc_ctx *ctx, const uint32_t *centre_ids, uint32_t C, const uint64_t *member_off,
+                        const uint32_t *members, int delta, uint32_t j0, uint32_t j1, uint32_t *new_centre);
+
+/*
  * ---- alignment mode (--align, or --id < 0.6: Runner.cpp:32-34, 332) ---------------------
  * The trainer then installs a classifier whose only feature is MC_FEAT_ALIGN (identity of
  * utility::GlobAlignE, normalised with min 0 / max 1, weights {-cutoff, 1}; Trainer.cpp:

@@ -109,6 +109,9 @@ def host_lib():
         lib.mcl_run.restype = C.c_int
         lib.mcl_run.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_char_p), C.c_int, C.c_char_p,
                                 C.c_char_p, C.c_int]
+        lib.mcl_run_sharded.restype = C.c_int
+        lib.mcl_run_sharded.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_char_p), C.c_int, C.c_char_p,
+                                        C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
         _host = lib
     return _host
 
@@ -260,14 +263,20 @@ class Dataset:
             raise MCError("parse failed: " + err.value.decode())
         self.n = self.lib.mcl_num_seqs(self.h)
 
-    def run(self, engine, args=(), upload=True, clstr=None):
-        """Run the full pipeline (reference options in ``args``); returns the stats dict."""
+    def run(self, engine, args=(), upload=True, clstr=None, comm=None):
+        """Run the full pipeline (reference options in ``args``); returns the stats dict.
+        ``comm`` (meshclust_amd.dist.TorchShardComm) shares the clustering over its ranks."""
         import json
         argv = [b"meshclust"] + [a.encode() for a in args]
         arr = (C.c_char_p * len(argv))(*argv)
         buf = C.create_string_buffer(1 << 16)
-        rc = self.lib.mcl_run(self.h, engine.ctx, len(argv), arr, 1 if upload else 0,
-                              clstr.encode() if clstr else None, buf, len(buf))
+        if comm is not None and comm.world > 1:
+            rc = self.lib.mcl_run_sharded(self.h, engine.ctx, len(argv), arr, 1 if upload else 0,
+                                          clstr.encode() if clstr else None, buf, len(buf), comm.rank, comm.world,
+                                          C.cast(comm.callback, C.c_void_p), None)
+        else:
+            rc = self.lib.mcl_run(self.h, engine.ctx, len(argv), arr, 1 if upload else 0,
+                                  clstr.encode() if clstr else None, buf, len(buf))
         st = json.loads(buf.value.decode() or "{}")
         if rc != 0:
             raise MCError("mcl_run failed (%d): %s" % (rc, st))

@@ -707,9 +707,11 @@ int mc_classify_values(mc_ctx *c, const double *raw, uint64_t m, uint8_t *simila
 }
 
 static int mean_shift_common(mc_ctx *c, const uint32_t *centre_ids, uint32_t C, const uint64_t *member_off,
-                             const uint32_t *members, int delta, const uint8_t *keep, uint32_t *new_centre) {
+                             const uint32_t *members, int delta, const uint8_t *keep, uint32_t *new_centre,
+                             uint32_t j0, uint32_t j1) {
   if (!c || !c->has_cls || c->k == 0 || delta < 0) return MC_ERR_STATE;
-  if (C == 0) return MC_OK;
+  if (j0 > j1 || j1 > C) return MC_ERR_ARG;
+  if (C == 0 || j0 == j1) return MC_OK;
   MCG_CHECK(hipSetDevice(c->device));
   TRY(check_ids(c, centre_ids, C));
   const uint64_t nm = member_off[C];
@@ -730,8 +732,8 @@ static int mean_shift_common(mc_ctx *c, const uint32_t *centre_ids, uint32_t C, 
   }
   TRY(ensure(c->flags_out, (size_t)C * 4 + 16));
   TRY(launch_mean_shift(c, (uint32_t *)c->s_a.p, C, (uint64_t *)c->s_b.p, member_off, (uint32_t *)c->s_c.p, delta,
-                        d_keep, (uint32_t *)c->flags_out.p));
-  TRY(download(new_centre, c->flags_out.p, C, c->stream));
+                        d_keep, (uint32_t *)c->flags_out.p, j0, j1));
+  TRY(download(new_centre, (uint32_t *)c->flags_out.p + j0, j1 - j0, c->stream));
   MCG_CHECK(hipStreamSynchronize(c->stream));
   flush_timers(c);
   return MC_OK;
@@ -741,13 +743,19 @@ int mc_mean_shift(mc_ctx *c, const uint32_t *centre_ids, uint32_t C, const uint6
                   int delta, uint32_t *new_centre) {
   if (!c) return MC_ERR_ARG;
   TRY(no_align(c, "mc_mean_shift"));
-  return mean_shift_common(c, centre_ids, C, member_off, members, delta, nullptr, new_centre);
+  return mean_shift_common(c, centre_ids, C, member_off, members, delta, nullptr, new_centre, 0, C);
+}
+
+int mc_mean_shift_range(mc_ctx *c, const uint32_t *centre_ids, uint32_t C, const uint64_t *member_off,
+                        const uint32_t *members, int delta, uint32_t j0, uint32_t j1, uint32_t *new_centre) {
+  TRY(no_align(c, "mc_mean_shift_range"));
+  return mean_shift_common(c, centre_ids, C, member_off, members, delta, nullptr, new_centre, j0, j1);
 }
 
 int mc_mean_shift_select(mc_ctx *c, const uint32_t *centre_ids, uint32_t C, const uint64_t *member_off,
                          const uint32_t *members, int delta, const uint8_t *keep, uint32_t *new_centre) {
   if (!c || !keep) return MC_ERR_ARG;
-  return mean_shift_common(c, centre_ids, C, member_off, members, delta, keep, new_centre);
+  return mean_shift_common(c, centre_ids, C, member_off, members, delta, keep, new_centre, 0, C);
 }
 
 int mc_timers(mc_ctx *c, double *ms_out, int n, int reset) {

@@ -374,10 +374,11 @@ __global__ __launch_bounds__(NT) void mean_shift_kernel(HistView H, DevClassifie
                                                         const uint32_t *__restrict__ mem, int delta,
                                                         const uint64_t *__restrict__ soff, uint32_t *__restrict__ kept,
                                                         uint32_t *__restrict__ nkept, double *__restrict__ gmean,
-                                                        const uint8_t *__restrict__ keep, uint32_t *__restrict__ newc) {
+                                                        const uint8_t *__restrict__ keep, uint32_t *__restrict__ newc,
+                                                        uint32_t jbase) {
   extern __shared__ __attribute__((aligned(16))) uint4 dyn[];
   __shared__ uint32_t cnt;
-  const uint32_t j = blockIdx.x;
+  const uint32_t j = jbase + blockIdx.x;
   const int nch = (int)((H.B * (int)sizeof(T) + 15) / 16);
   uint4 *clds = dyn;
   double *mean = reinterpret_cast<double *>(dyn + nch);
@@ -543,8 +544,9 @@ int launch_finalize(mc_ctx *c, int nblocks) {
 }
 
 int launch_mean_shift(mc_ctx *c, const uint32_t *d_cid, uint32_t C, const uint64_t *d_off, const uint64_t *h_off,
-                      const uint32_t *d_mem, int delta, const uint8_t *d_keep, uint32_t *d_new) {
-  if (C == 0) return MC_OK;
+                      const uint32_t *d_mem, int delta, const uint8_t *d_keep, uint32_t *d_new, uint32_t j0,
+                      uint32_t j1) {
+  if (C == 0 || j0 >= j1) return MC_OK;
   const HistView H = hist_view(c);
   const int nch = (int)((H.B * H.width + 15) / 16);
   // scratch: per-centre survivor lists (offsets = sizes of the neighbourhoods)
@@ -561,9 +563,9 @@ int launch_mean_shift(mc_ctx *c, const uint32_t *d_cid, uint32_t C, const uint64
   MCG_CHECK(hipMemcpyAsync(c->s_d.p, soff.data(), (C + 1) * 8, hipMemcpyHostToDevice, c->stream));
   const size_t lds = (size_t)nch * 16 + (gm ? 0 : (size_t)H.B * 8);
   timed_begin(c);
-  MCG_DISPATCH_T(c->width, (mean_shift_kernel<T><<<C, NT, lds, c->stream>>>(
+  MCG_DISPATCH_T(c->width, (mean_shift_kernel<T><<<j1 - j0, NT, lds, c->stream>>>(
                                H, c->cls, d_cid, C, d_off, d_mem, delta, (const uint64_t *)c->s_d.p,
-                               (uint32_t *)c->s_e.p, (uint32_t *)c->s_f.p, (double *)c->s_g.p, d_keep, d_new)));
+                               (uint32_t *)c->s_e.p, (uint32_t *)c->s_f.p, (double *)c->s_g.p, d_keep, d_new, j0)));
   MCG_CHECK(hipGetLastError());
   timed_end(c, F_MSHIFT);
   return MC_OK;

@@ -138,7 +138,8 @@ int launch_scan(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, const double
 int launch_values(mc_ctx *c, const double *d_raw, uint64_t m, uint8_t *d_sim, double *d_c0, double *d_sum);
 int launch_finalize(mc_ctx *c, int nblocks);
 int launch_mean_shift(mc_ctx *c, const uint32_t *d_cid, uint32_t C, const uint64_t *d_off, const uint64_t *h_off,
-                      const uint32_t *d_mem, int delta, const uint8_t *d_keep, uint32_t *d_new);
+                      const uint32_t *d_mem, int delta, const uint8_t *d_keep, uint32_t *d_new, uint32_t j0,
+                      uint32_t j1);
 int build_static(mc_ctx *c);
 bool accum_supported(const mc_ctx *c, uint32_t nb);
 int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, uint32_t nb, double sim,

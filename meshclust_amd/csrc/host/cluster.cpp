@@ -257,7 +257,17 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
       uint32_t e = std::min<uint32_t>(j + cfg.delta, C - 1);
       stats.update_evals += off[e + 1] - off[b];
     }
-    if (C && !memo) {
+    if (C && !memo && cfg.comm && cfg.comm->world > 1) {
+      // this rank's share of the centres, then the centre-reassignment all-gather
+      const uint32_t W = (uint32_t)cfg.comm->world, per = (C + W - 1) / W;
+      const uint32_t j0 = std::min<uint32_t>(C, per * (uint32_t)cfg.comm->rank), j1 = std::min<uint32_t>(C, j0 + per);
+      std::vector<uint32_t> mine(per, 0), all((size_t)per * W, 0);
+      check(mc_mean_shift_range(ctx, cids.data(), C, off.data(), members.data(), cfg.delta, j0, j1, mine.data()),
+            "mc_mean_shift_range");
+      if (cfg.comm->allgather(cfg.comm->user, mine.data(), (uint64_t)per * 4, all.data()) != 0)
+        throw Error("centre all-gather across ranks failed", 1);
+      std::copy(all.begin(), all.begin() + C, newc.begin());
+    } else if (C && !memo) {
       check(mc_mean_shift(ctx, cids.data(), C, off.data(), members.data(), cfg.delta, newc.data()), "mc_mean_shift");
     } else if (C) {
       // Trainer::filter(center clone, good): feat->compute(*member, *clone) (Trainer.cpp:334-349)

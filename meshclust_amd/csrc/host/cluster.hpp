@@ -19,7 +19,18 @@ struct Center {
   bool del = false;
 };
 
+// The ranks (one process per GPU) that share one clustering.  Every rank
+// runs the same sequential accumulation; each mean-shift iteration is split by centre and the
+// ranks exchange the new centres with `allgather` (equal blocks of `bytes`, rank order into
+// `out`; returns 0 on success).
+struct ShardComm {
+  int rank = 0, world = 1;
+  int (*allgather)(void *user, const void *in, uint64_t bytes, void *out) = nullptr;
+  void *user = nullptr;
+};
+
 struct ClusterConfig {
+  const ShardComm *comm = nullptr;  // null: one rank
   double sim = 0.90;
   int iterations = 15;
   int delta = 5;

@@ -119,7 +119,7 @@ static int find_k(const Dataset &ds, bool verbose) {
   return newk;
 }
 
-RunResult run_pipeline(const Dataset &ds, mc_ctx *ctx, Options opt, bool upload) {
+RunResult run_pipeline(const Dataset &ds, mc_ctx *ctx, Options opt, bool upload, const ShardComm *comm) {
   RunResult rr;
   rr.n = ds.size();
   const bool verbose = !opt.quiet;
@@ -174,6 +174,7 @@ RunResult run_pipeline(const Dataset &ds, mc_ctx *ctx, Options opt, bool upload)
   cc.delta = opt.delta;
   cc.verbose = verbose;
   cc.align = opt.align;
+  cc.comm = comm;
   rr.part = mean_shift_cluster(ds, ctx, bv, cc, rr.timer, rr.stats);
   rr.stats.nw_pairs = tr.nw_pairs;
   rr.stats.nw_cells = tr.nw_cells;

@@ -43,7 +43,8 @@ struct RunResult {
 };
 
 // Full pipeline on an already parsed dataset and an open context (bench.py reuses both).
-RunResult run_pipeline(const Dataset &ds, mc_ctx *ctx, Options opt, bool upload = true);
+RunResult run_pipeline(const Dataset &ds, mc_ctx *ctx, Options opt, bool upload = true,
+                       const ShardComm *comm = nullptr);
 
 // JSON summary of a run (phase timings, work counts) for --stats-json and the C API.
 std::string stats_json(const RunResult &rr, double parse_ms, double write_ms);

@@ -324,11 +324,12 @@ int mc_mean_shift_select(mc_ctx *c, const uint32_t *cid, uint32_t C, const uint6
   return MC_OK;
 }
 
-int mc_mean_shift(mc_ctx *c, const uint32_t *cid, uint32_t C, const uint64_t *off, const uint32_t *members, int delta,
-                  uint32_t *newc) {
+int mc_mean_shift_range(mc_ctx *c, const uint32_t *cid, uint32_t C, const uint64_t *off, const uint32_t *members,
+                        int delta, uint32_t j0, uint32_t j1, uint32_t *newc) {
   if (c->align) return fail(MC_ERR_STATE, "mc_mean_shift is not available in alignment mode");
+  if (j0 > j1 || j1 > C) return fail(MC_ERR_ARG, "bad centre range");
 #pragma omp parallel for schedule(dynamic)
-  for (uint32_t j = 0; j < C; j++) {
+  for (uint32_t j = j0; j < j1; j++) {
     long b = (long)j - delta < 0 ? 0 : (long)j - delta;
     long e = (long)j + delta < (long)C - 1 ? (long)j + delta : (long)C - 1;
     std::vector<uint32_t> good;
@@ -336,9 +337,14 @@ int mc_mean_shift(mc_ctx *c, const uint32_t *cid, uint32_t C, const uint64_t *of
       double s, c0;
       if (classify(c, members[q], cid[j], &s, &c0)) good.push_back(members[q]);
     }
-    newc[j] = good.empty() ? cid[j] : mean_closest(c, good);
+    newc[j - j0] = good.empty() ? cid[j] : mean_closest(c, good);
   }
   return MC_OK;
+}
+
+int mc_mean_shift(mc_ctx *c, const uint32_t *cid, uint32_t C, const uint64_t *off, const uint32_t *members, int delta,
+                  uint32_t *newc) {
+  return mc_mean_shift_range(c, cid, C, off, members, delta, 0, C, newc);
 }
 
 int mc_accumulate(mc_ctx *, const uint32_t *, const uint64_t *, uint32_t, double, uint32_t *, uint64_t *, uint32_t *,
