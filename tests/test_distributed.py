@@ -30,8 +30,8 @@ def _run_world2(name, tmp_path, gpu):
     fa, flags = fixtures.e2e_input(name, tmp_path)
     out = str(tmp_path / (name + ".clstr"))
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), WORKER, fa, out]
-    cmd += (["--gpu"] if gpu else []) + ["--"] + flags
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), WORKER]
+    cmd += (["--gpu"] if gpu else []) + [fa, out, "--"] + flags
     env = dict(os.environ, OMP_NUM_THREADS="2")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
