@@ -48,7 +48,7 @@ def test_libmcgpu_loads_and_has_gfx950_code(product):
 
 def test_host_library_and_cli(product):
     out = subprocess.run(["nm", "-D", "--defined-only", M.HOST_LIB], capture_output=True, text=True, check=True).stdout
-    for n in ("mcl_parse", "mcl_run", "mcl_num_seqs", "mcl_free"):
+    for n in ("mcl_parse", "mcl_run", "mcl_run_sharded", "mcl_num_seqs", "mcl_free"):
         assert " T " + n in out
     assert os.access(M.BIN, os.X_OK)
     # the CLI links libmcgpu (the GPU engine), never the oracle
