@@ -375,6 +375,38 @@ __global__ __launch_bounds__(64 * W) void nw_mw_kernel(NWPairs q) {
     const int lagw = w * (64 + KLAG);
     const int steps = lb + 63 + (W - 1) * (64 + KLAG);
     int bcur = 0, bnext = lane < lb ? b[lane] : 0;  // seq2 blocks for lane 0, as in nw_kernel
+    // lane 0's hand-in for its next column, loaded one step ahead so the LDS / global latency
+    // hides behind a step of cell updates (the slot was written >= KLAG steps earlier, with a
+    // barrier in between, see above)
+    int nM = NINF, nX = NINF, nY = NINF;
+    P nMP = 0, nXP = 0, nYP = 0;
+    auto fetch = [&](int jn) {
+      if (lane != 0 || jn < 1 || jn > lb) return;
+      if (w > 0) {
+        const int sl = jn % RING_C;
+        nM = rM[sl][w];
+        nX = rX[sl][w];
+        nY = rY[sl][w];
+        nMP = rMP[sl][w];
+        nXP = rXP[sl][w];
+        nYP = rYP[sl][w];
+      } else if (blk > 0) {
+        const int *sb = bnd + 6 * jn;
+        nM = sb[0];
+        nX = sb[1];
+        nY = sb[2];
+        nMP = (P)(uint32_t)sb[3];
+        nXP = (P)(uint32_t)sb[4];
+        nYP = (P)(uint32_t)sb[5];
+        if constexpr (sizeof(P) == 8) {
+          const int *s2 = bnd + 6 * (lb + 1) + 6 * jn;
+          nMP |= (P)(uint32_t)s2[3] << 32;
+          nXP |= (P)(uint32_t)s2[4] << 32;
+          nYP |= (P)(uint32_t)s2[5] << 32;
+        }
+      }
+    };
+    fetch(1 - lagw);
     for (int t = 0; t < steps; t++) {
       const int j = t - lane - lagw + 1;  // column of this lane at this step
       const int idx = t - lagw;           // lane 0 reads seq2[idx]
@@ -390,36 +422,22 @@ __global__ __launch_bounds__(64 * W) void nw_mw_kernel(NWPairs q) {
       if (lane == 0) {
         bc = (j >= 1 && j <= lb) ? b0 : 0;
         if (j >= 1 && j <= lb) {
-          if (w > 0) {  // bottom row of wave w-1 at column j
-            const int sl = j % RING_C;
-            uM = rM[sl][w];
-            uX = rX[sl][w];
-            uY = rY[sl][w];
-            uMP = rMP[sl][w];
-            uXP = rXP[sl][w];
-            uYP = rYP[sl][w];
-          } else if (blk == 0) {  // row 0: M = X = -inf, Y = -o - j*e, lengths j
+          if (w == 0 && blk == 0) {  // row 0: M = X = -inf, Y = -o - j*e, lengths j
             uM = NINF;
             uX = NINF;
             uY = -GO - j * GE;
             uMP = uXP = uYP = (P)j << SH;
-          } else {
-            const int *sb = bnd + 6 * j;
-            uM = sb[0];
-            uX = sb[1];
-            uY = sb[2];
-            uMP = (P)(uint32_t)sb[3];
-            uXP = (P)(uint32_t)sb[4];
-            uYP = (P)(uint32_t)sb[5];
-            if constexpr (sizeof(P) == 8) {
-              const int *s2 = bnd + 6 * (lb + 1) + 6 * j;
-              uMP |= (P)(uint32_t)s2[3] << 32;
-              uXP |= (P)(uint32_t)s2[4] << 32;
-              uYP |= (P)(uint32_t)s2[5] << 32;
-            }
+          } else {  // bottom row of wave w-1 (or of the previous row block) at column j
+            uM = nM;
+            uX = nX;
+            uY = nY;
+            uMP = nMP;
+            uXP = nXP;
+            uYP = nYP;
           }
         }
       }
+      fetch(j + 1);
       if (j >= 1 && j <= lb) {
         int aM = uM, aX = uX;
         P aMP = uMP, aXP = uXP;
