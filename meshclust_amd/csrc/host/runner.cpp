@@ -1,7 +1,9 @@
 // runner.cpp -- see runner.hpp.
+#include <malloc.h>
 #include "runner.hpp"
 
 #include <libgen.h>
+#include <malloc.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -119,7 +121,20 @@ static int find_k(const Dataset &ds, bool verbose) {
   return newk;
 }
 
+// The training sampler allocates ~150 MB of short-lived host arrays per clustering (split keys,
+// the per-pivot sort inputs).  Keep freed blocks in the heap instead of returning them to the
+// kernel, so repeated clusterings in one process (serving, bench.py) do not pay the page
+// faults again.  Process-wide, set once.
+static void keep_host_heap() {
+  static bool done = false;
+  if (done) return;
+  done = true;
+  mallopt(M_MMAP_THRESHOLD, 1 << 30);
+  mallopt(M_TRIM_THRESHOLD, 1 << 30);
+}
+
 RunResult run_pipeline(const Dataset &ds, mc_ctx *ctx, Options opt, bool upload, const ShardComm *comm) {
+  keep_host_heap();
   RunResult rr;
   rr.n = ds.size();
   const bool verbose = !opt.quiet;
