@@ -1,5 +1,4 @@
 // runner.cpp -- see runner.hpp.
-#include <malloc.h>
 #include "runner.hpp"
 
 #include <libgen.h>
