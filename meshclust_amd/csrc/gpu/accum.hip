@@ -33,6 +33,7 @@
 // Only the workgroups owning a chunk of the window take part in a step.  Every spin has a
 // deadline, so a fault cannot leave a wave spinning forever (error 99).
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 #include "bvec_core.hpp"
@@ -94,6 +95,7 @@ struct AccArgs {
   uint64_t *cl_off;    // N + 1
   uint64_t *out;       // [0] clusters [1] steps [2] candidates [3] error [4] members
   uint64_t budget;     // longest wait for one hand-off, s_memrealtime ticks (100 MHz)
+  int prof;            // controller phase timers (MC_ACCUM_PROFILE)
 };
 
 struct Red {  // LDS scratch for block-wide reductions and scans
@@ -443,7 +445,7 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
   for (;;) {
     // ============ controller: advance the accumulate loop to the next scan step ============
     if (ctl) {
-      if (threadIdx.x == 0) t_mark = __builtin_amdgcn_s_memrealtime();
+      if (A.prof && threadIdx.x == 0) t_mark = __builtin_amdgcn_s_memrealtime();
       uint64_t S = 0, E = 0;
       bool have = false;
       while (last != NONE && !err) {
@@ -481,9 +483,11 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
         st64(r + 3, tag | kn);
         drain();  // record and kill-log entries (all stored by this lane) complete
         st32(A.go, step);
-        const uint64_t t = __builtin_amdgcn_s_memrealtime();
-        t_win += t - t_mark;
-        t_mark = t;
+        if (A.prof) {
+          const uint64_t t = __builtin_amdgcn_s_memrealtime();
+          t_win += t - t_mark;
+          t_mark = t;
+        }
       }
     }
     // ============ everyone: wait for the step ============================================
@@ -492,8 +496,8 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       for (;;) {
         uint32_t v;
-        while ((v = ld32(A.go)) == seen) {
-          if (timed_out(A, t0)) break;
+        for (uint32_t it = 1; (v = ld32(A.go)) == seen; it++) {
+          if ((it & 255) == 0 && timed_out(A, t0)) break;  // deadline checked every 256 polls
           __builtin_amdgcn_s_sleep(1);
         }
         if (v == seen) {
@@ -630,16 +634,18 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
       s_abort = 0;
       const uint32_t want = cum + nact;
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      while (ld32(A.arrive) != want) {
-        if (timed_out(A, t0)) {
+      for (uint32_t it = 1; ld32(A.arrive) != want; it++) {
+        if ((it & 255) == 0 && timed_out(A, t0)) {
           s_abort = 1;
           break;
         }
         __builtin_amdgcn_s_sleep(1);
       }
-      const uint64_t t = __builtin_amdgcn_s_memrealtime();
-      t_wait += t - t_mark;
-      t_mark = t;
+      if (A.prof) {
+        const uint64_t t = __builtin_amdgcn_s_memrealtime();
+        t_wait += t - t_mark;
+        t_mark = t;
+      }
     }
     cum += nact;
     __syncthreads();
@@ -680,7 +686,7 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
         best_pos = s_bp[i];
       }
     uint64_t tq = 0;
-    if (threadIdx.x == 0) {
+    if (A.prof && threadIdx.x == 0) {
       tq = __builtin_amdgcn_s_memrealtime();
       t_sub[0] += tq - t_mark;
     }
@@ -705,7 +711,7 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
         bv.kill_one(p);
       }
       __syncthreads();
-      if (threadIdx.x == 0) {
+      if (A.prof && threadIdx.x == 0) {
         const uint64_t t = __builtin_amdgcn_s_memrealtime();
         t_sub[1] += t - tq;
         tq = t;
@@ -716,7 +722,7 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
       add_rows_acc<T>(Rs, in_lds ? s_mpos + M : A.mem_pos + mb, (uint32_t)nflag, A.nch, msum);
       M += nflag;
       __syncthreads();
-      if (threadIdx.x == 0) {
+      if (A.prof && threadIdx.x == 0) {
         const uint64_t t = __builtin_amdgcn_s_memrealtime();
         t_sub[2] += t - tq;
         tq = t;
@@ -728,7 +734,7 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
       __syncthreads();
       const uint64_t win = R.r0;
       __syncthreads();
-      if (threadIdx.x == 0) t_sub[3] += __builtin_amdgcn_s_memrealtime() - tq;
+      if (A.prof && threadIdx.x == 0) t_sub[3] += __builtin_amdgcn_s_memrealtime() - tq;
       last = (uint32_t)win;
       bv.invalidate();
     } else if (best_pos != ~0ull) {
@@ -750,7 +756,7 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
       if (p != ~0ull) new_cluster(p);
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (A.prof && threadIdx.x == 0) {
       const uint64_t t = __builtin_amdgcn_s_memrealtime();
       t_coll += t - t_mark;
     }
@@ -856,6 +862,7 @@ int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, 
   A.cl_off = d_cl_off;
   A.out = d_out;
   A.budget = 20ull * 100000000ull;  // a single hand-off never takes 20 s: give up, report error 99
+  A.prof = getenv("MC_ACCUM_PROFILE") ? 1 : 0;
   DevClassifier cls = c->cls;
   void *args[] = {&A, &cls};
   timed_begin(c);
