@@ -93,6 +93,7 @@ std::vector<PairId> Trainer::split() {
   std::vector<uint32_t> all_ids = points;  // distance keys are requested in id order
   {
     Scope s(timer_, "train.sort_keys");
+    Scope s2(timer_, "train.sort_keys.first");
     std::sort(points.begin(), points.end(),
               [&](uint32_t a, uint32_t b) { return ds_.lengths[a] < ds_.lengths[b]; });  // Trainer.cpp:672-675
     uint32_t begin_pt = points[N / 2];
@@ -121,7 +122,11 @@ std::vector<PairId> Trainer::split() {
   sorted.reserve(P);
   {
     Scope s(timer_, "train.sort_keys");
-    check(mc_distance_keys(ctx_, indices.data(), (uint32_t)P, all_ids.data(), N, keys.data()), "mc_distance_keys");
+    {
+      Scope s3(timer_, "train.sort_keys.pivots_dev");
+      check(mc_distance_keys(ctx_, indices.data(), (uint32_t)P, all_ids.data(), N, keys.data()), "mc_distance_keys");
+    }
+    Scope s4(timer_, "train.sort_keys.build");
     std::vector<std::vector<uint64_t>> w(P);
 #pragma omp parallel for schedule(dynamic) num_threads(cfg_.threads)
     for (size_t i = 0; i < P; i++) {
@@ -146,11 +151,17 @@ std::vector<PairId> Trainer::split() {
         if (active[i]) who.push_back(i);
       }
       batch.resize(who.size());
+      {
+        Scope s2(timer_, "train.nw_search.resolve");
 #pragma omp parallel for schedule(dynamic) num_threads(cfg_.threads)
-      for (size_t t = 0; t < who.size(); t++) batch[t] = PairId(indices[who[t]], pt_at(who[t], pivot[who[t]]));
+        for (size_t t = 0; t < who.size(); t++) batch[t] = PairId(indices[who[t]], pt_at(who[t], pivot[who[t]]));
+      }
       if (batch.empty()) break;
       std::vector<double> al;
-      nw_batch(batch, al);
+      {
+        Scope s3(timer_, "train.nw_search.align");
+        nw_batch(batch, al);
+      }
       for (size_t t = 0; t < who.size(); t++) {
         size_t i = who[t];
         double algn = al[t];
