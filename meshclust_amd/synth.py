@@ -39,6 +39,37 @@ def reads(n, length, n_templates, mut, seed):
         yield b"read%d template_%d" % (i, t), _ALPHA[base].tobytes()
 
 
+def _mutate(rng, s, mut):
+    p = mut / 3.0
+    r = rng.random(len(s))
+    sub = r < p
+    dele = (r >= p) & (r < 2 * p)
+    ins = (r >= 2 * p) & (r < mut)
+    s2 = s.copy()
+    s2[sub] = rng.integers(0, 4, size=int(sub.sum()), dtype=np.uint8)
+    keep = ~dele
+    reps = np.where(ins, 2, 1)[keep]
+    base = np.repeat(s2[keep], reps)
+    idx = np.cumsum(reps) - 1
+    insm = reps == 2
+    base[idx[insm]] = rng.integers(0, 4, size=int(insm.sum()), dtype=np.uint8)
+    return base
+
+
+def families(n_fam, per_fam, lmin, lmax, mut_lo, mut_hi, seed):
+    """Viral-shape set (the shape of Tables/Viral.csv): n_fam
+    family templates of uniform length in [lmin, lmax], each genome a copy of its family's
+    template with a per-genome mutation rate uniform in [mut_lo, mut_hi].  Headers
+    ``>genome{i} family_{f}``."""
+    rng = np.random.default_rng(seed)
+    temps = [rng.integers(0, 4, size=int(rng.integers(lmin, lmax + 1)), dtype=np.uint8)
+             for _ in range(n_fam)]
+    for i in range(n_fam * per_fam):
+        f = i % n_fam
+        base = _mutate(rng, temps[f], float(rng.uniform(mut_lo, mut_hi)))
+        yield b"genome%d family_%d" % (i, f), _ALPHA[base].tobytes()
+
+
 def write_fasta(path, records, width=60, newline=b"\n"):
     with open(path, "wb") as f:
         for hdr, seq in records:

@@ -9,6 +9,7 @@ STEPS="${*:-smoke pytest bench_small bench}"
 status() { echo "$1 rc=$2 t=$(date +%s)" | tee -a gpurun_out/status.txt; }
 for s in $STEPS; do
   case $s in
+    configs) timeout -k 10 1500 python scripts/configs.py ${CONFIGS:-E91 C20k E9100 C20k_m15} > gpurun_out/configs.log 2>&1 ;;
     e2e) timeout -k 10 300 python scripts/e2e_quick.py a1k b3k30 m2k_id80 fam2k fam2k_id85 > gpurun_out/e2e.log 2>&1 ;;
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 ;;
     pytest) timeout -k 10 1200 python -m pytest tests -m gpu -q -p no:cacheprovider --timeout 600 > gpurun_out/pytest_gpu.log 2>&1 ;;
