@@ -98,16 +98,62 @@ class LazyIntroSort {
     } else {
       std::iter_swap(f, b);
     }
-    uint64_t *first = f + 1, *last = f + n;
-    const uint64_t piv = *f;
-    for (;;) {
-      while (less(*first, piv)) ++first;
-      --last;
-      while (less(piv, *last)) --last;
-      if (!(first < last)) return first - f;
-      std::iter_swap(first, last);
-      ++first;
+    return hoare_cut(f, n);
+  }
+
+  // std::__unguarded_partition(f+1, f+n, f) computed from two stopper bitmasks.  The left
+  // scan stops at keys >= pivot, the right scan at keys <= pivot; the k-th swap exchanges the
+  // k-th left stopper l_k with the k-th right stopper r_k of the ORIGINAL array as long as
+  // l_k < r_k (neither scan ever reads a position an earlier swap wrote before the scans
+  // cross), and the returned cut is min(l_{K+1}, r_K): a left scan that runs past r_K stops
+  // there, because r_K now holds a key >= pivot.  Same swaps, same cut, without a
+  // data-dependent branch per element.
+  static int64_t hoare_cut(uint64_t *f, int64_t n) {
+    static thread_local std::vector<uint64_t> ge, le;
+    const uint64_t pk = f[0] >> 32;
+    const int64_t nw = (n + 63) >> 6;
+    ge.assign(nw, 0);
+    le.assign(nw, 0);
+    for (int64_t w = 0; w < nw; w++) {
+      const int64_t base = w << 6, cnt = std::min<int64_t>(64, n - base);
+      uint64_t g = 0, l = 0;
+      for (int64_t b = 0; b < cnt; b++) {
+        const uint64_t k = f[base + b] >> 32;
+        g |= (uint64_t)(k >= pk) << b;
+        l |= (uint64_t)(k <= pk) << b;
+      }
+      ge[w] = g;
+      le[w] = l;
     }
+    ge[0] &= ~1ull;  // the left scan starts at f+1; the right scan may stop at the pivot, f[0]
+    auto next_ge = [&](int64_t from) -> int64_t {
+      if (from >= n) return n;
+      int64_t w = from >> 6;
+      uint64_t bits = ge[w] & (~0ull << (from & 63));
+      while (!bits) {
+        if (++w >= nw) return n;
+        bits = ge[w];
+      }
+      return (w << 6) + __builtin_ctzll(bits);
+    };
+    auto prev_le = [&](int64_t from) -> int64_t {
+      if (from < 0) return -1;
+      int64_t w = from >> 6;
+      uint64_t bits = le[w] & (~0ull >> (63 - (from & 63)));
+      while (!bits) {
+        if (--w < 0) return -1;
+        bits = le[w];
+      }
+      return (w << 6) + 63 - __builtin_clzll(bits);
+    };
+    int64_t li = next_ge(1), ri = prev_le(n - 1), last_r = n;
+    while (li < ri) {
+      std::iter_swap(f + li, f + ri);
+      last_r = ri;
+      li = next_ge(li + 1);
+      ri = prev_le(ri - 1);
+    }
+    return std::min(li, last_r);
   }
 
   // stable insertion sort (std::__insertion_sort / __unguarded_linear_insert move only

@@ -7,6 +7,7 @@
 #include <cmath>
 #include <cstdio>
 #include <set>
+#include <thread>
 
 namespace mc {
 
@@ -141,26 +142,59 @@ std::vector<PairId> Trainer::split() {
   // batched NW launch per step.
   std::vector<size_t> offset(P, N / 4), pivot(P, 2 * (N / 4));
   std::vector<char> active(P, 1);
+  // Sampler positions of the current pivot estimate (the loops of :732-755 below).
+  auto sample_positions = [&](size_t i, size_t pv, std::vector<size_t> &out) {
+    const size_t npts = sorted[i].size();
+    double before_inc = (double)pv / to_add_each, after_inc = ((double)(npts - pv)) / to_add_each;
+    double bs = 0, as = (double)pv;
+    for (int t = 0; t < (int)to_add_each; t++, bs += before_inc) out.push_back((size_t)(int)std::round(bs));
+    for (int t = 0; t < (int)to_add_each && std::round(as) < (double)npts; t++, as += after_inc)
+      out.push_back((size_t)(int)std::round(as));
+  };
   {
     Scope s(timer_, "train.nw_search");
-    for (;;) {
-      std::vector<PairId> batch;
-      std::vector<size_t> who;
+    std::vector<PairId> batch;
+    std::vector<size_t> who;
+    auto gather = [&]() {
+      who.clear();
       for (size_t i = 0; i < P; i++) {
         if (active[i] && offset[i] == 0) active[i] = 0;
         if (active[i]) who.push_back(i);
       }
       batch.resize(who.size());
-      {
-        Scope s2(timer_, "train.nw_search.resolve");
+    };
+    gather();
+    {
+      Scope s2(timer_, "train.nw_search.resolve");
 #pragma omp parallel for schedule(dynamic) num_threads(cfg_.threads)
-        for (size_t t = 0; t < who.size(); t++) batch[t] = PairId(indices[who[t]], pt_at(who[t], pivot[who[t]]));
-      }
-      if (batch.empty()) break;
+      for (size_t t = 0; t < who.size(); t++) batch[t] = PairId(indices[who[t]], pt_at(who[t], pivot[who[t]]));
+    }
+    while (!batch.empty()) {
+      // The GPU aligns this round's pairs while the host resolves, in every chain, both
+      // positions the next round can probe (pivot -/+ offset), or in a chain's last round the
+      // sampler's positions around the final pivot: the lazy sorts' partitions are then ready
+      // when the identities come back.  Each LazyIntroSort is touched by one host thread only.
       std::vector<double> al;
+      std::thread gpu([&]() { nw_batch(batch, al); });
+      {
+        Scope s2(timer_, "train.nw_search.speculate");  // one core left to the thread driving the GPU
+#pragma omp parallel for schedule(dynamic) num_threads(std::max(1, cfg_.threads - 1))
+        for (size_t t = 0; t < who.size(); t++) {
+          const size_t i = who[t];
+          std::vector<size_t> pos;
+          if (offset[i] / 2 > 0) {
+            pos.push_back(pivot[i] - offset[i]);
+            pos.push_back(pivot[i] + offset[i]);
+          } else {  // last round: the final pivot is pivot-1, pivot or pivot+1
+            sample_positions(i, pivot[i], pos);
+          }
+          for (size_t q : pos)
+            if (q < sorted[i].size()) pt_at(i, q);
+        }
+      }
       {
         Scope s3(timer_, "train.nw_search.align");
-        nw_batch(batch, al);
+        gpu.join();
       }
       for (size_t t = 0; t < who.size(); t++) {
         size_t i = who[t];
@@ -170,6 +204,10 @@ std::vector<PairId> Trainer::split() {
         else { active[i] = 0; continue; }
         offset[i] /= 2;
       }
+      gather();
+      Scope s2(timer_, "train.nw_search.resolve");
+#pragma omp parallel for schedule(dynamic) num_threads(cfg_.threads)
+      for (size_t t = 0; t < who.size(); t++) batch[t] = PairId(indices[who[t]], pt_at(who[t], pivot[who[t]]));
     }
   }
   int aerr = 0;
