@@ -48,6 +48,38 @@ class LazyIntroSort {
 
   size_t size() const { return a_.size(); }
 
+  // The whole array sorted exactly as std::sort sorts it (same partitions, same leaves), the
+  // right part of every partition above `grain` elements handed to an OpenMP task.  Call
+  // from inside a parallel region's single construct, or serially.
+  static void sort_words(uint64_t *f, int64_t n, int depth = -1, int64_t grain = 8192) {
+    if (depth < 0) {
+      int lg = 0;
+      while (n >> (lg + 1)) lg++;
+      depth = 2 * lg;
+    }
+    while (n > 16) {
+      if (depth == 0) {
+        auto cmp = [](uint64_t x, uint64_t y) { return less(x, y); };
+        std::make_heap(f, f + n, cmp);
+        std::sort_heap(f, f + n, cmp);
+        return;
+      }
+      depth--;
+      const int64_t cut = partition_pivot(f, n);
+      uint64_t *r = f + cut;
+      const int64_t rn = n - cut;
+      const int d = depth;
+      if (rn > grain) {
+#pragma omp task firstprivate(r, rn, d, grain)
+        sort_words(r, rn, d, grain);
+      } else {
+        sort_words(r, rn, d, grain);
+      }
+      n = cut;
+    }
+    insertion_sort(f, n);
+  }
+
  private:
   struct Node {
     int64_t lo, hi;

@@ -95,14 +95,30 @@ std::vector<PairId> Trainer::split() {
   {
     Scope s(timer_, "train.sort_keys");
     Scope s2(timer_, "train.sort_keys.first");
-    std::sort(points.begin(), points.end(),
-              [&](uint32_t a, uint32_t b) { return ds_.lengths[a] < ds_.lengths[b]; });  // Trainer.cpp:672-675
+    // Both sorts are std::sort with a key-only comparator on (key << 32 | id) words:
+    // LazyIntroSort::sort_words performs the same partitions and leaves (so the same
+    // permutation, ties included), with the subranges sorted as parallel tasks.
+    auto exact_sort = [&](std::vector<uint64_t> &w) {
+#pragma omp parallel num_threads(cfg_.threads)
+#pragma omp single
+      LazyIntroSort::sort_words(w.data(), (int64_t)w.size());
+    };
+    std::vector<uint64_t> w(N);
+    bool wide = false;
+    for (size_t t = 0; t < N; t++) wide |= ds_.lengths[t] >> 32 != 0;
+    if (wide) {
+      std::sort(points.begin(), points.end(),
+                [&](uint32_t a, uint32_t b) { return ds_.lengths[a] < ds_.lengths[b]; });  // Trainer.cpp:672-675
+    } else {
+      for (size_t t = 0; t < N; t++) w[t] = ((uint64_t)ds_.lengths[t] << 32) | t;
+      exact_sort(w);
+      for (size_t t = 0; t < N; t++) points[t] = (uint32_t)w[t];
+    }
     uint32_t begin_pt = points[N / 2];
     std::vector<uint16_t> key0(N);
     check(mc_distance_keys(ctx_, &begin_pt, 1, all_ids.data(), N, key0.data()), "mc_distance_keys");
-    std::vector<uint64_t> w(N);
     for (size_t t = 0; t < N; t++) w[t] = ((uint64_t)key0[points[t]] << 32) | points[t];
-    std::sort(w.begin(), w.end(), [](uint64_t a, uint64_t b) { return (a >> 32) < (b >> 32); });
+    exact_sort(w);  // Trainer.cpp:679-684
     for (size_t t = 0; t < N; t++) points[t] = (uint32_t)w[t];
   }
   int num_iterations = (int)std::ceil(((double)cfg_.n_points) / cfg_.max_pts_from_one) - 1;

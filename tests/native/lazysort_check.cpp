@@ -39,6 +39,14 @@ int main() {
         printf("MISMATCH case %d n=%lld kmax=%u depth=%d pos=%lld\n", t, (long long)n, kmax, depth, (long long)q[i]);
         return 1;
       }
+    std::vector<uint64_t> full = a;  // the whole-array form, partitions run as OpenMP tasks
+#pragma omp parallel num_threads(4)
+#pragma omp single
+    mc::LazyIntroSort::sort_words(full.data(), n, depth, 64);
+    if (full != want) {
+      printf("MISMATCH sort_words case %d n=%lld kmax=%u depth=%d\n", t, (long long)n, kmax, depth);
+      return 1;
+    }
     cases++;
   }
   printf("OK %d cases\n", cases);

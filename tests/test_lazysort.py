@@ -10,7 +10,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 
 def test_lazy_introsort_matches_std_sort(tmp_path):
     exe = str(tmp_path / "lazysort_check")
-    subprocess.run(["g++", "-O2", "-std=c++17", os.path.join(HERE, "native", "lazysort_check.cpp"), "-o", exe],
+    subprocess.run(["g++", "-O2", "-fopenmp", "-std=c++17", os.path.join(HERE, "native", "lazysort_check.cpp"), "-o", exe],
                    check=True)
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and r.stdout.startswith("OK"), r.stdout + r.stderr
