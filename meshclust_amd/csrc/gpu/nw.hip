@@ -560,10 +560,28 @@ __global__ __launch_bounds__(64 * W) void nw_mw_kernel(NWPairs q) {
   }
 }
 
+// Waves per pair in the latency form.  Up to 1,024 rows four waves (one per SIMD, R = 4)
+// measured fastest; longer pairs (config E's 8-12 kb genomes) run eight (two waves per SIMD,
+// one wave's dependent-issue stalls filled by the other's cells): 14 % less end-to-end time
+// on the 10 kb sets, while eight waves on 1 kb pairs cost 7 % more NW time (profiles/
+// r01_v7_nw_waves.txt).  MC_NW_WAVES = 4, 8 or 16 forces one width for every pair.
+inline int mw_waves(uint64_t la) {
+  static const int forced = [] {
+    const char *e = getenv("MC_NW_WAVES");
+    const int v = e ? atoi(e) : 0;
+    return v == 4 || v == 8 || v == 16 ? v : 0;
+  }();
+  return forced ? forced : la <= 1024 ? 4 : 8;
+}
+
 template <int R, typename P>
-int launch_bucket_mw(mc_ctx *c, NWPairs q) {
+int launch_bucket_mw(mc_ctx *c, NWPairs q, int waves) {
   if (q.npairs == 0) return MC_OK;
-  nw_mw_kernel<R, P, 4><<<q.npairs, 256, 0, c->stream>>>(q);
+  switch (waves) {
+    case 4: nw_mw_kernel<R, P, 4><<<q.npairs, 256, 0, c->stream>>>(q); break;
+    case 16: nw_mw_kernel<R, P, 16><<<q.npairs, 1024, 0, c->stream>>>(q); break;
+    default: nw_mw_kernel<R, P, 8><<<q.npairs, 512, 0, c->stream>>>(q); break;
+  }
   MCG_CHECK(hipGetLastError());
   return MC_OK;
 }
@@ -576,10 +594,11 @@ int launch_nw(mc_ctx *c, const uint8_t *d_A, const uint64_t *d_aoff, const uint3
               int32_t *d_score, const uint32_t *d_out) {
   if (m == 0) return MC_OK;
   // bucket pairs by rows per lane and payload width; boundary scratch for multi-block pairs.
-  // Few pairs (fewer than the chip's SIMDs) are latency-bound: one 4-wave workgroup per pair;
+  // Few pairs (fewer than the chip's SIMDs) are latency-bound: one multi-wave workgroup per pair;
   // many pairs: one wavefront per pair.
   const bool mw = m < 1024;
-  enum { NB = 8 };
+  enum { NB = 24 };  // latency form: (R, payload) x waves 4 / 8 / 16
+  int bucket_waves[NB] = {0};
   std::vector<uint32_t> bucket[NB];
   std::vector<uint64_t> boff[NB];
   uint64_t scratch[NB] = {0};
@@ -589,9 +608,12 @@ int launch_nw(mc_ctx *c, const uint8_t *d_A, const uint64_t *d_aoff, const uint3
     int r, bk;
     uint64_t rows;
     if (mw) {
-      r = la <= 256 ? 0 : la <= 512 ? 1 : la <= 1024 ? 2 : 3;  // R = 1, 2, 4, 8 over 4 waves
-      bk = r + (wide ? 4 : 0);
-      rows = 256ull << r;
+      const int wv = mw_waves(la);
+      const uint64_t w64 = 64ull * wv;  // rows of R = 1
+      r = la <= w64 ? 0 : la <= 2 * w64 ? 1 : la <= 4 * w64 ? 2 : 3;  // R = 1, 2, 4, 8 over the waves
+      bk = r + (wide ? 4 : 0) + (wv == 4 ? 0 : wv == 8 ? 8 : 16);
+      bucket_waves[bk] = wv;
+      rows = w64 << r;
     } else {
       r = la <= 256 ? 0 : la <= 512 ? 1 : 2;  // R = 4, 8, 16
       bk = r + (wide ? 3 : 0);
@@ -622,15 +644,16 @@ int launch_nw(mc_ctx *c, const uint8_t *d_A, const uint64_t *d_aoff, const uint3
               (int *)c->s_c.p, (uint64_t *)c->s_b.p + io, d_ident, d_len, d_ids, d_score, d_out};
     int rc = MC_OK;
     if (mw) {
-      switch (k) {
-        case 0: rc = launch_bucket_mw<1, uint32_t>(c, q); break;
-        case 1: rc = launch_bucket_mw<2, uint32_t>(c, q); break;
-        case 2: rc = launch_bucket_mw<4, uint32_t>(c, q); break;
-        case 3: rc = launch_bucket_mw<8, uint32_t>(c, q); break;
-        case 4: rc = launch_bucket_mw<1, uint64_t>(c, q); break;
-        case 5: rc = launch_bucket_mw<2, uint64_t>(c, q); break;
-        case 6: rc = launch_bucket_mw<4, uint64_t>(c, q); break;
-        default: rc = launch_bucket_mw<8, uint64_t>(c, q); break;
+      const int wv = bucket_waves[k];
+      switch (k % 8) {
+        case 0: rc = launch_bucket_mw<1, uint32_t>(c, q, wv); break;
+        case 1: rc = launch_bucket_mw<2, uint32_t>(c, q, wv); break;
+        case 2: rc = launch_bucket_mw<4, uint32_t>(c, q, wv); break;
+        case 3: rc = launch_bucket_mw<8, uint32_t>(c, q, wv); break;
+        case 4: rc = launch_bucket_mw<1, uint64_t>(c, q, wv); break;
+        case 5: rc = launch_bucket_mw<2, uint64_t>(c, q, wv); break;
+        case 6: rc = launch_bucket_mw<4, uint64_t>(c, q, wv); break;
+        default: rc = launch_bucket_mw<8, uint64_t>(c, q, wv); break;
       }
     } else switch (k) {
       case 0: rc = launch_bucket<4, uint32_t>(c, q); break;

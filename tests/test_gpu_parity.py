@@ -77,7 +77,7 @@ def test_nw_golden(eng):
 
 
 def test_nw_golden_batch_paths(eng):
-    """The golden pairs through both launch forms: a small batch (one 4-wave workgroup per
+    """The golden pairs through both launch forms: a small batch (one multi-wave workgroup per
     pair, DPP lane shifts, LDS ring between waves) and a batch of >= 1024 pairs (one wavefront
     per pair)."""
     g = np.load(fixtures.golden("nw.npz"))
@@ -96,10 +96,12 @@ def test_nw_golden_batch_paths(eng):
 
 
 def test_nw_long_multiblock_vs_oracle(eng):
-    """Pairs longer than one 1024-row block (boundary row in scratch) and >64k total length."""
+    """Pairs longer than one row block of either launch form (boundary row in scratch: the
+    latency form's blocks are 64*R*W rows, 4096 at W = 8, 8192 at W = 16)."""
     rng = np.random.default_rng(9)
     pairs = []
-    for la, lb in ((1500, 1400), (2100, 2500), (4000, 3900), (1025, 1030), (3000, 200)):
+    for la, lb in ((1500, 1400), (2100, 2500), (4000, 3900), (1025, 1030), (3000, 200), (5000, 4900),
+                   (9000, 8500)):
         a = rng.integers(0, 4, size=la).astype(np.uint8)
         b = a[:lb].copy() if lb <= la else np.concatenate([a, rng.integers(0, 4, size=lb - la).astype(np.uint8)])
         flip = rng.random(len(b)) < 0.08
