@@ -6,9 +6,12 @@
 // consecutive rows of seq1 and sweeps the columns of seq2 one step behind lane l-1, so at
 // step t it computes column t-l+1 for its R rows.  The bottom row of lane l-1 (M, X, Y and
 // their payloads) and the seq2 code travel down the wave through one shuffle per value and
-// step; nothing but that hand-off leaves registers.  Length and identity count of a state
-// are packed into one payload word (len << 16 | ids, or 32/32 bits for long pairs), so a
-// predecessor choice moves both with one select.  Sequences longer than 64*R rows are cut
+// step; nothing but that hand-off leaves registers.  Every move adds 1 to GlobAlignE's path
+// length and a diagonal move consumes a base of each sequence, a gap move one base, so a
+// path ending at (i, j) has length i + j - (diagonal moves).  A state therefore carries the
+// diagonal count and the identity count packed in one payload word (diag << 16 | ids, or
+// 32/32 bits for long pairs): a predecessor choice moves both with one select, a gap move
+// leaves the payload unchanged, and the final length is la + lb - diag.  Sequences longer than 64*R rows are cut
 // into row blocks whose boundary row is kept in global scratch.
 //
 // Recurrences (rows i over seq1, columns j over seq2; GlobAlignE's names in brackets):
@@ -99,7 +102,7 @@ __global__ __launch_bounds__(64) void nw_kernel(NWPairs q) {
       M[r] = NINF;
       Y[r] = NINF;
       X[r] = -GO - i * GE;
-      MP[r] = XP[r] = YP[r] = (P)i << SH;
+      MP[r] = XP[r] = YP[r] = 0;  // i gap moves, no diagonal
     }
     // diagonal input for column 1: row itop-1 at column 0
     int dM, dX, dY;
@@ -115,7 +118,7 @@ __global__ __launch_bounds__(64) void nw_kernel(NWPairs q) {
         dM = NINF;
         dX = -GO - i * GE;
         dY = NINF;
-        dMP = dXP = dYP = (P)i << SH;
+        dMP = dXP = dYP = 0;
       }
     }
     int oM = NINF, oX = NINF, oY = NINF;  // this lane's bottom row, last computed column
@@ -143,7 +146,7 @@ __global__ __launch_bounds__(64) void nw_kernel(NWPairs q) {
           uM = NINF;
           uX = NINF;
           uY = -GO - j * GE;
-          uMP = uXP = uYP = (P)j << SH;
+          uMP = uXP = uYP = 0;
         } else if (j >= 1 && j <= lb) {
           const int *s = bnd + 6 * j;
           uM = s[0];
@@ -175,7 +178,7 @@ __global__ __launch_bounds__(64) void nw_kernel(NWPairs q) {
           const int yb = pM - (GO + GE), yc = pY - GE;
           const bool yFromM = yb >= yc;
           Y[r] = yFromM ? yb : yc;
-          YP[r] = (yFromM ? pMP : pYP) + LEN1;
+          YP[r] = yFromM ? pMP : pYP;
           // matches (:255-299)
           const bool hit = ac[r] == bc;
           const int s = hit ? MATCH : MISMATCH;
@@ -189,7 +192,7 @@ __global__ __launch_bounds__(64) void nw_kernel(NWPairs q) {
           const int xb = aM - (GO + GE), xc = aX - GE;
           const bool xFromM = xb >= xc;
           X[r] = xFromM ? xb : xc;
-          XP[r] = (xFromM ? aMP : aXP) + LEN1;
+          XP[r] = xFromM ? aMP : aXP;
           // next row: above = this row's new values, diagonal = this row's old values
           aM = M[r];
           aX = X[r];
@@ -272,7 +275,7 @@ __global__ __launch_bounds__(64) void nw_kernel(NWPairs q) {
       I = 0;
       fin_score = lb > 0 ? NINF : 0;
     } else {
-      L = (int)(fin_pay >> SH);
+      L = la + lb - (int)(fin_pay >> SH);
       I = (int)(fin_pay & (((P)1 << SH) - 1));
     }
     const uint32_t o = q.out ? q.out[p] : p;
@@ -351,7 +354,7 @@ __global__ __launch_bounds__(64 * W) void nw_mw_kernel(NWPairs q) {
       M[r] = NINF;  // column 0 (GlobAlignE.cpp:140-160)
       Y[r] = NINF;
       X[r] = -GO - i * GE;
-      MP[r] = XP[r] = YP[r] = (P)i << SH;
+      MP[r] = XP[r] = YP[r] = 0;  // i gap moves, no diagonal
     }
     int dM, dX, dY;
     P dMP, dXP, dYP;
@@ -366,7 +369,7 @@ __global__ __launch_bounds__(64 * W) void nw_mw_kernel(NWPairs q) {
         dM = NINF;
         dX = -GO - i * GE;
         dY = NINF;
-        dMP = dXP = dYP = (P)i << SH;
+        dMP = dXP = dYP = 0;
       }
     }
     int oM = NINF, oX = NINF, oY = NINF;
@@ -426,7 +429,7 @@ __global__ __launch_bounds__(64 * W) void nw_mw_kernel(NWPairs q) {
             uM = NINF;
             uX = NINF;
             uY = -GO - j * GE;
-            uMP = uXP = uYP = (P)j << SH;
+            uMP = uXP = uYP = 0;
           } else {  // bottom row of wave w-1 (or of the previous row block) at column j
             uM = nM;
             uX = nX;
@@ -450,7 +453,7 @@ __global__ __launch_bounds__(64 * W) void nw_mw_kernel(NWPairs q) {
           const int yb = pM - (GO + GE), yc = pY - GE;  // upperGap (GlobAlignE.cpp:233-251)
           const bool yFromM = yb >= yc;
           Y[r] = yFromM ? yb : yc;
-          YP[r] = (yFromM ? pMP : pYP) + LEN1;
+          YP[r] = yFromM ? pMP : pYP;
           const bool hit = ac[r] == (uint8_t)bc;  // matches (:255-299)
           const int sc = hit ? MATCH : MISMATCH;
           const bool fromM = gM >= gX && gM >= gY;
@@ -462,7 +465,7 @@ __global__ __launch_bounds__(64 * W) void nw_mw_kernel(NWPairs q) {
           const int xb = aM - (GO + GE), xc = aX - GE;  // lowerGap (:316-330)
           const bool xFromM = xb >= xc;
           X[r] = xFromM ? xb : xc;
-          XP[r] = (xFromM ? aMP : aXP) + LEN1;
+          XP[r] = xFromM ? aMP : aXP;
           aM = M[r];
           aX = X[r];
           aMP = MP[r];
@@ -549,7 +552,7 @@ __global__ __launch_bounds__(64 * W) void nw_mw_kernel(NWPairs q) {
       I = 0;
       fin_score = lb > 0 ? NINF : 0;
     } else {
-      L = (int)(fin_pay >> SH);
+      L = la + lb - (int)(fin_pay >> SH);
       I = (int)(fin_pay & (((P)1 << SH) - 1));
     }
     const uint32_t o = q.out ? q.out[p] : p;
