@@ -182,10 +182,13 @@ __global__ __launch_bounds__(64) void nw_kernel(NWPairs q) {
           // matches (:255-299)
           const bool hit = ac[r] == bc;
           const int s = hit ? MATCH : MISMATCH;
-          const bool fromM = gM >= gX && gM >= gY;
-          const bool fromX = !fromM && gX >= gY;
-          const int best = fromM ? gM : (fromX ? gX : gY);
-          const P bestP = fromM ? gMP : (fromX ? gXP : gYP);
+          // M on ties, then X, then Y: M iff gM >= max(gX, gY), else X iff gX >= gY
+          const bool xy = gX >= gY;
+          const int mxy = xy ? gX : gY;
+          const P pxy = xy ? gXP : gYP;
+          const bool fromM = gM >= mxy;
+          const int best = fromM ? gM : mxy;
+          const P bestP = fromM ? gMP : pxy;
           M[r] = best + s;
           MP[r] = bestP + LEN1 + (hit ? (P)1 : (P)0);
           // lowerGap (:316-330), from the row above in this column
@@ -456,10 +459,13 @@ __global__ __launch_bounds__(64 * W) void nw_mw_kernel(NWPairs q) {
           YP[r] = yFromM ? pMP : pYP;
           const bool hit = ac[r] == (uint8_t)bc;  // matches (:255-299)
           const int sc = hit ? MATCH : MISMATCH;
-          const bool fromM = gM >= gX && gM >= gY;
-          const bool fromX = !fromM && gX >= gY;
-          const int best = fromM ? gM : (fromX ? gX : gY);
-          const P bestP = fromM ? gMP : (fromX ? gXP : gYP);
+          // M on ties, then X, then Y: M iff gM >= max(gX, gY), else X iff gX >= gY
+          const bool xy = gX >= gY;
+          const int mxy = xy ? gX : gY;
+          const P pxy = xy ? gXP : gYP;
+          const bool fromM = gM >= mxy;
+          const int best = fromM ? gM : mxy;
+          const P bestP = fromM ? gMP : pxy;
           M[r] = best + sc;
           MP[r] = bestP + LEN1 + (hit ? (P)1 : (P)0);
           const int xb = aM - (GO + GE), xc = aX - GE;  // lowerGap (:316-330)
