@@ -5,8 +5,8 @@
 // One wavefront per pair, anti-diagonal wavefront over the DP matrix: lane l owns R
 // consecutive rows of seq1 and sweeps the columns of seq2 one step behind lane l-1, so at
 // step t it computes column t-l+1 for its R rows.  The bottom row of lane l-1 (M, X, Y and
-// their payloads) and the seq2 code travel down the wave through one shuffle per value and
-// step; nothing but that hand-off leaves registers.  Every move adds 1 to GlobAlignE's path
+// their payloads) and the seq2 code travel down the wave through one DPP lane shift per value
+// and step; nothing but that hand-off leaves registers.  Every move adds 1 to GlobAlignE's path
 // length and a diagonal move consumes a base of each sequence, a gap move one base, so a
 // path ending at (i, j) has length i + j - (diagonal moves).  A state therefore carries the
 // diagonal count and the identity count packed in one payload word (diag << 16 | ids, or
@@ -38,12 +38,15 @@ struct Pack<uint64_t> {
   static constexpr int SH = 32;
 };
 
+// Lane l receives lane l-1's value (DPP wave_shr:1, a VALU move; lane 0's result is
+// unspecified and always overwritten by the callers).
+__device__ __forceinline__ int dpp_shr1(int v) { return __builtin_amdgcn_mov_dpp(v, 0x138, 0xf, 0xf, false); }
 template <typename P>
-__device__ __forceinline__ P shup(P v) {
+__device__ __forceinline__ P dshr(P v) {
   if constexpr (sizeof(P) == 4) {
-    return (P)__shfl_up((int)v, 1, 64);
+    return (P)(uint32_t)dpp_shr1((int)v);
   } else {
-    uint32_t lo = __shfl_up((int)(uint32_t)v, 1, 64), hi = __shfl_up((int)(uint32_t)(v >> 32), 1, 64);
+    const uint32_t lo = (uint32_t)dpp_shr1((int)(uint32_t)v), hi = (uint32_t)dpp_shr1((int)(uint32_t)(v >> 32));
     return ((uint64_t)hi << 32) | lo;
   }
 }
@@ -136,9 +139,9 @@ __global__ __launch_bounds__(64) void nw_kernel(NWPairs q) {
         bnext = nx < lb ? b[nx] : 0;
       }
       // hand-off from lane-1: its bottom row at column j (computed at step t-1) + seq2 code
-      int uM = shup<int>(oM), uX = shup<int>(oX), uY = shup<int>(oY);
-      P uMP = shup<P>(oMP), uXP = shup<P>(oXP), uYP = shup<P>(oYP);
-      uint8_t bc = (uint8_t)__shfl_up((int)ob, 1, 64);
+      int uM = dpp_shr1(oM), uX = dpp_shr1(oX), uY = dpp_shr1(oY);
+      P uMP = dshr<P>(oMP), uXP = dshr<P>(oXP), uYP = dshr<P>(oYP);
+      uint8_t bc = (uint8_t)dpp_shr1((int)ob);
       const int b0 = __builtin_amdgcn_readlane(bcur, t & 63);
       if (lane == 0) {
         bc = (j >= 1 && j <= lb) ? (uint8_t)b0 : 0;
@@ -308,16 +311,6 @@ int launch_bucket(mc_ctx *c, NWPairs q) {
 // with DPP wave_shr:1 (a VALU move, no LDS round trip).
 constexpr int KLAG = 16, RING_C = 64;
 
-__device__ __forceinline__ int dpp_shr1(int v) { return __builtin_amdgcn_mov_dpp(v, 0x138, 0xf, 0xf, false); }
-template <typename P>
-__device__ __forceinline__ P dshr(P v) {
-  if constexpr (sizeof(P) == 4) {
-    return (P)(uint32_t)dpp_shr1((int)v);
-  } else {
-    const uint32_t lo = (uint32_t)dpp_shr1((int)(uint32_t)v), hi = (uint32_t)dpp_shr1((int)(uint32_t)(v >> 32));
-    return ((uint64_t)hi << 32) | lo;
-  }
-}
 
 template <int R, typename P, int W>
 __global__ __launch_bounds__(64 * W) void nw_mw_kernel(NWPairs q) {
