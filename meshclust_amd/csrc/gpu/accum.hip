@@ -24,12 +24,16 @@
 //
 // Hand-offs carry only a few words, so they use sc1 stores and loads (relaxed agent-scope
 // atomics: L1 bypassed, coherent across XCDs) with a drain before each signal instead of
-// release/acquire fences (MI355X_MICROARCH.md hand-off table, first row):
+// release/acquire fences (MI355X_MICROARCH.md hand-off table, first row).  The signal words
+// carry the step number in their upper half, so a reader polls the payload itself and one
+// L2 round trip per hand-off disappears:
 //   controller -> workers   a step record in a ring {centre, S, E, kill-log length}, each word
-//                           tagged with the step, then `go` = step; pops / erases are appended
-//                           to a kill log that owners apply before their next scan
-//   workers -> controller   flagged positions + {max, position, count} partial, then one
-//                           arrival per workgroup on `arrive`
+//                           tagged with the step (after a drain of the kill log: pops / erases
+//                           are appended to a log that owners apply before their next scan);
+//                           workers poll the next step's slot; `go` = step only serves a
+//                           workgroup that fell a whole ring behind
+//   workers -> controller   flagged positions, drained, then a 4-word {max, position, count}
+//                           partial, every word tagged with the step, polled by the controller
 // Only the workgroups owning a chunk of the window take part in a step.  Every spin has a
 // deadline, so a fault cannot leave a wave spinning forever (error 99).
 #include <algorithm>
@@ -50,11 +54,11 @@ constexpr uint32_t MCAP = 1024;  // members of the current cluster mirrored in L
 constexpr uint32_t RING = 64;    // step records kept for workgroups that read them late
 
 
+// A workgroup's result for one step: {val high half, val low half, position, flagged count},
+// each word tagged with the step in its upper 32 bits, so the controller polls the words
+// themselves (no arrival counter) and accepts them when all four carry the step.
 struct AccPartial {
-  double val;
-  uint64_t pos;
-  uint32_t nflag;
-  uint32_t pad;
+  uint64_t w[4];
 };
 
 // Static part of a centre's bvec window (bvec::get_range, bvec.cpp:245-278), per point id:
@@ -84,7 +88,7 @@ struct AccArgs {
   // hand-off (every handed-off word is stored and loaded with sc1 accesses, see below)
   uint64_t *ring;   // RING step records of 4 words
   uint32_t *klog;   // static positions killed by the controller (pop / erase), append-only
-  uint32_t *go, *arrive;
+  uint32_t *go;     // latest published step (for a workgroup that fell RING steps behind)
   AccPartial *partials;
   uint32_t *flist;  // G * fcap
   uint64_t fcap;
@@ -375,7 +379,6 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
   uint64_t ncl = 0, nsteps = 0, ncand = 0;
   uint32_t step = 0;
   uint64_t err = 0;
-  uint32_t cum = 0;                                  // arrivals expected so far
   uint32_t kn = 0;                                   // kill-log length
   uint64_t t_win = 0, t_wait = 0, t_coll = 0, t_mark = 0;  // controller phase time, 100 MHz ticks
   uint64_t t_sub[4] = {0, 0, 0, 0};  // collect: reduce, gather+kill, column sums, closest
@@ -477,11 +480,12 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
         // record even if the slot is being reused
         uint64_t *r = A.ring + (uint64_t)(step % RING) * 4;
         const uint64_t tag = (uint64_t)step << 32;
+        drain();  // kill-log entries complete before the record that announces them
         st64(r + 0, tag | (have ? last : NONE));
         st64(r + 1, tag | S);
         st64(r + 2, tag | E);
         st64(r + 3, tag | kn);
-        drain();  // record and kill-log entries (all stored by this lane) complete
+        drain();  // `go` (read only by a workgroup that fell RING steps behind) after the record
         st32(A.go, step);
         if (A.prof) {
           const uint64_t t = __builtin_amdgcn_s_memrealtime();
@@ -494,7 +498,36 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
     if (threadIdx.x == 0) {
       s_abort = 0;
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      for (;;) {
+      // steps are published in order: poll the next step's record itself (its words carry
+      // the step); a workgroup that finds the slot already rewritten for a later step fell
+      // RING steps behind and catches up through `go`
+      const uint32_t want = seen + 1;
+      const uint64_t *rn = A.ring + (uint64_t)(want % RING) * 4;
+      bool late = false;
+      for (uint32_t it = 1;; it++) {
+        const uint64_t w0 = ld64(rn + 0), w1 = ld64(rn + 1), w2 = ld64(rn + 2), w3 = ld64(rn + 3);
+        const uint32_t t_0 = (uint32_t)(w0 >> 32), t_1 = (uint32_t)(w1 >> 32), t_2 = (uint32_t)(w2 >> 32),
+                       t_3 = (uint32_t)(w3 >> 32);
+        if (t_0 == want && t_1 == want && t_2 == want && t_3 == want) {
+          s_rec[0] = w0;
+          s_rec[1] = (uint32_t)w1;
+          s_rec[2] = (uint32_t)w2;
+          s_rec[3] = w3;
+          s_go = want;
+          break;
+        }
+        if ((int32_t)(t_0 - want) > 0 || (int32_t)(t_1 - want) > 0 || (int32_t)(t_2 - want) > 0 ||
+            (int32_t)(t_3 - want) > 0) {
+          late = true;
+          break;
+        }
+        if ((it & 255) == 0 && timed_out(A, t0)) {
+          s_abort = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      while (late) {
         uint32_t v;
         for (uint32_t it = 1; (v = ld32(A.go)) == seen; it++) {
           if ((it & 255) == 0 && timed_out(A, t0)) break;  // deadline checked every 256 polls
@@ -619,49 +652,54 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
           v = s_bv[i];
           p = s_bp[i];
         }
-      uint64_t *q = reinterpret_cast<uint64_t *>(A.partials + g);
-      st64(q + 0, (uint64_t)__double_as_longlong(v));
-      st64(q + 1, p);
-      st64(q + 2, nfl);
-      drain();  // this lane's partial; the other waves' list stores drained before the barrier
-      __hip_atomic_fetch_add(A.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // every wave's list / alive stores were drained before the barrier: the tagged partial
+      // words are the signal
+      uint64_t *q = A.partials[g].w;
+      const uint64_t tag = (uint64_t)P.step << 32, vb = (uint64_t)__double_as_longlong(v);
+      st64(q + 0, tag | (vb >> 32));
+      st64(q + 1, tag | (vb & 0xffffffffull));
+      st64(q + 2, tag | (p == ~0ull ? (uint64_t)NONE : p));
+      st64(q + 3, tag | nfl);
     }
     }  // active workgroup
     if (!ctl) continue;
 
     // ============ controller: collect the step (get_close's reduction + get_mean) =========
-    if (threadIdx.x == 0) {
-      s_abort = 0;
-      const uint32_t want = cum + nact;
+    // thread t polls the partial of the t-th active workgroup until its four words carry this
+    // step (s_abort is 0 here: set only on a failed wait, which returns)
+    double bv_ = -1.0;
+    uint64_t bp_ = ~0ull, cnt_w = 0;
+    if (threadIdx.x < nact) {
+      const uint64_t *q = A.partials[(c0 + threadIdx.x) % G].w;
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      for (uint32_t it = 1; ld32(A.arrive) != want; it++) {
+      for (uint32_t it = 1;; it++) {
+        const uint64_t w0 = ld64(q + 0), w1 = ld64(q + 1), w2 = ld64(q + 2), w3 = ld64(q + 3);
+        if ((uint32_t)(w0 >> 32) == P.step && (uint32_t)(w1 >> 32) == P.step && (uint32_t)(w2 >> 32) == P.step &&
+            (uint32_t)(w3 >> 32) == P.step) {
+          bv_ = __longlong_as_double((long long)((w0 << 32) | (w1 & 0xffffffffull)));
+          const uint32_t p32 = (uint32_t)w2;
+          bp_ = p32 == NONE ? ~0ull : (uint64_t)p32;
+          cnt_w = (uint32_t)w3;
+          break;
+        }
         if ((it & 255) == 0 && timed_out(A, t0)) {
           s_abort = 1;
           break;
         }
         __builtin_amdgcn_s_sleep(1);
       }
-      if (A.prof) {
-        const uint64_t t = __builtin_amdgcn_s_memrealtime();
-        t_wait += t - t_mark;
-        t_mark = t;
-      }
     }
-    cum += nact;
+    if (A.prof && threadIdx.x == 0) {
+      const uint64_t t = __builtin_amdgcn_s_memrealtime();
+      t_wait += t - t_mark;
+      t_mark = t;
+    }
     __syncthreads();
     if (s_abort) {
       if (threadIdx.x == 0) atomicMax((unsigned long long *)&A.out[3], 99ull);
       return;
     }
     // first maximum over workgroups, flagged counts and their offsets
-    double bv_ = -1.0;
-    uint64_t bp_ = ~0ull, cnt_w = 0;
-    if (threadIdx.x < nact) {
-      const uint64_t *q = reinterpret_cast<const uint64_t *>(A.partials + (c0 + threadIdx.x) % G);
-      bv_ = __longlong_as_double((long long)ld64(q + 0));
-      bp_ = ld64(q + 1);
-      cnt_w = ld64(q + 2);
-    }
     uint64_t nflag;
     const uint64_t off_w = block_excl_scan(cnt_w, &nflag, R);
     if (threadIdx.x < nact) s_flag[threadIdx.x] = (uint32_t)off_w;  // nact <= G <= NT
@@ -821,7 +859,7 @@ int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, 
     return MC_ERR_HIP;
   }
   const uint64_t fcap = accum_fcap(c, G);
-  const size_t hand = 256 + (size_t)RING * 32;  // go, arrive, step ring
+  const size_t hand = 256 + (size_t)RING * 32;  // go, step ring
   const size_t part_bytes = ((size_t)G * sizeof(AccPartial) + 255) / 256 * 256;
   const size_t flist_bytes = ((size_t)G * fcap * 4 + 255) / 256 * 256;
   if (ensure(c->s_a, hand) || ensure(c->s_b, part_bytes + c->n * sizeof(WinTab)) ||
@@ -834,6 +872,7 @@ int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, 
   MCG_CHECK(hipGetLastError());
   timed_end(c, F_FINAL);
   MCG_CHECK(hipMemsetAsync(c->s_a.p, 0, hand, c->stream));
+  MCG_CHECK(hipMemsetAsync(c->s_b.p, 0, part_bytes, c->stream));  // no partial carries a step tag yet
   AccArgs A;
   memset(&A, 0, sizeof A);
   A.hs = (const uint4 *)c->hs.p;
@@ -850,7 +889,6 @@ int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, 
   A.sim = sim;
   A.wtab = d_wtab;
   A.go = (uint32_t *)c->s_a.p;
-  A.arrive = (uint32_t *)((char *)c->s_a.p + 128);
   A.ring = (uint64_t *)((char *)c->s_a.p + 256);
   A.partials = (AccPartial *)c->s_b.p;
   A.flist = (uint32_t *)c->s_c.p;
