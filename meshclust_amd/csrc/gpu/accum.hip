@@ -571,20 +571,27 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
     const uint32_t nact = (uint32_t)(c1 - c0 + 1 < (uint64_t)G ? c1 - c0 + 1 : (uint64_t)G);
     const uint32_t mine = (g + G - (uint32_t)(c0 % G)) % G;
     if (mine < nact) {
+    // The centre's chunks (staged in LDS below) and magnitudes depend only on the step record:
+    // loaded before the kill log is applied, so they share one round trip with the log's.
+    // (Prefetching the first chunk of candidate rows too would hold 64 more VGPRs across the
+    // barrier: the kernel then spills.)
+    const uint64_t ch0 = c0 + mine;
+    uint4 cpre = make_uint4(0, 0, 0, 0);
+    if (threadIdx.x < A.nch) cpre = Rs.chunk(P.centre, threadIdx.x);
+    const PInfo pc{A.mag_s[P.centre], A.sumsq_s[P.centre], A.len_s[P.centre]};
     for (uint64_t i = kcur + threadIdx.x; i < kend; i += NT) {  // controller kills since last time
       const uint32_t p = ld32(A.klog + i);
       const uint64_t ch = p / NT;
       if (ch % G == g) lal[(ch / G) * NT + p % NT] = 0;
     }
     kcur = kend;
-    for (int c = threadIdx.x; c < A.nch; c += NT)
-      clds[c] = Rs.chunk(P.centre, c);
-    const PInfo pc{A.mag_s[P.centre], A.sumsq_s[P.centre], A.len_s[P.centre]};
+    if (threadIdx.x < A.nch) clds[threadIdx.x] = cpre;
+    for (int c = NT + threadIdx.x; c < A.nch; c += NT) clds[c] = Rs.chunk(P.centre, c);
     __syncthreads();
     double best_v = -1.0;
     uint64_t best_p = ~0ull;
     uint32_t nfl = 0;  // this workgroup's flagged count (uniform)
-    for (uint64_t ch = c0 + mine; ch <= c1; ch += G) {
+    for (uint64_t ch = ch0; ch <= c1; ch += G) {
       const uint64_t pos = ch * NT + threadIdx.x;
       uint8_t *la = lal + (ch / G) * NT + threadIdx.x;
       const bool valid = pos >= P.S && pos <= P.E && *la;
@@ -592,17 +599,19 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
       if (valid) {
         Acc<T> acc;
         const uint4 *col = A.hs + pos;
+        PInfo pi;
         if (A.nch == 16) {
           uint4 v[16];
 #pragma unroll
           for (int k = 0; k < 16; k++) v[k] = col[(uint64_t)k * A.npad];
+          pi = PInfo{A.mag_s[pos], A.sumsq_s[pos], A.len_s[pos]};
 #pragma unroll
           for (int k = 0; k < 16; k++) acc.add(v[k], clds[k]);
         } else {
 #pragma unroll 8
           for (int k = 0; k < A.nch; k++) acc.add(col[(uint64_t)k * A.npad], clds[k]);
+          pi = PInfo{A.mag_s[pos], A.sumsq_s[pos], A.len_s[pos]};
         }
-        const PInfo pi{A.mag_s[pos], A.sumsq_s[pos], A.len_s[pos]};
         const PS s = acc.finish(pi.mag, pc.mag);
         double raw[MC_MAX_SINGLE];
 #pragma unroll

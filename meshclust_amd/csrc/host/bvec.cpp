@@ -7,6 +7,7 @@
 #include <limits>
 
 #include "common.hpp"
+#include "lazysort.hpp"
 
 namespace mc {
 
@@ -121,8 +122,28 @@ void BVec::insert(uint32_t id) {
 }
 
 void BVec::insert_finalize() {
-  for (auto &bin : data_)
-    std::sort(bin.begin(), bin.end(), [&](uint32_t a, uint32_t b) { return len_[a] < len_[b]; });
+  // std::sort of each bin by length (bvec.cpp's insert_finalize): the same permutation from
+  // LazyIntroSort::sort_words on (length << 32 | id) words, bins and subranges as tasks
+  bool wide = false;
+  for (uint64_t l : len_) wide |= l >> 32 != 0;
+  if (wide) {
+    for (auto &bin : data_)
+      std::sort(bin.begin(), bin.end(), [&](uint32_t a, uint32_t b) { return len_[a] < len_[b]; });
+  } else {
+#pragma omp parallel
+#pragma omp single
+    for (auto &bin : data_) {
+      if (bin.size() < 2) continue;
+      std::vector<uint32_t> *b = &bin;
+#pragma omp task firstprivate(b)
+      {
+        std::vector<uint64_t> w(b->size());
+        for (size_t t = 0; t < w.size(); t++) w[t] = (len_[(*b)[t]] << 32) | (*b)[t];
+        LazyIntroSort::sort_words(w.data(), (int64_t)w.size());
+        for (size_t t = 0; t < w.size(); t++) (*b)[t] = (uint32_t)w[t];
+      }
+    }
+  }
   order_.clear();
   bin_of_.clear();
   plen_.clear();

@@ -15,6 +15,7 @@ for s in $STEPS; do
     pytest) timeout -k 10 1200 python -m pytest tests -m gpu -q -p no:cacheprovider --timeout 600 > gpurun_out/pytest_gpu.log 2>&1 ;;
     bench_small) timeout -k 10 600 python bench.py --n 20000 --templates 200 --steps 2 --warmup 1 --no-cpu-baseline --stats-out gpurun_out/bench_small.json > gpurun_out/bench_small.log 2>&1 ;;
     bench_align) timeout -k 10 600 python bench.py --n 20000 --templates 200 --id 0.55 --steps 1 --warmup 1 --no-cpu-baseline --stats-out gpurun_out/bench_align.json > gpurun_out/bench_align.log 2>&1 ;;
+    bench_nocpu) timeout -k 10 900 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --stats-out gpurun_out/bench.json > gpurun_out/bench.log 2>&1 ;;
     bench) timeout -k 10 900 python bench.py --steps 3 --warmup 1 --stats-out gpurun_out/bench.json > gpurun_out/bench.log 2>&1 ;;
     prof) timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/prof.log 2>&1 ;;
     pmc) timeout -k 10 900 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/pmc_fetch.log 2>&1 &&
