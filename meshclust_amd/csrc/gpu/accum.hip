@@ -485,7 +485,8 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
         st64(r + 1, tag | S);
         st64(r + 2, tag | E);
         st64(r + 3, tag | kn);
-        drain();  // `go` (read only by a workgroup that fell RING steps behind) after the record
+        // `go` is only a hint for a workgroup that fell RING steps behind: it re-validates the
+        // record's tags after reading it, so no drain is needed between the two
         st32(A.go, step);
         if (A.prof) {
           const uint64_t t = __builtin_amdgcn_s_memrealtime();
