@@ -10,6 +10,8 @@
 #include <cerrno>
 #include <chrono>
 #include <cmath>
+#include <exception>
+#include <thread>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -170,18 +172,36 @@ RunResult run_pipeline(const Dataset &ds, mc_ctx *ctx, Options opt, bool upload,
   tc.threads = threads;
   tc.verbose = verbose;
   Trainer tr(ds, ctx, tc, rr.timer);
-  {
+  // The bvec (Runner.cpp:345-350: insert every point, insert_finalize) depends only on the
+  // lengths, so a host thread builds it while the trainer runs.
+  BVec bv(ds.lengths, 1000);
+  double bvec_ms = 0;
+  std::exception_ptr bvec_err;
+  std::thread bvec_thread([&]() {
+    try {
+      const auto b0 = std::chrono::steady_clock::now();
+      for (uint32_t id = 0; id < ds.size(); id++) bv.insert(id);
+      bv.insert_finalize();
+      bvec_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - b0).count();
+    } catch (...) {
+      bvec_err = std::current_exception();
+    }
+  });
+  try {
     Scope s(rr.timer, "train");
     tr.train();
+  } catch (...) {
+    bvec_thread.join();
+    throw;
   }
+  {
+    Scope s(rr.timer, "bvec.wait");
+    bvec_thread.join();
+  }
+  rr.timer.add("bvec", bvec_ms);
+  if (bvec_err) std::rethrow_exception(bvec_err);
   mc_classifier cls = tr.classifier();
   check(mc_set_classifier(ctx, &cls), "mc_set_classifier");
-  BVec bv(ds.lengths, 1000);
-  {
-    Scope s(rr.timer, "bvec");
-    for (uint32_t id = 0; id < ds.size(); id++) bv.insert(id);
-    bv.insert_finalize();
-  }
   ClusterConfig cc;
   cc.sim = opt.similarity;
   cc.iterations = opt.iterations;
