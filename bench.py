@@ -195,7 +195,7 @@ def main():
     nw_cells = sum(s["nw_cells"] for s in stats)
     nw_rate = nw_cells / (fam_ms["nw"] / 1e3) if fam_ms["nw"] else None
     cpu = None
-    if not a.no_cpu_baseline:
+    if not a.no_cpu_baseline and world == 1:  # the reference is timed on rank 0 at N = 1 only
         cpu = cpu_baseline(fasta, ["--id", a.id], min(a.cpu_sample, a.n), min(16, os.cpu_count() or 1))
     line = {
         "metric": "sequences clustered/sec (+ NW cell-updates/sec) at 1/2/4/8 MI355X",
