@@ -124,6 +124,8 @@ def main():
             comm = TorchShardComm()
 
     import torch
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local)  # sync() below must wait on this rank's GPU, not cuda:0
     sync = torch.cuda.synchronize if torch.cuda.is_available() else (lambda: None)
 
     t0 = time.perf_counter()
