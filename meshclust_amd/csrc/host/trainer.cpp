@@ -221,8 +221,9 @@ std::vector<PairId> Trainer::split() {
         offset[i] /= 2;
       }
       gather();
+      // The new pivots are pivot -/+ offset, both resolved by the speculation above: these are
+      // plain lookups, and waking a thread team for them cost more than the lookups themselves.
       Scope s2(timer_, "train.nw_search.resolve");
-#pragma omp parallel for schedule(dynamic) num_threads(cfg_.threads)
       for (size_t t = 0; t < who.size(); t++) batch[t] = PairId(indices[who[t]], pt_at(who[t], pivot[who[t]]));
     }
   }
