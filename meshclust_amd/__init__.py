@@ -105,6 +105,9 @@ def host_lib():
         lib.mcl_parse.argtypes = [C.POINTER(C.c_char_p), C.c_int, C.c_int, C.c_char_p, C.c_int]
         lib.mcl_num_seqs.restype = C.c_uint64
         lib.mcl_num_seqs.argtypes = [C.c_void_p]
+        lib.mcl_view.argtypes = [C.c_void_p] + [C.POINTER(C.c_void_p)] * 4
+        lib.mcl_header.restype = C.c_char_p
+        lib.mcl_header.argtypes = [C.c_void_p, C.c_uint64]
         lib.mcl_free.argtypes = [C.c_void_p]
         lib.mcl_run.restype = C.c_int
         lib.mcl_run.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_char_p), C.c_int, C.c_char_p,
@@ -263,6 +266,27 @@ class Dataset:
             raise MCError("parse failed: " + err.value.decode())
         self.n = self.lib.mcl_num_seqs(self.h)
 
+    def records(self):
+        """[(header, codes uint8, [[start, end], ...])] as parsed (ChromListMaker +
+        Chromosome::help + ChromosomeOneDigit encoding)."""
+        ptr = [C.c_void_p() for _ in range(4)]
+        self.lib.mcl_view(self.h, *[C.byref(p) for p in ptr])
+        n = self.n
+
+        def arr(p, ct, count):
+            return np.ctypeslib.as_array(C.cast(p, C.POINTER(ct)), shape=(count,)) if count else np.zeros(0)
+
+        seq_off = arr(ptr[1], C.c_uint64, n + 1).copy()
+        seg_off = arr(ptr[3], C.c_uint64, n + 1).copy()
+        codes = arr(ptr[0], C.c_uint8, int(seq_off[-1])).copy()
+        seg = arr(ptr[2], C.c_int32, 2 * int(seg_off[-1])).copy()
+        out = []
+        for i in range(n):
+            s = seg[2 * int(seg_off[i]):2 * int(seg_off[i + 1])]
+            out.append((self.lib.mcl_header(self.h, i).decode(), codes[int(seq_off[i]):int(seq_off[i + 1])],
+                        [[int(s[j]), int(s[j + 1])] for j in range(0, len(s), 2)]))
+        return out
+
     def run(self, engine, args=(), upload=True, clstr=None, comm=None):
         """Run the full pipeline (reference options in ``args``); returns the stats dict.
         ``comm`` (meshclust_amd.dist.TorchShardComm) shares the clustering over its ranks."""
@@ -278,7 +302,7 @@ class Dataset:
             rc = self.lib.mcl_run(self.h, engine.ctx, len(argv), arr, 1 if upload else 0,
                                   clstr.encode() if clstr else None, buf, len(buf))
         st = json.loads(buf.value.decode() or "{}")
-        if rc != 0:
+        if rc != 0 or "error" in st:  # incl. the reference's exit(0) stops (no partition)
             raise MCError("mcl_run failed (%d): %s" % (rc, st))
         return st
 

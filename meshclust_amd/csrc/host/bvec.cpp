@@ -121,7 +121,7 @@ void BVec::insert(uint32_t id) {
   data_.at(min_sizes[min_sizes.size() / 2]).push_back(id);
 }
 
-void BVec::insert_finalize() {
+void BVec::insert_finalize(int threads) {
   // std::sort of each bin by length (bvec.cpp's insert_finalize): the same permutation from
   // LazyIntroSort::sort_words on (length << 32 | id) words, bins and subranges as tasks
   bool wide = false;
@@ -130,7 +130,7 @@ void BVec::insert_finalize() {
     for (auto &bin : data_)
       std::sort(bin.begin(), bin.end(), [&](uint32_t a, uint32_t b) { return len_[a] < len_[b]; });
   } else {
-#pragma omp parallel
+#pragma omp parallel num_threads(threads > 0 ? threads : 1)
 #pragma omp single
     for (auto &bin : data_) {
       if (bin.size() < 2) continue;

@@ -22,7 +22,7 @@ class BVec {
  public:
   BVec(const std::vector<uint64_t> &lengths_by_id, uint64_t bin_size = 1000);  // bvec.cpp:9-24
   void insert(uint32_t id);                                                   // bvec.cpp:151-177
-  void insert_finalize();                                                     // bvec.cpp:208-218
+  void insert_finalize(int threads = 1);                                                 // bvec.cpp:208-218
   uint32_t pop();                                                             // bvec.cpp:26-37
   std::pair<BIdx, BIdx> get_range(uint64_t begin_len, uint64_t end_len) const;  // bvec.cpp:245-278
   void erase(size_t r, size_t c);                                             // bvec.cpp:280-284

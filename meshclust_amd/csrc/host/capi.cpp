@@ -21,11 +21,51 @@ void *mcl_parse(const char *const *files, int nfiles, int threads, char *err, in
 }
 
 uint64_t mcl_num_seqs(void *ds) { return ((mc::Dataset *)ds)->size(); }
+
+// Read-only view of a parsed dataset (what the reference's Chromosome objects hold after
+// ChromListMaker::makeChromOneDigitList): the concatenated one-digit codes with per-record
+// offsets, the [start, end] segment pairs with per-record pair offsets.  Pointers stay valid
+// until mcl_free.  Used by the parser parity tests.
+void mcl_view(void *dsv, const uint8_t **codes, const uint64_t **seq_off, const int32_t **seg,
+              const uint64_t **seg_off) {
+  auto *ds = (mc::Dataset *)dsv;
+  *codes = ds->codes.data();
+  *seq_off = ds->seq_off.data();
+  *seg = ds->seg.data();
+  *seg_off = ds->seg_off.data();
+}
+const char *mcl_header(void *ds, uint64_t i) { return ((mc::Dataset *)ds)->headers.at(i).c_str(); }
 void mcl_free(void *ds) { delete (mc::Dataset *)ds; }
+
+// Error text as a JSON string literal body (quotes, backslashes and control bytes escaped).
+static std::string json_escape(const char *m) {
+  std::string o;
+  for (const char *c = m; *c; c++) {
+    const unsigned char u = (unsigned char)*c;
+    if (u == '"' || u == '\\') {
+      o += '\\';
+      o += (char)u;
+    } else if (u < 0x20) {
+      char b[8];
+      snprintf(b, sizeof b, "\\u%04x", u);
+      o += b;
+    } else {
+      o += (char)u;
+    }
+  }
+  return o;
+}
+
+static void put_error(char *stats, int cap, const char *what, int code) {
+  if (stats && cap > 0) snprintf(stats, cap, "{\"error\": \"%s\", \"exit_code\": %d}", json_escape(what).c_str(), code);
+}
 
 // argv: reference-style options without input files (e.g. {"prog","--id","0.90"}).
 // upload != 0 re-uploads the sequences.  Writes the .clstr if clstr_path is non-NULL and
-// the JSON run summary into stats (cap bytes).  Returns 0, or the driver's exit code.
+// the JSON run summary into stats (cap bytes).  Returns 0, or the driver's exit code; an
+// error never ends the calling process.  The reference's exit(0) stops ("Identity value does
+// not match sampled data", Trainer.cpp:306-315) return 0 with {"error": ..., "exit_code": 0}
+// in stats and no partition, so a caller must check for "error" (Dataset.run raises).
 static int run_common(void *dsv, mc_ctx *ctx, int argc, char **argv, int upload, const char *clstr_path, char *stats,
                       int cap, const mc::ShardComm *comm) {
   auto *ds = (mc::Dataset *)dsv;
@@ -38,10 +78,10 @@ static int run_common(void *dsv, mc_ctx *ctx, int argc, char **argv, int upload,
     if (stats && cap > 0) snprintf(stats, cap, "%s", js.c_str());
     return 0;
   } catch (const mc::Error &e) {
-    if (stats && cap > 0) snprintf(stats, cap, "{\"error\": \"%s\"}", e.what());
-    return e.code ? e.code : 0;
+    put_error(stats, cap, e.what(), e.code);
+    return e.code;
   } catch (const std::exception &e) {
-    if (stats && cap > 0) snprintf(stats, cap, "{\"error\": \"%s\"}", e.what());
+    put_error(stats, cap, e.what(), 1);
     return 1;
   }
 }

@@ -228,9 +228,16 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
       timer.add("accumulate.dev_wait", st[3] / 1000.0);
       timer.add("accumulate.dev_collect", st[4] / 1000.0);
       done = true;
+      stats.accum_path = "device";
     } else if (rc != MC_ERR_UNSUPPORTED) {
       check(rc, "mc_accumulate");
+    } else {
+      // both loops are GPU paths and give identical partitions; say which one ran
+      stats.accum_path = std::string("steps (") + mc_last_error() + ")";
+      if (cfg.verbose) fprintf(stderr, "accumulation: host-driven get_close steps: %s\n", mc_last_error());
     }
+  } else {
+    stats.accum_path = memo ? "steps (alignment mode)" : "steps (MC_ACCUM_STEPS)";
   }
   if (!done) {
     Scope s(timer, "accumulate");

@@ -45,6 +45,9 @@ struct ClusterStats {
   uint64_t merge_evals = 0;
   uint64_t nw_pairs = 0, nw_cells = 0;  // training alignments
   uint64_t align_nw_pairs = 0, align_nw_cells = 0;  // alignment mode: classifier alignments
+  // which accumulation loop ran: "device" (mc_accumulate, one persistent kernel) or "steps"
+  // (host-driven mc_scan per get_close step) with the reason
+  std::string accum_path;
 };
 
 // Runs accumulation + `iterations` rounds of mean-shift update and merge.

@@ -63,7 +63,8 @@ void process_record(std::string &base, std::vector<int32_t> &out) {
     }
   }
   // mergeSegments (Chromosome.cpp:190-226); segment->at(0) throws on an empty list.
-  if (seg.empty()) throw Error("vector::_M_range_check: sequence has no non-N segment", 1);
+  // (a 1-base or all-N record has no closed run)
+  if (seg.empty()) throw Error("vector::_M_range_check: __n (which is 0) >= this->size() (which is 0)", 1);
   std::vector<int32_t> merged;
   int s = seg[0], e = seg[1];
   for (size_t i = 2; i < seg.size(); i += 2) {

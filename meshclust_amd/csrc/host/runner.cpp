@@ -30,6 +30,14 @@ static void usage(const char *prog) {
   printf("MI355X-native MeShClust (meshclust_amd, C-ABI v%d)\n", MC_ABI_VERSION);
 }
 
+// Bad options end the reference with a message (Runner.cpp:150-263: usage on stdout or a
+// message on stderr, then exit).  Here they throw OptionError, so a library caller (capi.cpp)
+// gets an error code instead of losing its process; meshclust_main prints the same text.
+struct OptionError : Error {
+  bool usage;  // print the usage text (stdout) instead of the message (stderr)
+  OptionError(const std::string &m, int c, bool u) : Error(m, c), usage(u) {}
+};
+
 Options parse_options(int argc, char **argv, bool require_files) {
   Options o;
   for (int i = 1; i < argc; i++) {
@@ -37,22 +45,14 @@ Options parse_options(int argc, char **argv, bool require_files) {
     auto need_long = [&](long lo, const char *msg) -> long {
       errno = 0;
       long v = strtol(argv[i + 1], nullptr, 10);
-      if (errno) {
-        perror(argv[i + 1]);
-        exit(EXIT_FAILURE);
-      } else if (v < lo) {
-        fprintf(stderr, "%s\n", msg);
-        exit(EXIT_FAILURE);
-      }
+      if (errno) throw OptionError(std::string(argv[i + 1]) + ": " + strerror(errno), EXIT_FAILURE, false);
+      if (v < lo) throw OptionError(msg, EXIT_FAILURE, false);
       return v;
     };
     if (arg == "--id" && i + 1 < argc) {
       char *end = nullptr;
       double v = strtod(argv[i + 1], &end);
-      if (end == argv[i + 1] || v <= 0 || v >= 1) {
-        fprintf(stderr, "Similarity must be between 0 and 1\n");
-        exit(EXIT_FAILURE);
-      }
+      if (end == argv[i + 1] || v <= 0 || v >= 1) throw OptionError("Similarity must be between 0 and 1", EXIT_FAILURE, false);
       o.similarity = v;
       i++;
     } else if ((arg == "-k" || arg == "--kmer") && i + 1 < argc) {
@@ -70,10 +70,7 @@ Options parse_options(int argc, char **argv, bool require_files) {
       i++;
     } else if ((arg == "-t" || arg == "--threads") && i + 1 < argc) {
       int t = atoi(argv[i + 1]);
-      if (t <= 0) {
-        fprintf(stderr, "Number of threads must be greater than 0.\n");
-        exit(1);
-      }
+      if (t <= 0) throw OptionError("Number of threads must be greater than 0.", 1, false);
       o.threads = t;
       i++;
     } else if ((arg == "-d" || arg == "--delta") && i + 1 < argc) {
@@ -90,18 +87,11 @@ Options parse_options(int argc, char **argv, bool require_files) {
       o.quiet = true;
     } else {
       struct stat st;
-      if (stat(argv[i], &st) == 0 && S_ISREG(st.st_mode)) {
-        o.files.push_back(argv[i]);
-      } else {
-        usage(argv[0]);
-        exit(EXIT_FAILURE);
-      }
+      if (stat(argv[i], &st) == 0 && S_ISREG(st.st_mode)) o.files.push_back(argv[i]);
+      else throw OptionError(std::string("unknown option or missing file: ") + argv[i], EXIT_FAILURE, true);
     }
   }
-  if (o.files.empty() && require_files) {
-    usage(argv[0]);
-    exit(EXIT_FAILURE);
-  }
+  if (o.files.empty() && require_files) throw OptionError("no input files", EXIT_FAILURE, true);
   std::sort(o.files.begin(), o.files.end(), [](const std::string &a, const std::string &b) {
     char *as = strdup(a.c_str()), *bs = strdup(b.c_str());
     bool r = std::string(basename(as)) < std::string(basename(bs));
@@ -173,7 +163,8 @@ RunResult run_pipeline(const Dataset &ds, mc_ctx *ctx, Options opt, bool upload,
   tc.verbose = verbose;
   Trainer tr(ds, ctx, tc, rr.timer);
   // The bvec (Runner.cpp:345-350: insert every point, insert_finalize) depends only on the
-  // lengths, so a host thread builds it while the trainer runs.
+  // lengths, so a host thread builds it while the trainer runs, with a quarter of the
+  // cores (the trainer's teams keep the rest); its time overlaps "train".
   BVec bv(ds.lengths, 1000);
   double bvec_ms = 0;
   std::exception_ptr bvec_err;
@@ -181,7 +172,7 @@ RunResult run_pipeline(const Dataset &ds, mc_ctx *ctx, Options opt, bool upload,
     try {
       const auto b0 = std::chrono::steady_clock::now();
       for (uint32_t id = 0; id < ds.size(); id++) bv.insert(id);
-      bv.insert_finalize();
+      bv.insert_finalize(std::max(1, threads / 4));
       bvec_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - b0).count();
     } catch (...) {
       bvec_err = std::current_exception();
@@ -198,7 +189,7 @@ RunResult run_pipeline(const Dataset &ds, mc_ctx *ctx, Options opt, bool upload,
     Scope s(rr.timer, "bvec.wait");
     bvec_thread.join();
   }
-  rr.timer.add("bvec", bvec_ms);
+  rr.timer.add("bvec.overlapped", bvec_ms);
   if (bvec_err) std::rethrow_exception(bvec_err);
   mc_classifier cls = tr.classifier();
   check(mc_set_classifier(ctx, &cls), "mc_set_classifier");
@@ -231,6 +222,7 @@ std::string stats_json(const RunResult &rr, double parse_ms, double write_ms) {
            (unsigned long long)rr.stats.nw_pairs, (unsigned long long)rr.stats.nw_cells,
            (unsigned long long)rr.stats.align_nw_pairs, (unsigned long long)rr.stats.align_nw_cells);
   o += b;
+  o += ", \"accum_path\": \"" + rr.stats.accum_path + "\"";
   o += ", \"phases_ms\": {";
   for (size_t i = 0; i < rr.timer.order.size(); i++) {
     snprintf(b, sizeof b, "%s\"%s\": %.3f", i ? ", " : "", rr.timer.order[i].c_str(), rr.timer.ms.at(rr.timer.order[i]));
@@ -248,7 +240,14 @@ static void write_stats(const std::string &path, const RunResult &rr, double par
 }
 
 int meshclust_main(int argc, char **argv) {
-  Options opt = parse_options(argc, argv);
+  Options opt;
+  try {
+    opt = parse_options(argc, argv);
+  } catch (const OptionError &e) {
+    if (e.usage) usage(argv[0]);
+    else fprintf(stderr, "%s\n", e.what());
+    return e.code;
+  }
   int threads = opt.threads;
 #ifdef _OPENMP
   if (threads > 0) omp_set_num_threads(threads);

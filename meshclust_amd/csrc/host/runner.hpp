@@ -29,7 +29,8 @@ struct Options {
   std::string stats_json;  // per-phase timings + work counts
 };
 
-// Parses argv exactly like the reference; exits with its messages on bad input.
+// Parses argv like the reference; bad input throws mc::Error (OptionError in runner.cpp)
+// with the reference's message and exit code.
 Options parse_options(int argc, char **argv, bool require_files = true);
 
 struct RunResult {

@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <exception>
 #include <set>
 #include <thread>
 
@@ -191,8 +192,18 @@ std::vector<PairId> Trainer::split() {
       // sampler's positions around the final pivot: the lazy sorts' partitions are then ready
       // when the identities come back.  Each LazyIntroSort is touched by one host thread only.
       std::vector<double> al;
-      std::thread gpu([&]() { nw_batch(batch, al); });
-      {
+      // An error of the GPU thread (mc::Error from check()) must not escape the std::thread
+      // (std::terminate would end the host process): it is carried out and rethrown here.
+      std::exception_ptr gpu_err;
+      std::thread gpu([&]() {
+        try {
+          nw_batch(batch, al);
+        } catch (...) {
+          gpu_err = std::current_exception();
+        }
+      });
+      std::exception_ptr spec_err;
+      try {
         Scope s2(timer_, "train.nw_search.speculate");  // one core left to the thread driving the GPU
 #pragma omp parallel for schedule(dynamic) num_threads(std::max(1, cfg_.threads - 1))
         for (size_t t = 0; t < who.size(); t++) {
@@ -207,11 +218,15 @@ std::vector<PairId> Trainer::split() {
           for (size_t q : pos)
             if (q < sorted[i].size()) pt_at(i, q);
         }
+      } catch (...) {
+        spec_err = std::current_exception();
       }
       {
         Scope s3(timer_, "train.nw_search.align");
         gpu.join();
       }
+      if (gpu_err) std::rethrow_exception(gpu_err);
+      if (spec_err) std::rethrow_exception(spec_err);
       for (size_t t = 0; t < who.size(); t++) {
         size_t i = who[t];
         double algn = al[t];

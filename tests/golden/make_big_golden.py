@@ -1,0 +1,118 @@
+"""Reference partitions at the BASELINE.json sizes (config B 100k, config D 1M).
+
+Runs ONLY in the build container: the reference (oracle/_ref/meshclust, compiled from the
+read-only sources by oracle/Makefile) clusters the synthetic input that meshclust_amd.synth
+regenerates deterministically, and the canonical partition is stored compactly:
+
+  cfg_<name>.npz   n, clusters, centres (sorted centre read ids), digest (SHA-256 of the
+                   canonical partition, see canonical_digest), and for inputs up to
+                   200k reads centre_of[i] = read id of the centre of read i's cluster.
+
+Partitions and centres of the reference are deterministic across thread counts (SURVEY.md
+§5; member and cluster order are not, and are not compared), so the reference runs with all
+cores.  Read ids come from the synthetic headers (">read{i} template_{t}").
+
+Usage: python tests/golden/make_big_golden.py NAME [--threads T]      NAME in BIG
+"""
+import argparse
+import hashlib
+import json
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+from meshclust_amd import synth  # noqa: E402
+
+REF = os.path.join(ROOT, "oracle", "_ref", "meshclust")
+
+# name -> (synth.generate args (n, L, T, mut, seed), flags): SURVEY.md §8(d)
+BIG = {
+    "B100k": ((100000, 1000, 1000, 0.03, 41), ["--id", "0.90"]),
+    "D1M": ((1000000, 1000, 10000, 0.03, 51), ["--id", "0.90"]),
+}
+
+
+def read_id(header):
+    """'>read123 template_4' -> 123"""
+    return int(header[1:].split(" ", 1)[0][4:])
+
+
+def clusters_of(clstr_path):
+    """[(centre id, [member ids])] from a .clstr (ClusterFactory.cpp:495-520 format)."""
+    out, cur = [], None
+    with open(clstr_path) as f:
+        for line in f:
+            if line.startswith(">Cluster"):
+                cur = [None, []]
+                out.append(cur)
+                continue
+            if not line.strip():
+                continue
+            rest = line.split("\t", 1)[1].split("nt, ", 1)[1]
+            hdr = rest.rsplit("... ", 1)[0]
+            i = read_id(hdr)
+            cur[1].append(i)
+            if line.rstrip().endswith("*"):
+                cur[0] = i
+    return out
+
+
+def canonical_digest(clusters):
+    """SHA-256 over the clusters sorted by centre id, each as uint32 [centre, size, sorted
+    member ids...]: equal digests <=> equal partitions with equal centres."""
+    h = hashlib.sha256()
+    for c, mem in sorted(clusters, key=lambda x: x[0]):
+        h.update(np.array([c, len(mem)] + sorted(mem), dtype=np.uint32).tobytes())
+    return h.hexdigest()
+
+
+def summary(clusters, n):
+    centres = np.array(sorted(c for c, _ in clusters), dtype=np.uint32)
+    out = {"n": n, "clusters": len(clusters), "centres": centres, "digest": canonical_digest(clusters)}
+    if n <= 200000:
+        centre_of = np.full(n, 0xffffffff, dtype=np.uint32)
+        for c, mem in clusters:
+            centre_of[np.array(mem, dtype=np.int64)] = c
+        out["centre_of"] = centre_of
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("name", choices=sorted(BIG))
+    ap.add_argument("--threads", type=int, default=os.cpu_count())
+    ap.add_argument("--workdir", default="/tmp/mc_big")
+    a = ap.parse_args()
+    gen, flags = BIG[a.name]
+    os.makedirs(a.workdir, exist_ok=True)
+    fa = os.path.join(a.workdir, a.name + ".fa")
+    if not os.path.exists(fa):
+        synth.generate(fa + ".tmp", *gen)
+        os.replace(fa + ".tmp", fa)
+    out = os.path.join(a.workdir, a.name + ".clstr")
+    t0 = time.time()
+    subprocess.run([REF, fa] + flags + ["--threads", str(a.threads), "--output", out], check=True,
+                   stdout=subprocess.DEVNULL)
+    wall = time.time() - t0
+    s = summary(clusters_of(out), gen[0])
+    np.savez_compressed(os.path.join(HERE, "cfg_%s.npz" % a.name), n=s["n"], clusters=s["clusters"],
+                        centres=s["centres"], digest=s["digest"],
+                        **({"centre_of": s["centre_of"]} if "centre_of" in s else {}))
+    man_path = os.path.join(HERE, "manifest.json")
+    man = json.load(open(man_path))
+    man.setdefault("big", {})[a.name] = {"generator": list(gen), "flags": flags, "threads": a.threads,
+                                         "reference_wall_s": round(wall, 1), "clusters": s["clusters"],
+                                         "digest": s["digest"]}
+    with open(man_path, "w") as f:
+        json.dump(man, f, indent=1, sort_keys=True)
+    print(json.dumps(man["big"][a.name]))
+
+
+if __name__ == "__main__":
+    main()

@@ -48,6 +48,8 @@ E2E = {
     # related templates (families): ambiguous pairs, many merges
     "fam2k": (("family", 2000, 50, 10, 0.10, 0.03, 25), ["--id", "0.90"]),
     "fam2k_id85": (("family", 2000, 40, 8, 0.12, 0.04, 26), ["--id", "0.85", "--delta", "8"]),
+    # lower-case, IUPAC, N runs, records < 20 bp (the parser's edge cases end to end)
+    "noisy2k": (("noisy", 2000, 40, 0.04, 27), ["--id", "0.90"]),
     # alignment mode (Feature::align classifier; --align, or --id < 0.6 switches it on)
     "al300": ((300, 500, 10, 0.03, 7), ["--align", "--id", "0.9"]),
     "al_fam400_id55": (("family", 400, 16, 4, 0.25, 0.05, 31), ["--id", "0.55"]),
@@ -117,7 +119,40 @@ def family_reads(n, n_templates, n_families, tmut, mut, seed, length=1000):
         yield b"read%d family_%d template_%d" % (i, t % n_families, t), alpha[mutate(temps[t], mut)].tobytes()
 
 
+def noisy_reads(n, n_templates, mut, seed, length=1000):
+    """Reads with what real FASTA carries: lower-case stretches, IUPAC ambiguity letters,
+    short N runs (merged into the segment: N -> C) and long N runs (segment splits, 'N' kept),
+    leading/trailing N, and a few records shorter than 20 bp (no segment)."""
+    rng = np.random.default_rng(seed)
+    base_reads = list(synth.reads(n, length, n_templates, mut, seed))
+    iupac = np.frombuffer(b"RYMKSWHBVDX", np.uint8)
+    for i, (hdr, seq) in enumerate(base_reads):
+        s = bytearray(seq)
+        L = len(s)
+        if i % 7 == 0:  # lower-case stretch
+            a = int(rng.integers(0, L - 50))
+            s[a:a + 50] = bytes(s[a:a + 50]).lower()
+        if i % 5 == 0:  # IUPAC letters
+            for q in rng.integers(0, L, size=3):
+                s[int(q)] = int(iupac[int(rng.integers(0, len(iupac)))])
+        if i % 11 == 0:  # short N run (< 10: merged)
+            a = int(rng.integers(30, L - 40))
+            s[a:a + int(rng.integers(1, 9))] = b"N" * len(s[a:a + int(rng.integers(1, 9))])
+        if i % 13 == 0:  # long N run (>= 10: split, 'N' kept outside segments)
+            a = int(rng.integers(30, L - 60))
+            s[a:a + 25] = b"N" * 25
+        if i % 17 == 0:  # leading / trailing N
+            s = bytearray(b"NNNN") + s + bytearray(b"nn")
+        if i % 97 == 0:  # shorter than 20: no segment, pseudocount-only histogram
+            s = s[:15]
+        yield hdr, bytes(s)
+
+
 def make_input(spec, path):
+    if spec[0] == "noisy":
+        _, n, t, mut, seed = spec
+        synth.write_fasta(path, noisy_reads(n, t, mut, seed))
+        return sha256(path)
     if spec[0] == "family":
         _, n, t, f, tmut, mut, seed = spec
         synth.write_fasta(path, family_reads(n, t, f, tmut, mut, seed))
@@ -141,8 +176,27 @@ def run_probe(*args):
     return text
 
 
-def golden_parse():
-    text = run_probe("parse", os.path.join(HERE, "edge.fa"))
+def long_fasta():
+    """One 2.5 Mb record with a run of N (a 2.3 Mb segment: two 1 Mb fragments) and a short one."""
+    rng = np.random.default_rng(0)
+    seq = bytearray(np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, 2_500_000)].tobytes())
+    seq[2_300_000:2_300_050] = b"N" * 50
+    return b">long\n" + bytes(seq) + b"\n>short\n" + bytes(seq[:100]) + b"\n"
+
+
+def crlf_variant(src, dst):
+    """edge.fa with mixed line ends: "\r\n", a lone "\r" and "\n" in turn (safe_getline,
+    ChromListMaker.cpp:23-47), plus a blank "\r\n" line."""
+    with open(src, "rb") as f:
+        lines = f.read().split(b"\n")
+    ends = (b"\r\n", b"\r", b"\n")
+    out = b"".join(l + ends[i % 3] for i, l in enumerate(lines[:-1]) if l) + b"\r\n"
+    with open(dst, "wb") as f:
+        f.write(out)
+
+
+def parse_records(fa):
+    text = run_probe("parse", fa)
     recs = []
     cur = None
     for line in text.splitlines():
@@ -160,8 +214,26 @@ def golden_parse():
             cur["segments"] = []
         elif tag == "D":
             cur["data_hex"] = rest.strip()
+    return recs
+
+
+def golden_parse():
+    recs = parse_records(os.path.join(HERE, "edge.fa"))
     with open(os.path.join(HERE, "edge_parse.json"), "w") as f:
         json.dump(recs, f, indent=1)
+    # a 2.5 Mb record (makeSegmentList's 1 Mb fragments): segments and a digest of the codes
+    with tempfile.TemporaryDirectory() as td:
+        fa = os.path.join(td, "long.fa")
+        with open(fa, "wb") as f:
+            f.write(long_fasta())
+        long_recs = parse_records(fa)
+    for r in long_recs:
+        r["codes_sha256"] = hashlib.sha256(bytes.fromhex(r.pop("data_hex"))).hexdigest()
+    with open(os.path.join(HERE, "long_parse.json"), "w") as f:
+        json.dump(long_recs, f, indent=1)
+    crlf_variant(os.path.join(HERE, "edge.fa"), os.path.join(HERE, "edge_crlf.fa"))
+    with open(os.path.join(HERE, "edge_crlf_parse.json"), "w") as f:
+        json.dump(parse_records(os.path.join(HERE, "edge_crlf.fa")), f, indent=1)
     hist = {}
     for k in (1, 3, 4, 6):
         text = run_probe("hist", os.path.join(HERE, "edge.fa"), k)
@@ -174,6 +246,30 @@ def golden_parse():
         hist["k%d" % k] = np.array(rows, dtype=np.uint64)
         hist["mag%d" % k] = np.array(mags, dtype=np.uint64)
     np.savez_compressed(os.path.join(HERE, "edge_hist.npz"), **hist)
+
+
+# inputs the reference rejects while reading (Chromosome.cpp:162-258, ChromosomeOneDigit.cpp:95-144)
+PARSE_ERRORS = {
+    "invalid_nucleotide": b">a\nACGTACGTACGTACGTACGTACGTAC\n>b\nACGTQACGTACGTACGTACGTACGTACGT\n",
+    "one_base": b">a\nACGTACGTACGTACGTACGTACGTAC\n>b\nA\n",
+    "all_n": b">a\nACGTACGTACGTACGTACGTACGTAC\n>b\nNNNNNNNN\n",
+}
+
+
+def golden_parse_errors(tmp):
+    """The reference's exit status and the message of what it throws, per error input."""
+    out = {}
+    for name, data in PARSE_ERRORS.items():
+        fa = os.path.join(tmp, name + ".fa")
+        with open(fa, "wb") as f:
+            f.write(data)
+        r = subprocess.run([REF, fa, "--id", "0.9", "--kmer", "3", "--threads", "1", "--output",
+                            os.path.join(tmp, name + ".clstr")], capture_output=True, text=True)
+        msg = [l for l in (r.stdout + r.stderr).splitlines() if "Invalid nucleotide" in l or "what():" in l]
+        out[name] = {"fasta": data.decode(), "returncode": r.returncode,
+                     "message": msg[-1].split("what():")[-1].strip() if msg else None}
+    with open(os.path.join(HERE, "parse_errors.json"), "w") as f:
+        json.dump(out, f, indent=1, sort_keys=True)
 
 
 def nw_pairs():
@@ -315,6 +411,7 @@ def main():
     with tempfile.TemporaryDirectory() as tmp:
         if want is None or "parse" in want:
             golden_parse()
+            golden_parse_errors(tmp)
         if want is None or "nw" in want:
             nw_pairs()
         if want is None or "train" in want:

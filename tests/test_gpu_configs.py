@@ -1,0 +1,96 @@
+"""GPU parity at the BASELINE.json sizes: bin/meshclust on MI355X against the reference's own
+partitions of the same synthetic inputs.
+
+* config E (viral shape: 7 families x 13 genomes, 8-12 kb, k = 6, --id 0.80) against the
+  reference's .clstr (tests/golden/cfg_E91.clstr.gz, canonical partition + centres);
+* config B (100k x 1 kb, --id 0.90) and config D (1M x 1 kb, --id 0.90) against the
+  reference's canonical partition digests (tests/golden/cfg_B100k.npz, cfg_D1M.npz, written by
+  make_big_golden.py from oracle/_ref/meshclust with all cores; partitions and centres of the
+  reference do not depend on its thread count).
+
+Reference loop: ClusterFactory.cpp:637-761 (accumulate, MS), Trainer.cpp:34-157, 334-365.
+The inputs are regenerated here by meshclust_amd.synth (deterministic; SHA-256 checked).
+"""
+import hashlib
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import clstr
+import fixtures
+import meshclust_amd as M
+from meshclust_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+sys.path.insert(0, fixtures.GOLDEN)
+import make_big_golden as BG  # noqa: E402
+
+
+def _cache_dir():
+    d = os.environ.get("MC_TEST_CACHE", os.path.join("/tmp", "mc_test_cache_%d" % os.getuid()))
+    os.makedirs(d, exist_ok=True)
+    return d
+
+
+def _run(fa, flags, out, timeout):
+    st = out + ".stats.json"
+    r = subprocess.run([M.BIN, fa] + flags + ["--output", out, "--stats-json", st, "--quiet", "--threads", "16"],
+                       capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return json.load(open(st))
+
+
+@pytest.fixture(scope="module")
+def product():
+    M.build()
+    return M.BIN
+
+
+def test_config_E91_partition_equals_reference(product, tmp_path):
+    fa = str(tmp_path / "E91.fa")
+    synth.write_fasta(fa, synth.families(7, 13, 8000, 12000, 0.05, 0.15, 61))
+    out = str(tmp_path / "E91.clstr")
+    st = _run(fa, ["--id", "0.80"], out, 300)
+    assert st["k"] == 6 and st["n"] == 91
+    assert clstr.canonical(out) == clstr.canonical(fixtures.golden("cfg_E91.clstr.gz"))
+
+
+def _big(name, product, timeout):
+    gen, flags = BG.BIG[name]
+    gpath = fixtures.golden("cfg_%s.npz" % name)
+    if not os.path.exists(gpath):
+        pytest.skip("reference partition for %s not generated" % name)
+    g = np.load(gpath)
+    fa = os.path.join(_cache_dir(), "%s.fa" % name)
+    if not os.path.exists(fa):
+        synth.generate(fa + ".tmp", *gen)
+        os.replace(fa + ".tmp", fa)
+    out = fa[:-3] + ".clstr"
+    st = _run(fa, flags, out, timeout)
+    got = BG.clusters_of(out)
+    assert sorted(c for c, _ in got) == [int(x) for x in g["centres"]], "centre sets differ"
+    if "centre_of" in g:
+        mine = np.full(int(g["n"]), 0xffffffff, np.uint32)
+        for c, mem in got:
+            mine[np.array(mem, np.int64)] = c
+        diff = int((mine != g["centre_of"]).sum())
+        assert diff == 0, "%d reads in a different cluster" % diff
+    assert BG.canonical_digest(got) == str(g["digest"])
+    assert st["clusters"] == int(g["clusters"])
+    return st
+
+
+def test_config_B100k_partition_equals_reference(product):
+    st = _big("B100k", product, 300)
+    assert st["accum_path"] == "device"
+
+
+@pytest.mark.timeout(1200)
+def test_config_D1M_partition_equals_reference(product):
+    st = _big("D1M", product, 900)
+    print("config D accumulation path:", st["accum_path"])
