@@ -101,7 +101,24 @@ int mc_ctx_destroy(mc_ctx *ctx);
 int mc_load_sequences(mc_ctx *ctx, const uint8_t *codes, const uint64_t *seq_off, uint64_t n,
                       const int32_t *seg, const uint64_t *seg_off);
 
-/* Largest k-mer count of the pseudocount-1 uint64 tables (Runner.cpp:57-67). */
+/*
+ * The same sequences in the form the host parser produces (meshclust_amd/csrc/host/fasta.cpp):
+ * 2-bit codes, 16 bases per 32-bit word (base j of a record at bits 2*(j % 16) of word
+ * pk_off[i] + j / 16; pk_off[i+1] - pk_off[i] = ceil(length_i / 16)), plus the nexc bytes that
+ * are not 0..3 (the 'N' ChromosomeOneDigit leaves outside segments, ChromosomeOneDigit.cpp:
+ * 122-144, or the raw bytes of a record without segments) at ascending global byte positions
+ * exc_pos.  seq_off/seg/seg_off as for mc_load_sequences.  A quarter of the bytes cross PCIe;
+ * the device keeps both the packed form (K1 input) and the expanded bytes (NW input).
+ */
+int mc_load_packed(mc_ctx *ctx, const uint32_t *packed, const uint64_t *pk_off, const uint64_t *seq_off, uint64_t n,
+                   const uint64_t *exc_pos, const uint8_t *exc_val, uint64_t nexc, const int32_t *seg,
+                   const uint64_t *seg_off);
+
+/*
+ * Largest k-mer count of the pseudocount-1 uint64 tables (Runner.cpp:57-67).  The pass also
+ * writes the 8-bit histograms, so when the count fits 8 bits the following
+ * mc_kmer_build(ctx, k, 1) costs nothing (K1 reads the sequences once).  1 <= k <= 12.
+ */
 int mc_kmer_max(mc_ctx *ctx, int k, uint64_t *largest);
 
 /*

@@ -85,7 +85,7 @@ def gpu_lib():
         lib.mc_last_error.restype = C.c_char_p
         lib.mc_ctx_create.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
         lib.mc_ctx_destroy.argtypes = [C.c_void_p]
-        for name in ("mc_load_sequences", "mc_kmer_max", "mc_kmer_build", "mc_get_histograms", "mc_distance_keys",
+        for name in ("mc_load_sequences", "mc_load_packed", "mc_kmer_max", "mc_kmer_build", "mc_get_histograms", "mc_distance_keys",
                      "mc_pair_features", "mc_set_classifier", "mc_classify_pairs", "mc_nw_identity",
                      "mc_nw_identity_raw", "mc_set_order", "mc_kill", "mc_cluster_begin", "mc_scan",
                      "mc_mean_shift", "mc_timers", "mc_classify_values", "mc_mean_shift_select", "mc_accumulate"):
@@ -156,6 +156,35 @@ class Engine:
         self.n = len(seq_off) - 1
         _check(self.lib.mc_load_sequences(self.ctx, _p(codes), _p(seq_off), C.c_uint64(self.n), _p(seg),
                                           _p(seg_off)), "mc_load_sequences")
+
+    def load_packed(self, seqs, segs):
+        """seqs: list of uint8 one-digit arrays; segs: per sequence [[s, e], ...].  Packs them the
+        way the host parser does (2-bit words, records word-aligned, exception bytes) and loads
+        them with mc_load_packed."""
+        lens = [len(x) for x in seqs]
+        seq_off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+        pk_off = np.concatenate([[0], np.cumsum([(l + 15) // 16 for l in lens])]).astype(np.uint64)
+        packed = np.zeros(max(1, int(pk_off[-1])), np.uint32)
+        exc_pos, exc_val = [], []
+        for i, x in enumerate(seqs):
+            x = np.asarray(x, np.uint8)
+            pad = np.zeros((len(x) + 15) // 16 * 16, np.uint32)
+            pad[:len(x)] = x & 3
+            w = (pad.reshape(-1, 16) << (2 * np.arange(16, dtype=np.uint32))).sum(axis=1, dtype=np.uint64)
+            packed[int(pk_off[i]):int(pk_off[i + 1])] = w.astype(np.uint32)
+            bad = np.nonzero(x > 3)[0]
+            exc_pos.extend((int(seq_off[i]) + bad).tolist())
+            exc_val.extend(x[bad].tolist())
+        seg = np.array([v for s in segs for pair in s for v in pair], np.int32)
+        seg_off = np.concatenate([[0], np.cumsum([len(s) for s in segs])]).astype(np.uint64)
+        if seg.size == 0:
+            seg = np.zeros(2, np.int32)
+        ep = np.array(exc_pos, np.uint64)
+        ev = np.array(exc_val, np.uint8)
+        self.n = len(seqs)
+        _check(self.lib.mc_load_packed(self.ctx, _p(packed), _p(pk_off), _p(seq_off), C.c_uint64(self.n),
+                                       _p(ep) if len(ep) else None, _p(ev) if len(ev) else None, C.c_uint64(len(ep)),
+                                       _p(seg), _p(seg_off)), "mc_load_packed")
 
     def kmer_max(self, k):
         out = C.c_uint64()

@@ -165,7 +165,7 @@ int mc_ctx_destroy(mc_ctx *c) {
   if (!c) return MC_OK;
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
-  for (Buf *b : {&c->codes, &c->seq_off, &c->seg, &c->seg_off, &c->hist, &c->mag, &c->sumsq, &c->len, &c->order,
+  for (Buf *b : {&c->codes, &c->seq_off, &c->seg, &c->seg_off, &c->packed, &c->pk_off, &c->impure, &c->hist, &c->mag, &c->sumsq, &c->len, &c->order,
                  &c->alive, &c->members, &c->member_keys, &c->partials, &c->scan_dev, &c->flags_out, &c->s_a, &c->s_b,
                  &c->s_c, &c->s_d, &c->s_e, &c->s_f, &c->s_g, &c->hs, &c->mag_s, &c->sumsq_s, &c->len_s, &c->ticket,
                  &c->msum, &c->ident_s, &c->al_a, &c->al_b, &c->al_out, &c->acc_out})
@@ -180,25 +180,84 @@ int mc_ctx_destroy(mc_ctx *c) {
   return MC_OK;
 }
 
-int mc_load_sequences(mc_ctx *c, const uint8_t *codes, const uint64_t *seq_off, uint64_t n, const int32_t *seg,
-                      const uint64_t *seg_off) {
-  if (!c || !seq_off || !seg_off || (n && !codes)) return MC_ERR_ARG;
+// shared by both loaders: offsets, segments, buffers; the byte and packed forms follow
+static int load_common(mc_ctx *c, const uint64_t *seq_off, uint64_t n, const int32_t *seg, const uint64_t *seg_off,
+                       std::vector<uint64_t> &pk_off) {
   MCG_CHECK(hipSetDevice(c->device));
+  for (uint64_t i = 0; i < n; i++)
+    if (seq_off[i + 1] < seq_off[i] || seg_off[i + 1] < seg_off[i]) {
+      set_error("offsets must be non-decreasing");
+      return MC_ERR_ARG;
+    }
   c->n = n;
+  c->k = 0;
+  c->kmer_spec_k = 0;
   c->h_seq_off.assign(seq_off, seq_off + n + 1);
-  TRY(upload(c->codes, codes, seq_off[n], c->stream));
+  if (pk_off.empty()) {
+    pk_off.resize(n + 1);
+    pk_off[0] = 0;
+    for (uint64_t i = 0; i < n; i++) pk_off[i + 1] = pk_off[i] + (seq_off[i + 1] - seq_off[i] + 15) / 16;
+  }
+  TRY(ensure(c->codes, seq_off[n] + 16));
+  TRY(ensure(c->packed, pk_off[n] * 4 + 16));
+  TRY(ensure(c->impure, n + 16));
+  TRY(upload(c->pk_off, pk_off.data(), n + 1, c->stream));
   TRY(upload(c->seq_off, seq_off, n + 1, c->stream));
   TRY(upload(c->seg, seg, 2 * seg_off[n], c->stream));
   TRY(upload(c->seg_off, seg_off, n + 1, c->stream));
-  MCG_CHECK(hipStreamSynchronize(c->stream));
-  flush_timers(c);
-  c->k = 0;
   return MC_OK;
 }
 
-static int kmer_common(mc_ctx *c, int k, int width, bool build, uint64_t *largest) {
-  if (!c || k < 1 || k > 7) {
-    set_error("k must be in 1..7 (4^k bins held in LDS)");
+int mc_load_sequences(mc_ctx *c, const uint8_t *codes, const uint64_t *seq_off, uint64_t n, const int32_t *seg,
+                      const uint64_t *seg_off) {
+  if (!c || !seq_off || !seg_off || (n && !codes)) return MC_ERR_ARG;
+  std::vector<uint64_t> pk_off;
+  TRY(load_common(c, seq_off, n, seg, seg_off, pk_off));
+  if (seq_off[n]) MCG_CHECK(hipMemcpyAsync(c->codes.p, codes, seq_off[n], hipMemcpyHostToDevice, c->stream));
+  if (n) TRY(launch_pack(c));
+  MCG_CHECK(hipStreamSynchronize(c->stream));
+  flush_timers(c);
+  return MC_OK;
+}
+
+int mc_load_packed(mc_ctx *c, const uint32_t *packed, const uint64_t *pk_off, const uint64_t *seq_off, uint64_t n,
+                   const uint64_t *exc_pos, const uint8_t *exc_val, uint64_t nexc, const int32_t *seg,
+                   const uint64_t *seg_off) {
+  if (!c || !pk_off || !seq_off || !seg_off || (n && !packed) || (nexc && (!exc_pos || !exc_val))) return MC_ERR_ARG;
+  for (uint64_t i = 0; i < n; i++)
+    if (pk_off[i + 1] - pk_off[i] != (seq_off[i + 1] - seq_off[i] + 15) / 16) {
+      set_error("pk_off must give every record ceil(length / 16) words");
+      return MC_ERR_ARG;
+    }
+  // impure sequences: those holding an exception byte (exc_pos ascending)
+  std::vector<uint8_t> imp(n, 0);
+  for (uint64_t q = 0, i = 0; q < nexc; q++) {
+    if (exc_pos[q] >= seq_off[n] || (q && exc_pos[q] <= exc_pos[q - 1])) {
+      set_error("exception positions must be ascending and inside the sequences");
+      return MC_ERR_ARG;
+    }
+    while (seq_off[i + 1] <= exc_pos[q]) i++;
+    imp[i] = 1;
+  }
+  std::vector<uint64_t> pko(pk_off, pk_off + n + 1);
+  TRY(load_common(c, seq_off, n, seg, seg_off, pko));
+  if (pk_off[n]) MCG_CHECK(hipMemcpyAsync(c->packed.p, packed, pk_off[n] * 4, hipMemcpyHostToDevice, c->stream));
+  if (n) MCG_CHECK(hipMemcpyAsync(c->impure.p, imp.data(), n, hipMemcpyHostToDevice, c->stream));
+  if (nexc) {
+    TRY(ensure(c->s_a, nexc * 8 + 16));
+    TRY(ensure(c->s_b, nexc + 16));
+    MCG_CHECK(hipMemcpyAsync(c->s_a.p, exc_pos, nexc * 8, hipMemcpyHostToDevice, c->stream));
+    MCG_CHECK(hipMemcpyAsync(c->s_b.p, exc_val, nexc, hipMemcpyHostToDevice, c->stream));
+  }
+  if (n) TRY(launch_expand(c, nexc, (const uint64_t *)c->s_a.p, (const uint8_t *)c->s_b.p));
+  MCG_CHECK(hipStreamSynchronize(c->stream));
+  flush_timers(c);
+  return MC_OK;
+}
+
+static int kmer_common(mc_ctx *c, int k, int width, bool write, uint64_t *largest) {
+  if (!c || k < 1 || k > 12) {
+    set_error("k must be in 1..12 (dense 4^k-bin histograms)");
     return MC_ERR_ARG;
   }
   if (c->n == 0 || !c->codes.p) {
@@ -210,17 +269,16 @@ static int kmer_common(mc_ctx *c, int k, int width, bool build, uint64_t *larges
   MCG_CHECK(hipMemsetAsync(c->s_f.p, 0, 64, c->stream));
   uint64_t *d_max = (uint64_t *)c->s_f.p;
   int *d_err = (int *)((char *)c->s_f.p + 8);
-  if (build) {
-    c->k = k;
-    c->B = 1 << (2 * k);
-    c->width = width;
-    c->pitch = ((uint64_t)c->B * width + 15) / 16 * 16;
-    TRY(ensure(c->hist, c->n * c->pitch));
-    TRY(ensure(c->mag, c->n * 8));
-    TRY(ensure(c->sumsq, c->n * 8));
-    TRY(ensure(c->len, c->n * 8));
-  }
-  TRY(launch_kmer(c, k, width, build, d_max, d_err));
+  c->k = 0;  // rows are being (re)written
+  c->kmer_spec_k = 0;
+  c->B = 1 << (2 * k);
+  c->width = width;
+  c->pitch = ((uint64_t)c->B * width + 15) / 16 * 16;
+  TRY(ensure(c->hist, c->n * c->pitch));
+  TRY(ensure(c->mag, c->n * 8));
+  TRY(ensure(c->sumsq, c->n * 8));
+  TRY(ensure(c->len, c->n * 8));
+  TRY(launch_kmer(c, k, width, write, d_max, d_err));
   uint64_t h[2] = {0, 0};
   MCG_CHECK(hipMemcpyAsync(h, c->s_f.p, 16, hipMemcpyDeviceToHost, c->stream));
   MCG_CHECK(hipStreamSynchronize(c->stream));
@@ -233,11 +291,25 @@ static int kmer_common(mc_ctx *c, int k, int width, bool build, uint64_t *larges
   return MC_OK;
 }
 
-int mc_kmer_max(mc_ctx *c, int k, uint64_t *largest) { return kmer_common(c, k, 8, false, largest); }
+// The largest-count pass (Runner.cpp:57-67) writes the 8-bit rows as it goes: when the
+// maximum fits 8 bits, mc_kmer_build(k, 1) then has nothing left to do (K1 runs once).
+int mc_kmer_max(mc_ctx *c, int k, uint64_t *largest) {
+  uint64_t mx = 0;
+  TRY(kmer_common(c, k, 1, true, &mx));
+  if (mx <= 0xff) {
+    c->k = k;
+    c->kmer_spec_k = k;
+  }
+  if (largest) *largest = mx;
+  return MC_OK;
+}
 
 int mc_kmer_build(mc_ctx *c, int k, int width) {
-  if (width != 1 && width != 2 && width != 4 && width != 8) return MC_ERR_ARG;
-  return kmer_common(c, k, width, true, nullptr);
+  if (!c || (width != 1 && width != 2 && width != 4 && width != 8)) return MC_ERR_ARG;
+  if (c->kmer_spec_k == k && width == 1 && c->k == k) return MC_OK;  // written by mc_kmer_max
+  TRY(kmer_common(c, k, width, true, nullptr));
+  c->k = k;
+  return MC_OK;
 }
 
 int mc_get_histograms(mc_ctx *c, void *hist, uint64_t *mags) {

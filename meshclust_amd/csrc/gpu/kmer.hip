@@ -1,137 +1,370 @@
-// kmer.hip -- K1: per-sequence k-mer histograms.
+// kmer.hip -- sequence residency and K1, the per-sequence k-mer histograms (SURVEY.md §8(a)
+// a4-a7).
 //
-// Reference: fill_table (src/cluster/src/ClusterFactory.h:40-55) drives
+// Residency.  Every sequence is held twice in HBM: as 2-bit codes (16 bases per 32-bit word,
+// each record starting on a word: K1's input) and as one-digit bytes (the NW input,
+// Point::get_data_str).  The host parser uploads the packed form plus the sparse list of bytes
+// that are not 0..3 (the 'N' encodeNucleotides leaves outside segments) -- a quarter of the
+// bytes over PCIe -- and expand_kernel writes the byte form; mc_load_sequences (bytes) runs
+// the other way through pack_kernel.  A sequence with any byte outside 0..3 is "impure": K1
+// then reads its bytes (where such a byte inside a k-mer must raise the reference's error).
+//
+// K1.  Reference: fill_table (src/cluster/src/ClusterFactory.h:40-55) drives
 // KmerHashTable::wholesaleIncrement (src/nonltr/KmerHashTable.cpp:193-223) over every
 // segment [s, e]: k-mers start at s .. e-k+1, index = sum code[i]*4^(k-1-i) (first base most
 // significant), forward strand only, table initialised to the pseudocount 1.
 //
-// One workgroup per sequence: the 4^k counters live in LDS (k <= 7: <= 64 KiB), each
-// thread hashes a strided subset of k-mer start positions and increments with LDS atomics,
-// then the table is written out as one histogram row of the chosen width together with its
-// magnitude (sum of bins incl. pseudocounts = DivergencePoint::mag) and sum of squares.
-// Pass `build == false` only reduces the largest bin (Runner.cpp:57-67 picks the width).
+// Per-wavefront LDS bins: each wave owns a 4^k u32 table in LDS.  Short sequences: one wave
+// per sequence (no cross-wave traffic at all).  Long sequences (mean length >= 4 kb): the W
+// waves of a workgroup share one sequence and their tables are summed at write-out.  A lane
+// takes 16 consecutive k-mer starts: it loads the three packed words that cover bases
+// [p, p + 16 + k - 1) (the wave's loads are consecutive words: coalesced), funnels them into a
+// 64-bit window and rolls the k-mer index over it.  k >= 8 (4^k u32 > LDS) uses per-wave
+// tables in global scratch with the same code.
+//
+// One pass: the row is written at the width the caller asks for (mc_kmer_max speculates
+// 8 bits) together with its magnitude (sum of bins incl. pseudocounts = DivergencePoint::mag),
+// sum of squares and length, and the row maxima are reduced; the reference's largest-count
+// pass (Runner.cpp:57-67) is that maximum, so a second pass runs only when 8 bits do not hold
+// it.
 #include "mcgpu.hpp"
 
 namespace mcg {
 
 namespace {
 
-constexpr int KT = 256;  // threads per workgroup
+constexpr int KT = 256;       // threads per workgroup
+constexpr int KW = KT / 64;   // waves per workgroup
 
-__device__ __forceinline__ uint64_t block_sum_u64(uint64_t v, uint64_t *red) {
-  for (int o = 32; o >= 1; o >>= 1) {
-    uint32_t lo = __shfl_xor((uint32_t)v, o, 64), hi = __shfl_xor((uint32_t)(v >> 32), o, 64);
-    v += ((uint64_t)hi << 32) | lo;
+// ---------------------------------------------------------------- residency kernels
+// packed word w of sequence s -> 16 bytes of the one-digit string (one lane per word)
+__global__ __launch_bounds__(256) void expand_kernel(const uint32_t *__restrict__ pk, const uint64_t *__restrict__ pk_off,
+                                                     const uint64_t *__restrict__ seq_off, uint64_t n,
+                                                     uint8_t *__restrict__ codes) {
+  const int lane = threadIdx.x & 63;
+  for (uint64_t s = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / 64; s < n;
+       s += (uint64_t)gridDim.x * blockDim.x / 64) {
+    const uint64_t w0 = pk_off[s], w1 = pk_off[s + 1], b0 = seq_off[s], L = seq_off[s + 1] - b0;
+    for (uint64_t w = w0 + lane; w < w1; w += 64) {
+      const uint32_t v = pk[w];
+      const uint64_t j0 = (w - w0) * 16;
+      uint8_t *dst = codes + b0 + j0;
+      const uint64_t m = L - j0 < 16 ? L - j0 : 16;
+      for (uint64_t j = 0; j < m; j++) dst[j] = (uint8_t)((v >> (2 * j)) & 3u);
+    }
   }
-  const int w = threadIdx.x >> 6;
-  __syncthreads();
-  if ((threadIdx.x & 63) == 0) red[w] = v;
-  __syncthreads();
-  uint64_t t = 0;
-  for (int i = 0; i < KT / 64; i++) t += red[i];
-  return t;
 }
 
-__device__ __forceinline__ uint64_t block_max_u64(uint64_t v, uint64_t *red) {
+__global__ __launch_bounds__(256) void exceptions_kernel(const uint64_t *__restrict__ pos, const uint8_t *__restrict__ val,
+                                                         uint64_t m, uint8_t *__restrict__ codes) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x)
+    codes[pos[i]] = val[i];
+}
+
+// one-digit bytes -> packed words + impure flag (one wave per sequence)
+__global__ __launch_bounds__(256) void pack_kernel(const uint8_t *__restrict__ codes, const uint64_t *__restrict__ seq_off,
+                                                   const uint64_t *__restrict__ pk_off, uint64_t n,
+                                                   uint32_t *__restrict__ pk, uint8_t *__restrict__ impure) {
+  const int lane = threadIdx.x & 63;
+  for (uint64_t s = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / 64; s < n;
+       s += (uint64_t)gridDim.x * blockDim.x / 64) {
+    const uint64_t w0 = pk_off[s], w1 = pk_off[s + 1], b0 = seq_off[s], L = seq_off[s + 1] - b0;
+    bool bad = false;
+    for (uint64_t w = w0 + lane; w < w1; w += 64) {
+      const uint64_t j0 = (w - w0) * 16;
+      const uint64_t m = L - j0 < 16 ? L - j0 : 16;
+      uint32_t v = 0;
+      for (uint64_t j = 0; j < m; j++) {
+        const uint8_t c = codes[b0 + j0 + j];
+        bad |= c > 3;
+        v |= (uint32_t)(c & 3) << (2 * j);
+      }
+      pk[w] = v;
+    }
+    const bool any = __ballot(bad) != 0;
+    if (lane == 0) impure[s] = any ? 1 : 0;
+  }
+}
+
+// ---------------------------------------------------------------- K1
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
   for (int o = 32; o >= 1; o >>= 1) {
-    uint32_t lo = __shfl_xor((uint32_t)v, o, 64), hi = __shfl_xor((uint32_t)(v >> 32), o, 64);
-    uint64_t x = ((uint64_t)hi << 32) | lo;
+    const uint32_t lo = __shfl_xor((uint32_t)v, o, 64), hi = __shfl_xor((uint32_t)(v >> 32), o, 64);
+    v += ((uint64_t)hi << 32) | lo;
+  }
+  return v;
+}
+__device__ __forceinline__ uint64_t wave_max64(uint64_t v) {
+  for (int o = 32; o >= 1; o >>= 1) {
+    const uint32_t lo = __shfl_xor((uint32_t)v, o, 64), hi = __shfl_xor((uint32_t)(v >> 32), o, 64);
+    const uint64_t x = ((uint64_t)hi << 32) | lo;
     v = x > v ? x : v;
   }
-  const int w = threadIdx.x >> 6;
-  __syncthreads();
-  if ((threadIdx.x & 63) == 0) red[w] = v;
-  __syncthreads();
-  uint64_t t = 0;
-  for (int i = 0; i < KT / 64; i++) t = red[i] > t ? red[i] : t;
-  return t;
+  return v;
+}
+
+struct KArgs {
+  const uint32_t *pk;
+  const uint64_t *pk_off;
+  const uint8_t *codes;
+  const uint64_t *seq_off;
+  const uint8_t *impure;
+  const int32_t *seg;
+  const uint64_t *seg_off;
+  uint64_t n;
+  int k;
+  int coop;          // 1: the waves of a workgroup share one sequence
+  int shared;        // 1: ... and one table (k = 7: 4^7 u32 = 64 KiB of LDS)
+  uint32_t *gtab;    // k >= 8: per-wave tables in global memory (gridDim * KW * B)
+  uint8_t *hist;
+  uint64_t pitch;
+  uint64_t *mag, *sumsq, *len_out;
+  unsigned long long *gmax;
+  int *err;
+};
+
+// Count the k-mers of starts [p_lo, p_hi] of sequence s (segment-local start range) into
+// `tab` with this wave's lanes taking 16 consecutive starts each; `part` / `nparts` split the
+// 16-start groups between the waves that share the sequence.
+__device__ __forceinline__ void count_range(const KArgs &A, uint64_t s, int64_t p_lo, int64_t p_hi, int64_t L,
+                                            bool pure, uint32_t *tab, int part, int nparts) {
+  const int lane = threadIdx.x & 63;
+  const int k = A.k;
+  const uint32_t mask = k == 16 ? 0xffffffffu : ((1u << (2 * k)) - 1u);
+  const int64_t ngroups = (p_hi - p_lo) / 16 + 1;
+  for (int64_t g = (int64_t)part * 64 + lane; g < ngroups; g += (int64_t)nparts * 64) {
+    const int64_t p0 = p_lo + g * 16;
+    const int cnt = (int)(p_hi - p0 + 1 < 16 ? p_hi - p0 + 1 : 16);
+    if (p0 + cnt - 1 + k > L) {  // a k-mer past the sequence end (only a segment shorter than k)
+      atomicOr(A.err, 1);
+      continue;
+    }
+    if (pure) {
+      // bases [p0, p0 + cnt + k - 1) from the 2-bit words: a 64-bit window at bit 2*(p0 % 16)
+      const uint32_t *w = A.pk + A.pk_off[s] + (p0 >> 4);
+      const uint64_t nw = A.pk_off[s + 1] - A.pk_off[s] - (uint64_t)(p0 >> 4);
+      const uint64_t lo = ((uint64_t)(nw > 1 ? w[1] : 0u) << 32) | w[0];
+      const uint64_t hi = nw > 2 ? w[2] : 0u;
+      const int sh = (int)(p0 & 15) * 2;
+      const uint64_t win = sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+      uint32_t h = 0;
+      for (int i = 0; i < k - 1; i++) h = (h << 2) | (uint32_t)((win >> (2 * i)) & 3u);
+      for (int j = 0; j < cnt; j++) {
+        h = ((h << 2) | (uint32_t)((win >> (2 * (j + k - 1))) & 3u)) & mask;
+        atomicAdd(&tab[h], 1u);
+      }
+    } else {
+      const uint8_t *b = A.codes + A.seq_off[s] + p0;
+      uint32_t h = 0;
+      bool bad = false;
+      for (int i = 0; i < k - 1; i++) {
+        const uint8_t c = b[i];
+        bad |= c > 3;
+        h = (h << 2) | (c & 3u);
+      }
+      for (int j = 0; j < cnt; j++) {
+        const uint8_t c = b[j + k - 1];
+        bad |= c > 3;
+        h = ((h << 2) | (c & 3u)) & mask;
+        if (!bad) atomicAdd(&tab[h], 1u);
+      }
+      if (bad) atomicOr(A.err, 1);  // KmerHashTable::hash throws InvalidInputException
+    }
+  }
+}
+
+__device__ __forceinline__ void count_sequence(const KArgs &A, uint64_t s, uint32_t *tab, int part, int nparts) {
+  const int64_t L = (int64_t)(A.seq_off[s + 1] - A.seq_off[s]);
+  const bool pure = A.impure[s] == 0;
+  for (uint64_t g = A.seg_off[s]; g < A.seg_off[s + 1]; g++) {
+    const int64_t first = A.seg[2 * g], last = (int64_t)A.seg[2 * g + 1] - A.k + 1;
+    count_range(A, s, first, last < first ? first : last, L, pure, tab, part, nparts);  // a short segment still hashes at `first`
+  }
+}
+
+// Table reads / zeroing: plain LDS accesses, or for the global tables relaxed agent-scope
+// atomics (sc1: the L1 is bypassed, the counts live in L2 where the atomics added them).
+__device__ __forceinline__ uint32_t tab_ld(const uint32_t *p, bool glob) {
+  return glob ? __hip_atomic_load(const_cast<uint32_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *p;
+}
+__device__ __forceinline__ void tab_zero(uint32_t *p, bool glob) {
+  if (glob) __hip_atomic_store(p, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = 0;
+}
+// every table access of this wave complete (LDS: lgkmcnt; global: vmcnt)
+__device__ __forceinline__ void tab_drain(bool glob) {
+  if (glob) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+// Row of sequence s from the summed tables tabs[0..ntab) (stride B): write (width T) + stats;
+// the calling wave only.  Zeroes the tables for the next sequence.
+template <typename T>
+__device__ __forceinline__ void write_row(const KArgs &A, uint64_t s, uint32_t *tab0, int ntab, int B, bool write,
+                                          bool glob, uint64_t *wmax) {
+  const int lane = threadIdx.x & 63;
+  constexpr int per = 16 / (int)sizeof(T);  // bins per 16-byte store
+  uint64_t m = 0, sq = 0, mx = 0;
+  uint8_t *row = A.hist + s * A.pitch;
+  const int nst = (B + per - 1) / per;
+  for (int q = lane; q < nst; q += 64) {
+    T out[per];
+#pragma unroll
+    for (int e = 0; e < per; e++) {
+      const int b = q * per + e;
+      uint64_t v = 0;
+      if (b < B) {
+        uint32_t c = 0;
+        for (int t = 0; t < ntab; t++) {
+          c += tab_ld(tab0 + (size_t)t * B + b, glob);
+          tab_zero(tab0 + (size_t)t * B + b, glob);
+        }
+        v = (uint64_t)c + 1;  // pseudocount (ClusterFactory.cpp:995)
+        m += v;
+        sq += v * v;
+        mx = v > mx ? v : mx;
+      }
+      out[e] = (T)v;
+    }
+    if (write) {
+      if ((q + 1) * per <= B || B * (int)sizeof(T) >= 16) {
+        *reinterpret_cast<uint4 *>(row + (size_t)q * 16) = *reinterpret_cast<const uint4 *>(out);
+      } else {  // a row narrower than 16 bytes (k = 1, 8-bit): bytes, then zero the pad
+        for (int e = 0; e < B - q * per; e++) reinterpret_cast<T *>(row)[q * per + e] = out[e];
+      }
+    }
+  }
+  if (write) {
+    const uint64_t used = ((uint64_t)B * sizeof(T) + 15) / 16 * 16;
+    for (uint64_t b = (uint64_t)B * sizeof(T) + lane; b < A.pitch; b += 64)
+      if (b >= used || B * sizeof(T) < 16) row[b] = 0;
+  }
+  m = wave_sum64(m);
+  sq = wave_sum64(sq);
+  mx = wave_max64(mx);
+  if (lane == 0 && write) {
+    A.mag[s] = m;
+    A.sumsq[s] = sq;
+    A.len_out[s] = A.seq_off[s + 1] - A.seq_off[s];
+  }
+  *wmax = mx > *wmax ? mx : *wmax;
 }
 
 template <typename T>
-__global__ __launch_bounds__(KT) void kmer_kernel(const uint8_t *__restrict__ codes, const uint64_t *__restrict__ seq_off,
-                                                  const int32_t *__restrict__ seg, const uint64_t *__restrict__ seg_off,
-                                                  uint64_t n, int k, bool build, uint8_t *__restrict__ hist,
-                                                  uint64_t pitch, uint64_t *__restrict__ mag,
-                                                  uint64_t *__restrict__ sumsq, uint64_t *__restrict__ len_out,
-                                                  unsigned long long *__restrict__ gmax, int *__restrict__ err) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t table[];
-  __shared__ uint64_t red[KT / 64];
-  const int B = 1 << (2 * k);
-  for (uint64_t s = blockIdx.x; s < n; s += gridDim.x) {
-    for (int b = threadIdx.x; b < B; b += KT) table[b] = 0;
+__global__ __launch_bounds__(KT) void kmer_kernel(KArgs A, bool write) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t ltab[];
+  __shared__ uint64_t s_max[KW];
+  const int B = 1 << (2 * A.k);
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const bool glob = A.gtab != nullptr;
+  uint32_t *base = glob ? A.gtab + (uint64_t)blockIdx.x * KW * (uint64_t)B : ltab;  // this workgroup's tables
+  uint32_t *mytab = base + (A.shared ? 0 : (size_t)wv * B);
+  uint64_t wmax = 0;
+  if (!A.shared || wv == 0)
+    for (int b = lane; b < B; b += 64) tab_zero(mytab + b, glob);
+  tab_drain(glob);
+  if (!A.coop) {
+    // one wave per sequence: the wave's own table, no workgroup barrier
+    for (uint64_t s = (uint64_t)blockIdx.x * KW + wv; s < A.n; s += (uint64_t)gridDim.x * KW) {
+      count_sequence(A, s, mytab, 0, 1);
+      tab_drain(glob);
+      write_row<T>(A, s, mytab, 1, B, write, glob, &wmax);
+      tab_drain(glob);
+    }
+  } else {
+    // the KW waves share a sequence (per-wave tables, or one shared table); wave 0 sums the
+    // tables into the row
     __syncthreads();
-    const uint8_t *seq = codes + seq_off[s];
-    const int64_t L = (int64_t)(seq_off[s + 1] - seq_off[s]);
-    for (uint64_t g = seg_off[s]; g < seg_off[s + 1]; g++) {
-      const int64_t first = seg[2 * g], last = (int64_t)seg[2 * g + 1] - k + 1;
-      const int64_t lastp = last < first ? first : last;  // a short segment still hashes at `first`
-      for (int64_t p = first + threadIdx.x; p <= lastp; p += KT) {
-        if (p + k > L) {
-          atomicOr(err, 1);
-          continue;
-        }
-        uint32_t h = 0;
-        bool bad = false;
-        for (int i = 0; i < k; i++) {
-          uint8_t c = seq[p + i];
-          bad |= c > 3;
-          h = (h << 2) | (c & 3);
-        }
-        if (bad) {
-          atomicOr(err, 1);
-          continue;
-        }
-        atomicAdd(&table[h], 1u);
+    for (uint64_t s = blockIdx.x; s < A.n; s += gridDim.x) {
+      count_sequence(A, s, mytab, wv, KW);
+      tab_drain(glob);
+      __syncthreads();
+      if (wv == 0) {
+        write_row<T>(A, s, base, A.shared ? 1 : KW, B, write, glob, &wmax);
+        tab_drain(glob);
       }
+      __syncthreads();
     }
-    __syncthreads();
-    uint64_t m = 0, sq = 0, mx = 0;
-    for (int b = threadIdx.x; b < B; b += KT) {
-      uint64_t v = (uint64_t)table[b] + 1;  // pseudocount (ClusterFactory.cpp:995)
-      m += v;
-      sq += v * v;
-      mx = v > mx ? v : mx;
-    }
-    if (build) {
-      T *row = reinterpret_cast<T *>(hist + s * pitch);
-      for (int b = threadIdx.x; b < B; b += KT) row[b] = (T)(table[b] + 1);
-      const int used = B * (int)sizeof(T);
-      for (int b = used + threadIdx.x; b < (int)pitch; b += KT) hist[s * pitch + b] = 0;  // zero padding
-      uint64_t tm = block_sum_u64(m, red);
-      uint64_t tq = block_sum_u64(sq, red);
-      if (threadIdx.x == 0) {
-        mag[s] = tm;
-        sumsq[s] = tq;
-        len_out[s] = (uint64_t)L;
-      }
-    } else {
-      uint64_t tx = block_max_u64(mx, red);
-      if (threadIdx.x == 0) atomicMax(gmax, (unsigned long long)tx);
-    }
-    __syncthreads();
+  }
+  if (lane == 0) s_max[wv] = wmax;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t t = 0;
+    for (int i = 0; i < KW; i++) t = s_max[i] > t ? s_max[i] : t;
+    atomicMax(A.gmax, (unsigned long long)t);
   }
 }
 
 }  // namespace
 
-int launch_kmer(mc_ctx *c, int k, int width, bool build, uint64_t *d_max, int *d_err) {
+int launch_expand(mc_ctx *c, uint64_t nexc, const uint64_t *d_exc_pos, const uint8_t *d_exc_val) {
+  const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((c->n + 3) / 4, 8192));
+  expand_kernel<<<grid, 256, 0, c->stream>>>((const uint32_t *)c->packed.p, (const uint64_t *)c->pk_off.p,
+                                            (const uint64_t *)c->seq_off.p, c->n, (uint8_t *)c->codes.p);
+  MCG_CHECK(hipGetLastError());
+  if (nexc) {
+    exceptions_kernel<<<(int)std::min<uint64_t>((nexc + 255) / 256, 4096), 256, 0, c->stream>>>(
+        d_exc_pos, d_exc_val, nexc, (uint8_t *)c->codes.p);
+    MCG_CHECK(hipGetLastError());
+  }
+  return MC_OK;
+}
+
+int launch_pack(mc_ctx *c) {
+  const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((c->n + 3) / 4, 8192));
+  pack_kernel<<<grid, 256, 0, c->stream>>>((const uint8_t *)c->codes.p, (const uint64_t *)c->seq_off.p,
+                                          (const uint64_t *)c->pk_off.p, c->n, (uint32_t *)c->packed.p,
+                                          (uint8_t *)c->impure.p);
+  MCG_CHECK(hipGetLastError());
+  return MC_OK;
+}
+
+int launch_kmer(mc_ctx *c, int k, int width, bool write, uint64_t *d_max, int *d_err) {
   const int B = 1 << (2 * k);
-  const size_t lds = (size_t)B * 4;
-  const int grid = (int)std::min<uint64_t>(c->n, 8192);
+  KArgs A;
+  A.pk = (const uint32_t *)c->packed.p;
+  A.pk_off = (const uint64_t *)c->pk_off.p;
+  A.codes = (const uint8_t *)c->codes.p;
+  A.seq_off = (const uint64_t *)c->seq_off.p;
+  A.impure = (const uint8_t *)c->impure.p;
+  A.seg = (const int32_t *)c->seg.p;
+  A.seg_off = (const uint64_t *)c->seg_off.p;
+  A.n = c->n;
+  A.k = k;
+  // long sequences: the waves of a workgroup share one (mean length >= 4 kb); k = 7: one
+  // 64 KiB LDS table shared by the workgroup's waves
+  const bool per_wave_lds = (size_t)KW * B * 4 <= 64 * 1024, shared_lds = !per_wave_lds && (size_t)B * 4 <= 64 * 1024;
+  A.shared = shared_lds ? 1 : 0;
+  A.coop = (c->n && c->h_seq_off[c->n] / c->n >= 4096) || shared_lds ? 1 : 0;
+  A.hist = (uint8_t *)c->hist.p;
+  A.pitch = c->pitch;
+  A.mag = (uint64_t *)c->mag.p;
+  A.sumsq = (uint64_t *)c->sumsq.p;
+  A.len_out = (uint64_t *)c->len.p;
+  A.gmax = (unsigned long long *)d_max;
+  A.err = d_err;
+  const uint64_t units = A.coop ? c->n : (c->n + KW - 1) / KW;
+  int grid = (int)std::min<uint64_t>(units, 8192);
   if (grid == 0) return MC_OK;
+  size_t lds = 0;
+  A.gtab = nullptr;
+  if (per_wave_lds || shared_lds) {
+    lds = shared_lds ? (size_t)B * 4 : (size_t)KW * B * 4;
+  } else {
+    // 4^k u32 per wave does not fit LDS: per-wave tables in global scratch, as many resident
+    // workgroups as the scratch allows (<= 1 GiB)
+    const uint64_t per_wg = (uint64_t)KW * B * 4;
+    grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)grid, (1ull << 30) / per_wg));
+    if (int rc = ensure(c->s_g, (size_t)grid * per_wg)) return rc;
+    MCG_CHECK(hipMemsetAsync(c->s_g.p, 0, (size_t)grid * per_wg, c->stream));
+    A.gtab = (uint32_t *)c->s_g.p;
+  }
   timed_begin(c);
-  const uint8_t *codes = (const uint8_t *)c->codes.p;
-  const uint64_t *so = (const uint64_t *)c->seq_off.p;
-  const int32_t *sg = (const int32_t *)c->seg.p;
-  const uint64_t *sgo = (const uint64_t *)c->seg_off.p;
-  uint8_t *h = (uint8_t *)c->hist.p;
-  uint64_t *mg = (uint64_t *)c->mag.p, *sq = (uint64_t *)c->sumsq.p, *ln = (uint64_t *)c->len.p;
-  auto *mx = (unsigned long long *)d_max;
   switch (width) {
-    case 1: kmer_kernel<uint8_t><<<grid, KT, lds, c->stream>>>(codes, so, sg, sgo, c->n, k, build, h, c->pitch, mg, sq, ln, mx, d_err); break;
-    case 2: kmer_kernel<uint16_t><<<grid, KT, lds, c->stream>>>(codes, so, sg, sgo, c->n, k, build, h, c->pitch, mg, sq, ln, mx, d_err); break;
-    case 4: kmer_kernel<uint32_t><<<grid, KT, lds, c->stream>>>(codes, so, sg, sgo, c->n, k, build, h, c->pitch, mg, sq, ln, mx, d_err); break;
-    default: kmer_kernel<uint64_t><<<grid, KT, lds, c->stream>>>(codes, so, sg, sgo, c->n, k, build, h, c->pitch, mg, sq, ln, mx, d_err); break;
+    case 1: kmer_kernel<uint8_t><<<grid, KT, lds, c->stream>>>(A, write); break;
+    case 2: kmer_kernel<uint16_t><<<grid, KT, lds, c->stream>>>(A, write); break;
+    case 4: kmer_kernel<uint32_t><<<grid, KT, lds, c->stream>>>(A, write); break;
+    default: kmer_kernel<uint64_t><<<grid, KT, lds, c->stream>>>(A, write); break;
   }
   MCG_CHECK(hipGetLastError());
   timed_end(c, F_KMER);

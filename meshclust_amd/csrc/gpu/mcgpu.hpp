@@ -2,6 +2,7 @@
 //
 // Data layout in HBM (one context = one GPU):
 //   codes      n sequences' one-digit bytes, concatenated (the NW input, Point::get_data_str)
+//   packed     the same as 2-bit codes, 16 bases per 32-bit word, records word-aligned (K1 input)
 //   seq_off    byte offsets (n+1), seg/seg_off: k-mer segments per sequence
 //   hist       n rows of B = 4^k bins of width w bytes, id order, row pitch 16-byte aligned
 //   mag/sumsq  per row: sum of bins (pseudo magnitude) and sum of squared bins
@@ -76,6 +77,8 @@ struct mc_ctx {
   uint64_t n = 0;
   std::vector<uint64_t> h_seq_off;
   mcg::Buf codes, seq_off, seg, seg_off;
+  mcg::Buf packed, pk_off, impure;  // 2-bit codes (16 bases per word, records word-aligned), impure flags
+  int kmer_spec_k = 0;              // K1 rows already written at 8 bits for this k (mc_kmer_max's pass)
   // histograms
   int k = 0, B = 0, width = 0;
   uint64_t pitch = 0;
@@ -129,7 +132,9 @@ void flush_timers(mc_ctx *c);  // after a stream synchronisation
 HistView hist_view(const mc_ctx *c);
 
 // ---- launchers (defined in kmer.hip, k2.hip, nw.hip) -------------------------------------
-int launch_kmer(mc_ctx *c, int k, int width, bool build, uint64_t *d_max, int *d_err);
+int launch_expand(mc_ctx *c, uint64_t nexc, const uint64_t *d_exc_pos, const uint8_t *d_exc_val);
+int launch_pack(mc_ctx *c);
+int launch_kmer(mc_ctx *c, int k, int width, bool write, uint64_t *d_max, int *d_err);
 int launch_distance_keys(mc_ctx *c, const uint32_t *d_piv, uint32_t npiv, const uint32_t *d_ids, uint64_t m,
                          uint16_t *d_keys);
 int launch_pairs(mc_ctx *c, const uint32_t *d_a, const uint32_t *d_b, uint64_t m, const uint16_t *flags, int nflag,

@@ -1,5 +1,6 @@
 // capi.cpp -- in-process C API of libmeshclust.so (used by bench.py and the Python package):
 // parse once, keep the dataset, run the GPU pipeline repeatedly on a resident context.
+#include <chrono>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -29,7 +30,8 @@ uint64_t mcl_num_seqs(void *ds) { return ((mc::Dataset *)ds)->size(); }
 void mcl_view(void *dsv, const uint8_t **codes, const uint64_t **seq_off, const int32_t **seg,
               const uint64_t **seg_off) {
   auto *ds = (mc::Dataset *)dsv;
-  *codes = ds->codes.data();
+  if (ds->bytes_view.size() != ds->bases()) ds->bytes_view = mc::unpack_codes(*ds);
+  *codes = ds->bytes_view.data();
   *seq_off = ds->seq_off.data();
   *seg = ds->seg.data();
   *seg_off = ds->seg_off.data();
@@ -73,8 +75,10 @@ static int run_common(void *dsv, mc_ctx *ctx, int argc, char **argv, int upload,
     mc::Options opt = mc::parse_options(argc, argv, false);
     opt.quiet = true;
     mc::RunResult rr = mc::run_pipeline(*ds, ctx, opt, upload != 0, comm);
-    if (clstr_path) mc::write_clstr(clstr_path, *ds, rr.part);
-    std::string js = mc::stats_json(rr, 0, 0);
+    const auto t1 = std::chrono::steady_clock::now();
+    if (clstr_path) mc::write_clstr(clstr_path, *ds, rr.part, opt.threads > 0 ? opt.threads : 1);
+    const double write_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();
+    std::string js = mc::stats_json(rr, 0, write_ms);
     if (stats && cap > 0) snprintf(stats, cap, "%s", js.c_str());
     return 0;
   } catch (const mc::Error &e) {

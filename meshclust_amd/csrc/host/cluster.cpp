@@ -345,25 +345,59 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
   return part;
 }
 
-void write_clstr(const std::string &path, const Dataset &ds, const std::vector<Center> &part) {
+namespace {
+inline void put_uint(std::string &o, unsigned long long v) {
+  char b[24];
+  int n = 0;
+  do {
+    b[n++] = (char)('0' + v % 10);
+    v /= 10;
+  } while (v);
+  while (n) o.push_back(b[--n]);
+}
+}  // namespace
+
+// print_output (ClusterFactory.cpp:495-520): ">Cluster c" for every non-empty cluster, then
+// "i\t{len}nt, {header}... " per member with '*' after the centre.  Clusters are formatted
+// into per-thread buffers in parallel and written in order.
+void write_clstr(const std::string &path, const Dataset &ds, const std::vector<Center> &part, int threads) {
   FILE *f = fopen(path.c_str(), "w");
   if (!f) throw Error("cannot open output " + path, 1);
-  std::vector<char> buf(1 << 20);
-  setvbuf(f, buf.data(), _IOFBF, buf.size());
+  const size_t C = part.size();
+  std::vector<int> label(C, -1);
   int counter = 0;
-  for (const auto &cen : part) {
-    if (cen.points.empty()) continue;
-    fprintf(f, ">Cluster %d\n", counter);
-    int pt = 0;
-    for (uint32_t p : cen.points) {
-      fprintf(f, "%d\t%llunt, %s... ", pt, (unsigned long long)ds.lengths[p], ds.headers[p].c_str());
-      if (p == cen.centre) fputc('*', f);
-      fputc('\n', f);
-      pt++;
+  for (size_t c = 0; c < C; c++)
+    if (!part[c].points.empty()) label[c] = counter++;
+  const int T = std::max(1, std::min<int>(threads, (int)(C / 64) + 1));
+  std::vector<std::string> out(T);
+#pragma omp parallel for schedule(static, 1) num_threads(T)
+  for (int t = 0; t < T; t++) {
+    std::string &o = out[t];
+    const size_t c0 = C * t / T, c1 = C * (t + 1) / T;
+    for (size_t c = c0; c < c1; c++) {
+      const auto &cen = part[c];
+      if (cen.points.empty()) continue;
+      o += ">Cluster ";
+      put_uint(o, (unsigned long long)label[c]);
+      o += '\n';
+      unsigned long long pt = 0;
+      for (uint32_t p : cen.points) {
+        put_uint(o, pt++);
+        o += '\t';
+        put_uint(o, (unsigned long long)ds.lengths[p]);
+        o += "nt, ";
+        o += ds.headers[p];
+        o += "... ";
+        if (p == cen.centre) o += '*';
+        o += '\n';
+      }
     }
-    counter++;
   }
-  fclose(f);
+  bool ok = true;
+  for (const auto &o : out)
+    if (!o.empty()) ok &= fwrite(o.data(), 1, o.size(), f) == o.size();
+  ok &= fclose(f) == 0;
+  if (!ok) throw Error("cannot write output " + path, 1);
 }
 
 }  // namespace mc

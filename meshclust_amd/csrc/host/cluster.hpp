@@ -55,6 +55,6 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
                                        PhaseTimer &timer, ClusterStats &stats);
 
 // CD-HIT style writer (ClusterFactory.cpp:495-520).
-void write_clstr(const std::string &path, const Dataset &ds, const std::vector<Center> &part);
+void write_clstr(const std::string &path, const Dataset &ds, const std::vector<Center> &part, int threads = 1);
 
 }  // namespace mc

@@ -1,4 +1,9 @@
 // fasta.cpp -- see fasta.hpp.
+//
+// One pass per file, in parallel: the mapped file is cut into chunks at record starts (a '>'
+// at the start of a line), each thread splits its chunk into records with safe_getline's
+// line semantics, runs Chromosome::help + encodeNucleotides on every record in place and
+// packs the codes; the chunks are then stitched together with prefix sums.
 #include "fasta.hpp"
 
 #include <fcntl.h>
@@ -6,8 +11,10 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cctype>
 #include <cstring>
+#include <exception>
 
 #include "common.hpp"
 
@@ -19,35 +26,31 @@ namespace {
 // IUPAC ambiguity letters mapped onto one of them; 255 = not in the map.
 struct CodeTable {
   uint8_t v[256];
+  uint8_t up[256];  // toupper (Chromosome::toUpperCase, Chromosome.cpp:153-157)
   CodeTable() {
     memset(v, 255, sizeof v);
     v['A'] = 0; v['C'] = 1; v['G'] = 2; v['T'] = 3;
     v['R'] = 2; v['Y'] = 1; v['M'] = 0; v['K'] = 3; v['S'] = 2; v['W'] = 3;
     v['H'] = 1; v['B'] = 3; v['V'] = 0; v['D'] = 3; v['N'] = 1; v['X'] = 2;
+    for (int c = 0; c < 256; c++) up[c] = (uint8_t)toupper(c);
   }
 };
 const CodeTable kCodes;
 
-[[noreturn]] void invalid_nucleotide(char c) {
-  throw Error(std::string("Invalid nucleotide: ") + c, 1);
+[[noreturn]] void invalid_nucleotide(uint8_t c) {
+  throw Error(std::string("Invalid nucleotide: ") + (char)c, 1);
 }
-
-struct RawRecord {
-  std::string header;
-  std::string base;
-  bool base_ready = false;
-};
 
 }  // namespace
 
 // Chromosome::help(1000000, true) then ChromosomeOneDigit::help().
-void process_record(std::string &base, std::vector<int32_t> &out) {
+void process_record(uint8_t *base, size_t usize, std::vector<int32_t> &out) {
+  const int size = (int)usize;
   // toUpperCase (Chromosome.cpp:153-157)
-  for (auto &c : base) c = (char)toupper((unsigned char)c);
+  for (int i = 0; i < size; i++) base[i] = kCodes.up[base[i]];
   // removeN (Chromosome.cpp:162-184): maximal non-N runs; a run that starts on the very last
   // character is never closed (the else-if chain at :166-182).
   std::vector<int32_t> seg;
-  const int size = (int)base.size();
   int start = -1;
   for (int i = 0; i < size; i++) {
     if (base[i] != 'N' && start == -1) {
@@ -62,8 +65,8 @@ void process_record(std::string &base, std::vector<int32_t> &out) {
       start = -1;
     }
   }
-  // mergeSegments (Chromosome.cpp:190-226); segment->at(0) throws on an empty list.
-  // (a 1-base or all-N record has no closed run)
+  // mergeSegments (Chromosome.cpp:190-226); segment->at(0) throws on an empty list
+  // (a 1-base or all-N record has no closed run).
   if (seg.empty()) throw Error("vector::_M_range_check: __n (which is 0) >= this->size() (which is 0)", 1);
   std::vector<int32_t> merged;
   int s = seg[0], e = seg[1];
@@ -100,19 +103,19 @@ void process_record(std::string &base, std::vector<int32_t> &out) {
   const int nseg = (int)out.size() / 2;
   for (int k = 0; k < nseg; k++) {
     for (int i = out[2 * k]; i <= out[2 * k + 1]; i++) {
-      uint8_t v = kCodes.v[(unsigned char)base[i]];
+      uint8_t v = kCodes.v[base[i]];
       if (v == 255) invalid_nucleotide(base[i]);
-      base[i] = (char)v;
+      base[i] = v;
     }
   }
   if (nseg > 0) {  // the skipped intervals: every non-'N' byte is encoded, 'N' stays
     auto outside = [&](int a, int b) {
       for (int i = a; i <= b; i++) {
-        char c = base[i];
+        uint8_t c = base[i];
         if (c != 'N') {
-          uint8_t v = kCodes.v[(unsigned char)c];
+          uint8_t v = kCodes.v[c];
           if (v == 255) invalid_nucleotide(c);
-          base[i] = (char)v;
+          base[i] = v;
         }
       }
     };
@@ -124,107 +127,210 @@ void process_record(std::string &base, std::vector<int32_t> &out) {
 
 namespace {
 
-// Splits a file into records with safe_getline's line semantics (ChromListMaker.cpp:23-47):
-// lines end at "\n", "\r\n", a lone "\r", or EOF.
-void read_records(const std::string &path, std::vector<RawRecord> &recs) {
-  int fd = open(path.c_str(), O_RDONLY);
-  if (fd < 0) throw Error("File \"" + path + "\" does not exist", 1);
-  struct stat st;
-  fstat(fd, &st);
-  size_t n = (size_t)st.st_size;
-  const char *buf = nullptr;
-  if (n > 0) {
-    void *m = mmap(nullptr, n, PROT_READ, MAP_PRIVATE, fd, 0);
-    if (m == MAP_FAILED) {
-      close(fd);
-      throw Error("cannot map " + path, 1);
-    }
-    madvise(m, n, MADV_SEQUENTIAL);
-    buf = (const char *)m;
-  }
-  close(fd);
-  if (n == 0) throw Error("input file " + path + " is empty", 1);
-  RawRecord *cur = nullptr;
-  size_t pos = 0;
-  auto on_line = [&](const char *p, size_t len) {
-    if (len > 0 && p[0] == '>') {
-      recs.emplace_back();
-      cur = &recs.back();
-      cur->header.assign(p, len);
+// One chunk of a file: whole records, parsed, encoded and packed.
+struct Chunk {
+  struct Rec {
+    size_t hdr, hdr_len;  // header line in the mapped file
+    size_t off, len;      // one-digit bytes in `bytes`
+    bool ready;           // isBaseReady: some line followed the header (or EOF did)
+  };
+  std::vector<Rec> recs;
+  std::vector<uint8_t> bytes;
+  std::vector<int32_t> seg;
+  std::vector<uint64_t> nseg;     // segment pairs per record
+  std::vector<uint64_t> exc_pos;  // chunk-local byte positions
+  std::vector<uint8_t> exc_val;
+  uint64_t words = 0;
+  std::string err;
+};
+
+inline bool line_start(const char *buf, size_t i) { return i == 0 || buf[i - 1] == '\n' || buf[i - 1] == '\r'; }
+
+// Records of buf[a, z) with safe_getline's line semantics (ChromListMaker.cpp:23-47): lines
+// end at "\n", "\r\n", a lone "\r", or EOF.  A line starting with '>' opens a record whose
+// header is the whole line; other lines are appended to the current record.  `eof`: the chunk
+// ends the file (the final empty read sets isBaseReady of the last record).
+void split_chunk(const char *buf, size_t a, size_t z, bool first, bool eof, const std::string &path, Chunk &ck) {
+  Chunk::Rec *cur = nullptr;
+  auto on_line = [&](size_t p, size_t len) {
+    if (len > 0 && buf[p] == '>') {
+      ck.recs.push_back({p, len, ck.bytes.size(), 0, false});
+      cur = &ck.recs.back();
     } else {
       if (!cur) {
         if (len == 0) return;  // blank lines before the first header
-        throw Error("sequence data before the first '>' header in " + path, 1);
+        if (first) throw Error("sequence data before the first '>' header in " + path, 1);
+        throw Error("internal: chunk does not start at a record", 1);
       }
-      cur->base.append(p, len);
-      cur->base_ready = true;
+      ck.bytes.insert(ck.bytes.end(), buf + p, buf + p + len);
+      cur->len += len;
+      cur->ready = true;
     }
   };
-  while (pos < n) {
+  size_t pos = a;
+  while (pos < z) {
     const char *p = buf + pos;
-    size_t rem = n - pos;
+    const size_t rem = z - pos;
     const char *nl = (const char *)memchr(p, '\n', rem);
     const char *cr = (const char *)memchr(p, '\r', nl ? (size_t)(nl - p) : rem);
     if (cr) {
-      on_line(p, (size_t)(cr - p));
+      on_line(pos, (size_t)(cr - p));
       pos = (size_t)(cr - buf) + 1;
-      if (pos < n && buf[pos] == '\n') pos++;
+      if (pos < z && buf[pos] == '\n') pos++;
     } else if (nl) {
-      on_line(p, (size_t)(nl - p));
+      on_line(pos, (size_t)(nl - p));
       pos = (size_t)(nl - buf) + 1;
     } else {
-      on_line(p, rem);
-      pos = n;
+      on_line(pos, rem);
+      pos = z;
     }
   }
-  on_line(buf + n, 0);  // the final empty read at EOF (sets isBaseReady of the last record)
-  munmap((void *)buf, n);
+  if (eof && cur) cur->ready = true;
+}
+
+void finish_chunk(Chunk &ck) {
+  ck.nseg.resize(ck.recs.size());
+  std::vector<int32_t> segs;
+  for (size_t r = 0; r < ck.recs.size(); r++) {
+    auto &rec = ck.recs[r];
+    if (!rec.ready) throw Error("The header and the sequence must be set before calling finalize", 1);
+    process_record(ck.bytes.data() + rec.off, rec.len, segs);
+    ck.seg.insert(ck.seg.end(), segs.begin(), segs.end());
+    ck.nseg[r] = segs.size() / 2;
+    const uint8_t *b = ck.bytes.data() + rec.off;
+    for (size_t i = 0; i < rec.len; i++)
+      if (b[i] > 3) {
+        ck.exc_pos.push_back(rec.off + i);
+        ck.exc_val.push_back(b[i]);
+      }
+    ck.words += (rec.len + 15) / 16;
+  }
+}
+
+// up to 16 one-digit bytes -> one word (bytes outside 0..3 pack as their low two bits; the
+// exception list restores them)
+inline uint32_t pack16(const uint8_t *b, size_t n) {
+  uint32_t w = 0;
+  for (size_t j = 0; j < n; j++) w |= (uint32_t)(b[j] & 3) << (2 * j);
+  return w;
 }
 
 }  // namespace
 
 void parse_fasta_files(const std::vector<std::string> &files, Dataset &ds, int threads) {
-  for (const auto &f : files) {
-    std::vector<RawRecord> recs;
-    read_records(f, recs);
-    const size_t nr = recs.size();
-    std::vector<std::vector<int32_t>> segs(nr);
-    std::vector<std::string> err(nr);
-#pragma omp parallel for schedule(dynamic, 64) num_threads(threads)
-    for (size_t i = 0; i < nr; i++) {
+  if (threads < 1) threads = 1;
+  if (ds.seq_off.empty()) {
+    ds.seq_off.push_back(0);
+    ds.seg_off.push_back(0);
+    ds.pk_off.push_back(0);
+  }
+  for (const auto &path : files) {
+    int fd = open(path.c_str(), O_RDONLY);
+    if (fd < 0) throw Error("File \"" + path + "\" does not exist", 1);
+    struct stat st;
+    fstat(fd, &st);
+    const size_t n = (size_t)st.st_size;
+    if (n == 0) {
+      close(fd);
+      throw Error("input file " + path + " is empty", 1);
+    }
+    void *m = mmap(nullptr, n, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
+    close(fd);
+    if (m == MAP_FAILED) throw Error("cannot map " + path, 1);
+    const char *buf = (const char *)m;
+    // chunk starts: the first record start at or after t * n / T
+    const int T = (int)std::max<size_t>(1, std::min<size_t>((size_t)threads * 4, n / (1 << 16) + 1));
+    std::vector<size_t> cut(T + 1, n);
+    cut[0] = 0;
+    for (int t = 1; t < T; t++) {
+      size_t i = std::max(cut[t - 1], (size_t)((double)n * t / T));
+      while (i < n && !(buf[i] == '>' && line_start(buf, i))) {
+        const char *q = i + 1 < n ? (const char *)memchr(buf + i + 1, '>', n - i - 1) : nullptr;
+        i = q ? (size_t)(q - buf) : n;
+      }
+      cut[t] = i;
+    }
+    std::vector<Chunk> ck(T);
+#pragma omp parallel for schedule(dynamic, 1) num_threads(threads)
+    for (int t = 0; t < T; t++) {
       try {
-        if (!recs[i].base_ready)
-          throw Error("The header and the sequence must be set before calling finalize", 1);
-        process_record(recs[i].base, segs[i]);
+        if (cut[t] < cut[t + 1]) {
+          split_chunk(buf, cut[t], cut[t + 1], t == 0, cut[t + 1] == n, path, ck[t]);
+          finish_chunk(ck[t]);
+        }
       } catch (const std::exception &e) {
-        err[i] = e.what();
+        ck[t].err = e.what();
       }
     }
-    for (size_t i = 0; i < nr; i++)
-      if (!err[i].empty()) throw Error(err[i] + " (record " + recs[i].header + ")", 1);
+    // the first failing record in file order reports (the reference stops there)
+    for (int t = 0; t < T; t++)
+      if (!ck[t].err.empty()) {
+        munmap(m, n);
+        throw Error(ck[t].err, 1);
+      }
+    // stitch: prefix sums over chunks, then parallel copies
+    std::vector<uint64_t> rec0(T + 1, ds.size()), byte0(T + 1, ds.bases()), word0(T + 1, ds.pk_off.back()),
+        seg0(T + 1, ds.seg.size() / 2), exc0(T + 1, ds.exc_pos.size());
     uint64_t lsum = 0;
-    size_t old = ds.codes.size();
-    size_t add = 0;
-    for (auto &r : recs) add += r.base.size();
-    ds.codes.resize(old + add);
-    if (ds.seq_off.empty()) ds.seq_off.push_back(0);
-    if (ds.seg_off.empty()) ds.seg_off.push_back(0);
-    std::vector<uint64_t> offs(nr + 1, old);
-    for (size_t i = 0; i < nr; i++) offs[i + 1] = offs[i] + recs[i].base.size();
-#pragma omp parallel for schedule(static) num_threads(threads)
-    for (size_t i = 0; i < nr; i++)
-      if (!recs[i].base.empty()) memcpy(&ds.codes[offs[i]], recs[i].base.data(), recs[i].base.size());
-    for (size_t i = 0; i < nr; i++) {
-      ds.headers.push_back(std::move(recs[i].header));
-      ds.lengths.push_back(recs[i].base.size());
-      lsum += recs[i].base.size();
-      ds.seq_off.push_back(offs[i + 1]);
-      ds.seg.insert(ds.seg.end(), segs[i].begin(), segs[i].end());
-      ds.seg_off.push_back(ds.seg.size() / 2);
+    for (int t = 0; t < T; t++) {
+      rec0[t + 1] = rec0[t] + ck[t].recs.size();
+      byte0[t + 1] = byte0[t] + ck[t].bytes.size();
+      word0[t + 1] = word0[t] + ck[t].words;
+      seg0[t + 1] = seg0[t] + ck[t].seg.size() / 2;
+      exc0[t + 1] = exc0[t] + ck[t].exc_pos.size();
+      lsum += ck[t].bytes.size();
     }
-    ds.file_count.push_back(nr);
+    const uint64_t nr = rec0[T], nwords = word0[T];
+    ds.headers.resize(nr);
+    ds.lengths.resize(nr);
+    ds.seq_off.resize(nr + 1);
+    ds.pk_off.resize(nr + 1);
+    ds.seg_off.resize(nr + 1);
+    ds.seg.resize(2 * seg0[T]);
+    ds.exc_pos.resize(exc0[T]);
+    ds.exc_val.resize(exc0[T]);
+    {
+      PodArray<uint32_t> grown;
+      grown.resize(nwords);
+      if (word0[0]) memcpy(grown.data(), ds.packed.data(), word0[0] * 4);
+      ds.packed = std::move(grown);
+    }
+#pragma omp parallel for schedule(dynamic, 1) num_threads(threads)
+    for (int t = 0; t < T; t++) {
+      const Chunk &c = ck[t];
+      uint64_t w = word0[t], sg = seg0[t];
+      for (size_t r = 0; r < c.recs.size(); r++) {
+        const auto &rec = c.recs[r];
+        const uint64_t id = rec0[t] + r;
+        ds.headers[id].assign(buf + rec.hdr, rec.hdr_len);
+        ds.lengths[id] = rec.len;
+        ds.seq_off[id + 1] = byte0[t] + rec.off + rec.len;
+        const uint8_t *b = c.bytes.data() + rec.off;
+        for (size_t j = 0; j < rec.len; j += 16) ds.packed[w++] = pack16(b + j, std::min<size_t>(16, rec.len - j));
+        ds.pk_off[id + 1] = w;
+        sg += c.nseg[r];
+        ds.seg_off[id + 1] = sg;
+      }
+      std::copy(c.seg.begin(), c.seg.end(), ds.seg.begin() + 2 * seg0[t]);
+      for (size_t q = 0; q < c.exc_pos.size(); q++) {
+        ds.exc_pos[exc0[t] + q] = byte0[t] + c.exc_pos[q];
+        ds.exc_val[exc0[t] + q] = c.exc_val[q];
+      }
+    }
+    munmap(m, n);
+    ds.file_count.push_back(nr - rec0[0]);
     ds.file_len_sum.push_back(lsum);
   }
+}
+
+std::vector<uint8_t> unpack_codes(const Dataset &ds) {
+  std::vector<uint8_t> out(ds.bases());
+  for (size_t i = 0; i < ds.size(); i++) {
+    const uint32_t *w = ds.packed.data() + ds.pk_off[i];
+    for (uint64_t j = 0; j < ds.lengths[i]; j++) out[ds.seq_off[i] + j] = (uint8_t)((w[j / 16] >> (2 * (j % 16))) & 3);
+  }
+  for (size_t q = 0; q < ds.exc_pos.size(); q++) out[ds.exc_pos[q]] = ds.exc_val[q];
+  return out;
 }
 
 }  // namespace mc

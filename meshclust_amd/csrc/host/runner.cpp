@@ -143,8 +143,9 @@ RunResult run_pipeline(const Dataset &ds, mc_ctx *ctx, Options opt, bool upload,
   auto t0 = std::chrono::steady_clock::now();
   if (upload) {
     Scope s(rr.timer, "upload");
-    check(mc_load_sequences(ctx, ds.codes.data(), ds.seq_off.data(), ds.size(), ds.seg.data(), ds.seg_off.data()),
-          "mc_load_sequences");
+    check(mc_load_packed(ctx, ds.packed.data(), ds.pk_off.data(), ds.seq_off.data(), ds.size(), ds.exc_pos.data(),
+                         ds.exc_val.data(), ds.exc_pos.size(), ds.seg.data(), ds.seg_off.data()),
+          "mc_load_packed");
   }
   {
     Scope s(rr.timer, "kmer");
@@ -268,7 +269,7 @@ int meshclust_main(int argc, char **argv) {
     RunResult rr = run_pipeline(ds, ctx, opt);
     auto t1 = std::chrono::steady_clock::now();
     if (!opt.quiet) printf("Printing output\n");
-    write_clstr(opt.output, ds, rr.part);
+    write_clstr(opt.output, ds, rr.part, threads);
     double write_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();
     if (!opt.stats_json.empty()) write_stats(opt.stats_json, rr, parse_ms, write_ms);
     mc_ctx_destroy(ctx);

@@ -61,6 +61,18 @@ int mc_load_sequences(mc_ctx *c, const uint8_t *codes, const uint64_t *seq_off, 
   return MC_OK;
 }
 
+// the packed form of the host parser: unpacked here to the bytes the reference holds
+int mc_load_packed(mc_ctx *c, const uint32_t *packed, const uint64_t *pk_off, const uint64_t *seq_off, uint64_t n,
+                   const uint64_t *exc_pos, const uint8_t *exc_val, uint64_t nexc, const int32_t *seg,
+                   const uint64_t *seg_off) {
+  std::vector<uint8_t> codes(seq_off[n]);
+  for (uint64_t i = 0; i < n; i++)
+    for (uint64_t j = 0; j < seq_off[i + 1] - seq_off[i]; j++)
+      codes[seq_off[i] + j] = (uint8_t)((packed[pk_off[i] + j / 16] >> (2 * (j % 16))) & 3u);
+  for (uint64_t q = 0; q < nexc; q++) codes[exc_pos[q]] = exc_val[q];
+  return mc_load_sequences(c, codes.data(), seq_off, n, seg, seg_off);
+}
+
 static int hist_of(mc_ctx *c, uint64_t i, int k, std::vector<uint64_t> &h) {
   h.resize((size_t)1 << (2 * k));
   const uint8_t *s = c->codes.data() + c->seq_off[i];

@@ -67,6 +67,60 @@ def test_kmer_widths_match_oracle(eng):
             assert h.dtype == dt and np.array_equal(h.astype(np.uint64), want)
 
 
+@pytest.mark.parametrize("mean_len", [900, 9000])
+def test_kmer_all_k_and_table_modes_vs_oracle(eng, mean_len):
+    """K1's three table modes against the oracle: per-wave LDS tables (k <= 6), one shared LDS
+    table (k = 7), per-wave global tables (k >= 8); one wave per sequence (short) and the
+    waves of a workgroup sharing a sequence (mean length >= 4 kb).  Sequences with several
+    segments, an 'N' outside segments (impure: byte path) and lengths not a multiple of 16."""
+    rng = np.random.default_rng(11 + mean_len)
+    recs = []
+    for i in range(24):
+        L = int(rng.integers(mean_len // 2, mean_len * 3 // 2)) + (i % 16)
+        c = rng.integers(0, 4, size=L).astype(np.uint8)
+        if i % 3 == 0:
+            a = L // 3
+            c[a:a + 30] = 78  # 'N' run outside the segments
+            recs.append((c, [[0, a - 1], [a + 30, L - 1]]))
+        else:
+            recs.append((c, [[0, L - 1]]))
+    load_records(eng, recs)
+    for k in (1, 2, 5, 7, 8):
+        want = np.array([O.kmer_hist(c, s, k) for c, s in recs])
+        width = 1 if want.max() <= 255 else 2
+        assert eng.kmer_max(k) == int(want.max()), k
+        eng.kmer_build(k, width)
+        h, mags = eng.histograms()
+        assert np.array_equal(h.astype(np.uint64), want), k
+        assert np.array_equal(mags, want.sum(axis=1)), k
+
+
+def test_load_packed_equals_bytes(eng):
+    """mc_load_packed (2-bit words + exception bytes, the host parser's form) leaves the same
+    sequences on the device as mc_load_sequences: same histograms, same NW identities."""
+    rng = np.random.default_rng(12)
+    recs = []
+    for i in range(40):
+        L = int(rng.integers(20, 700))
+        c = rng.integers(0, 4, size=L).astype(np.uint8)
+        if i % 4 == 0:
+            c[L // 2:L // 2 + 12] = 78
+        recs.append((c, [[0, L // 2 - 1]] if i % 4 == 0 else [[0, L - 1]]))
+    load_records(eng, recs)
+    eng.kmer_build(3, 1)
+    h0, m0 = eng.histograms()
+    a = np.arange(40, dtype=np.uint32)
+    b = (a * 7 + 3) % 40
+    id0 = eng.nw_identity(a, b)
+    eng.load_packed([c for c, _ in recs], [s for _, s in recs])
+    eng.kmer_build(3, 1)
+    h1, m1 = eng.histograms()
+    assert np.array_equal(h0, h1) and np.array_equal(m0, m1)
+    id1 = eng.nw_identity(a, b)
+    for x, y in zip(id0, id1):
+        assert np.array_equal(x, y)
+
+
 def test_nw_golden(eng):
     g = np.load(fixtures.golden("nw.npz"))
     ident, ln, ids, sc = eng.nw_identity_raw(g["a"], g["a_off"], g["b"], g["b_off"])
