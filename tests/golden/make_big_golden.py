@@ -8,11 +8,15 @@ regenerates deterministically, and the canonical partition is stored compactly:
                    canonical partition, see canonical_digest), and for inputs up to
                    200k reads centre_of[i] = read id of the centre of read i's cluster.
 
-Partitions and centres of the reference are deterministic across thread counts (SURVEY.md
-§5; member and cluster order are not, and are not compared), so the reference runs with all
-cores.  Read ids come from the synthetic headers (">read{i} template_{t}").
+The reference runs with --threads 1: its OpenMP reductions break ties between equal values
+in thread-combine order (Trainer.cpp:38-40, 132-134; ClusterFactory.cpp:406-412), and at 100k
+reads its 8-thread run differs from its 1-thread run in 3 centres and 2 memberships (measured
+here).  The serial order is the reference's defined semantics (first maximum in get_close,
+first minimum in get_mean / closest), and the product restates it.  Read ids
+come from the synthetic headers (">read{i} template_{t}").
 
-Usage: python tests/golden/make_big_golden.py NAME [--threads T]      NAME in BIG
+Usage: python tests/golden/make_big_golden.py NAME [--threads T] [--reuse WALL_S]      NAME in BIG
+(--reuse: summarise an existing <workdir>/<NAME>.clstr of a reference run that took WALL_S)
 """
 import argparse
 import hashlib
@@ -86,8 +90,9 @@ def summary(clusters, n):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("name", choices=sorted(BIG))
-    ap.add_argument("--threads", type=int, default=os.cpu_count())
+    ap.add_argument("--threads", type=int, default=1)
     ap.add_argument("--workdir", default="/tmp/mc_big")
+    ap.add_argument("--reuse", type=float, default=None)
     a = ap.parse_args()
     gen, flags = BIG[a.name]
     os.makedirs(a.workdir, exist_ok=True)
@@ -96,10 +101,13 @@ def main():
         synth.generate(fa + ".tmp", *gen)
         os.replace(fa + ".tmp", fa)
     out = os.path.join(a.workdir, a.name + ".clstr")
-    t0 = time.time()
-    subprocess.run([REF, fa] + flags + ["--threads", str(a.threads), "--output", out], check=True,
-                   stdout=subprocess.DEVNULL)
-    wall = time.time() - t0
+    if a.reuse is not None:
+        wall = a.reuse
+    else:
+        t0 = time.time()
+        subprocess.run([REF, fa] + flags + ["--threads", str(a.threads), "--output", out], check=True,
+                       stdout=subprocess.DEVNULL)
+        wall = time.time() - t0
     s = summary(clusters_of(out), gen[0])
     np.savez_compressed(os.path.join(HERE, "cfg_%s.npz" % a.name), n=s["n"], clusters=s["clusters"],
                         centres=s["centres"], digest=s["digest"],
