@@ -167,7 +167,7 @@ int mc_ctx_destroy(mc_ctx *c) {
   (void)hipStreamSynchronize(c->stream);
   for (Buf *b : {&c->codes, &c->seq_off, &c->seg, &c->seg_off, &c->packed, &c->pk_off, &c->impure, &c->hist, &c->mag, &c->sumsq, &c->len, &c->order,
                  &c->alive, &c->members, &c->member_keys, &c->partials, &c->scan_dev, &c->flags_out, &c->s_a, &c->s_b,
-                 &c->s_c, &c->s_d, &c->s_e, &c->s_f, &c->s_g, &c->hs, &c->mag_s, &c->sumsq_s, &c->len_s, &c->ticket,
+                 &c->s_c, &c->s_d, &c->s_e, &c->s_f, &c->s_g, &c->s_h, &c->hs, &c->mag_s, &c->sumsq_s, &c->len_s, &c->ticket,
                  &c->msum, &c->ident_s, &c->al_a, &c->al_b, &c->al_out, &c->acc_out})
     release(*b);
   if (c->h_scan) (void)hipHostFree(c->h_scan);
@@ -751,10 +751,35 @@ int mc_accumulate(mc_ctx *c, const uint32_t *bin_lo, const uint64_t *bounds, uin
     stats[1] = out[2];
     for (int i = 0; i < 3; i++) stats[2 + i] = out[5 + i] / 100;  // controller phases, 100 MHz ticks -> us
   }
-  if (getenv("MC_ACCUM_PROFILE"))
-    fprintf(stderr, "[accum] steps %llu window %.3f wait %.3f collect %.3f (reduce %.3f gather+kill %.3f sums %.3f closest %.3f) ms\n",
-            (unsigned long long)out[1], out[5] / 1e5, out[6] / 1e5, out[7] / 1e5, out[8] / 1e5, out[9] / 1e5, out[10] / 1e5,
-            out[11] / 1e5);
+  if (getenv("MC_ACCUM_PROFILE")) {
+    fprintf(stderr, "[accum] steps %llu window %.3f (centre data %.3f window %.3f record %.3f) wait %.3f collect %.3f "
+            "(reduce %.3f gather+kill %.3f sums+mean %.3f closest %.3f) ms\n",
+            (unsigned long long)out[1], out[5] / 1e5, out[12] / 1e5, out[13] / 1e5, out[14] / 1e5, out[6] / 1e5,
+            out[7] / 1e5, out[8] / 1e5, out[9] / 1e5, out[10] / 1e5, out[11] / 1e5);
+    if (atoi(getenv("MC_ACCUM_PROFILE")) >= 2 && c->s_h.p) {
+      // per step (first 4096): record published -> seen by the last active worker -> its scan
+      // done -> its partial stored -> controller has every partial -> collect done
+      std::vector<uint64_t> tr(4096 * 8);
+      MCG_CHECK(hipMemcpy(tr.data(), c->s_h.p, tr.size() * 8, hipMemcpyDeviceToHost));
+      double a[5] = {0, 0, 0, 0, 0};
+      uint64_t cnt = 0, nact = 0;
+      for (uint64_t st = 1; st < 4096; st++) {
+        const uint64_t *t = &tr[st * 8];
+        if (!t[0] || !t[2] || !t[5] || !t[6]) continue;
+        a[0] += (double)(int64_t)(t[2] - t[0]);
+        a[1] += (double)(int64_t)(t[3] - t[2]);
+        a[2] += (double)(int64_t)(t[4] - t[3]);
+        a[3] += (double)(int64_t)(t[5] - t[4]);
+        a[4] += (double)(int64_t)(t[6] - t[5]);
+        nact += t[7];
+        cnt++;
+      }
+      if (cnt)
+        fprintf(stderr, "[accum trace] %llu steps, avg us: publish->seen %.2f scan %.2f ->partial %.2f ->all seen %.2f "
+                "collect %.2f; active WGs %.1f\n", (unsigned long long)cnt, a[0] / cnt / 100, a[1] / cnt / 100,
+                a[2] / cnt / 100, a[3] / cnt / 100, a[4] / cnt / 100, (double)nact / cnt);
+    }
+  }
   return MC_OK;
 }
 

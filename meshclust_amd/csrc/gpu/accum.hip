@@ -3,39 +3,35 @@
 //
 // Every step of accumulation depends on the previous one (the next centre is the member
 // closest to the cluster's mean), so the phase is a chain of ~2 steps per cluster, each a
-// scan of the bvec window.  Driving that chain from the host costs a launch and a PCIe round
-// trip per step; here the chain never leaves the GPU:
+// scan of the bvec window.  The chain never leaves the GPU:
 //
-//   WG 0 (controller)   keeps the bvec in LDS -- an alive bitmap over static positions plus
-//                       per-bin alive counts -- and runs bvec::get_range / the bvec_iterator
-//                       window (bvec_core.hpp, the closed forms checked against the host
-//                       restatement), pop / erase / remove_available, the cluster's running
-//                       integer column sums, get_mean + Trainer::closest, and the cluster
-//                       bookkeeping; it publishes each step's (centre, S, E) and collects the
-//                       step's result.
-//   all WGs             scan the window: Trainer::get_close (Trainer.cpp:34-114) on the
-//                       chunk-major static layout, one lane per candidate, centre in LDS;
-//                       similar candidates are killed and listed per workgroup, combo-0's
-//                       first maximum is reduced per workgroup.
+//   WG 0 (controller)   keeps the bvec -- an alive bitmap over static positions (LDS, or
+//                       global memory for very large n) plus per-bin alive counts with a
+//                       Fenwick tree -- and runs bvec::get_range / the bvec_iterator window
+//                       (bvec_core.hpp: four nearest-alive queries when both edge bins hold
+//                       alive elements, the general closed forms otherwise), pop / erase /
+//                       remove_available, the cluster's integer column sums, get_mean +
+//                       Trainer::closest over a member cache in LDS, and publishes each step.
+//   every WG            scans the chunks of the window it owns: Trainer::get_close
+//                       (Trainer.cpp:34-114), one lane per candidate, centre in LDS; similar
+//                       candidates are killed and handed over with their histogram rows, the
+//                       first maximum of combo 0 is reduced per workgroup.
 //
-// Static chunk c (NT positions) is always scanned by workgroup c mod G, and G is a multiple
-// of 8, so a chunk always lands on the same XCD and its rows stay in that XCD's L2; the alive
-// flags of a workgroup's chunks live in its own LDS.
+// Static chunk c (NT positions) always belongs to workgroup c mod G, and G is a multiple of the
+// 8 XCDs, so a chunk stays on one XCD.  When every workgroup owns at most RES chunks (n up to
+// RES * G * NT: 131k reads per chunk slot on 256 CUs) the chunks' histogram rows are loaded
+// into registers once and stay there for the whole phase: a step then reads no candidate
+// bytes from memory at all.  Larger n streams the window's rows from HBM every step.
 //
-// Hand-offs carry only a few words, so they use sc1 stores and loads (relaxed agent-scope
-// atomics: L1 bypassed, coherent across XCDs) with a drain before each signal instead of
-// release/acquire fences (MI355X_MICROARCH.md hand-off table, first row).  The signal words
-// carry the step number in their upper half, so a reader polls the payload itself and one
-// L2 round trip per hand-off disappears:
-//   controller -> workers   a step record in a ring {centre, S, E, kill-log length}, each word
-//                           tagged with the step (after a drain of the kill log: pops / erases
-//                           are appended to a log that owners apply before their next scan);
-//                           workers poll the next step's slot; `go` = step only serves a
-//                           workgroup that fell a whole ring behind
-//   workers -> controller   flagged positions, drained, then a 4-word {max, position, count}
-//                           partial, every word tagged with the step, polled by the controller
-// Only the workgroups owning a chunk of the window take part in a step.  Every spin has a
-// deadline, so a fault cannot leave a wave spinning forever (error 99).
+// Hand-offs are 8-byte {step tag, data} granules written with sc1 stores and read with sc1
+// loads, so a reader that sees every tag equal to the step it waits for holds an untorn
+// record without a fence (MI355X_MICROARCH.md, hand-off table row 1; data-tagged granules as
+// in handoff-1to1):
+//   controller -> workers   the step record: centre row + magnitudes, window S..E, kill-log
+//                           length and its last KINL entries (pops / erases)
+//   workers -> controller   the flagged candidates (position, magnitudes, row: sc1 stores,
+//                           drained), then a 5-granule partial {max, position, flagged, scanned}
+// Every spin has a deadline (error 99: never a hang).
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
@@ -50,21 +46,16 @@ namespace {
 constexpr int NT = 512;
 constexpr int NW = NT / 64;
 constexpr uint32_t NONE = 0xffffffffu;
-constexpr uint32_t MCAP = 1024;  // members of the current cluster mirrored in LDS
-constexpr uint32_t RING = 64;    // step records kept for workgroups that read them late
+constexpr uint64_t NONE64 = ~0ull;
+constexpr uint32_t RING = 64;          // step records kept for workgroups that read them late
+constexpr uint32_t TRACE_STEPS = 4096;
+constexpr int KINL = 4;                // kill-log entries carried inline in a step record
+constexpr int REC_HDR = 14;            // centre, S, E, kn, KINL kills, mag / sumsq / len (2 each)
+constexpr int PART_G = 8;              // granules per partial (5 used)
 
-
-// A workgroup's result for one step: {val high half, val low half, position, flagged count},
-// each word tagged with the step in its upper 32 bits, so the controller polls the words
-// themselves (no arrival counter) and accepts them when all four carry the step.
-struct AccPartial {
-  uint64_t w[4];
-};
-
-// Static part of a centre's bvec window (bvec::get_range, bvec.cpp:245-278), per point id:
-// the window lengths, the bins index_of picks, and how many static positions of those bins
-// are shorter than (or not longer than) the window lengths.  Only alive counts change during
-// accumulation, so the controller turns these into inner_index_of's ranks with LDS popcounts.
+// Static part of a centre's bvec window (bvec::get_range, bvec.cpp:245-278), per static
+// position: the window lengths, the bins index_of picks, and how many static positions of
+// those bins are shorter than (or not longer than) the window lengths.
 struct WinTab {
   uint64_t bl, el;          // (uint64_t)(len * sim), (uint64_t)(len / sim)
   uint32_t fb, bb;          // index_of(bl).low, index_of(el).high
@@ -73,7 +64,7 @@ struct WinTab {
 };
 
 struct AccArgs {
-  // chunk-major static layout (scan.hip build_static) and id-major rows (centre)
+  // chunk-major static layout (scan.hip build_static)
   const uint4 *hs;
   uint64_t npad;
   int nch, B;
@@ -81,42 +72,38 @@ struct AccArgs {
   // bvec structure
   uint64_t N;
   uint32_t nb;
-  const uint32_t *bin_lo;    // nb + 1 static starts
-  const uint64_t *bounds;    // nb begin_bounds
-  double sim;
-  const WinTab *wtab;        // per static position
-  // hand-off (every handed-off word is stored and loaded with sc1 accesses, see below)
-  uint64_t *ring;   // RING step records of 4 words
-  uint32_t *klog;   // static positions killed by the controller (pop / erase), append-only
-  uint32_t *go;     // latest published step (for a workgroup that fell RING steps behind)
-  AccPartial *partials;
-  uint32_t *flist;  // G * fcap
+  const uint32_t *bin_lo;  // nb + 1 static starts
+  const uint64_t *bounds;  // nb begin_bounds
+  const WinTab *wtab;      // per static position
+  uint32_t *gbits;         // alive bitmap in global memory (n too large for LDS), else null
+  // hand-off
+  uint64_t *ring;  // RING records of rec_g granules
+  uint32_t rec_g;
+  uint32_t *klog;      // static positions killed by the controller (pop / erase), append-only
+  uint32_t *go;        // latest published step (for a workgroup that fell RING steps behind)
+  uint64_t *partials;  // G * PART_G granules
+  uint32_t *fpos;      // worker w's flagged positions at w * fcap
+  uint64_t *finfo;     // ... their mag / sumsq / len (3 words each)
+  uint4 *frow;         // ... their rows (nch chunks each)
   uint64_t fcap;
+  int res;        // chunks per worker whose rows live in its LDS (0: rows stream from memory)
+  uint32_t mrow;  // member cache entries (LDS)
   // output
-  uint32_t *mem_pos;   // N: member static positions, cluster after cluster
-  uint64_t *mkeys;     // N: (step << 32 | pos), 0 for a cluster's seed
-  uint32_t *cl_centre; // N: static position of each cluster's centre
-  uint64_t *cl_off;    // N + 1
-  uint64_t *out;       // [0] clusters [1] steps [2] candidates [3] error [4] members
-  uint64_t budget;     // longest wait for one hand-off, s_memrealtime ticks (100 MHz)
-  int prof;            // controller phase timers (MC_ACCUM_PROFILE)
+  uint32_t *mem_pos;    // N: member static positions, cluster after cluster
+  uint64_t *mkeys;      // N: (step << 32 | pos), 0 for a cluster's seed
+  uint32_t *cl_centre;  // N: static position of each cluster's centre
+  uint64_t *cl_off;     // N + 1
+  uint64_t *out;        // [0] clusters [1] steps [2] candidates [3] error [4] members, timers
+  uint64_t budget;      // longest wait for one hand-off, s_memrealtime ticks (100 MHz)
+  int prof;             // controller phase timers (MC_ACCUM_PROFILE)
+  uint64_t *trace;      // MC_ACCUM_PROFILE=2: per-step timestamps, TRACE_STEPS x 8
 };
 
-struct Red {  // LDS scratch for block-wide reductions and scans
-  uint64_t a[NW], b[NW];
-  double d[NW];
-  uint64_t r0, r1;
-};
+__device__ __forceinline__ uint64_t now() { return __builtin_amdgcn_s_memrealtime(); }
+__device__ __forceinline__ bool timed_out(const AccArgs &A, uint64_t t0) { return now() - t0 > A.budget; }
 
-__device__ __forceinline__ bool timed_out(const AccArgs &A, uint64_t t0) {
-  return __builtin_amdgcn_s_memrealtime() - t0 > A.budget;
-}
-
-// Hand-off primitives.  Relaxed agent-scope atomics lower to global loads/stores with sc1:
-// they bypass the CU's L1 and are coherent across XCDs without release/acquire fences when
-// every handed-off word is written this way, each storing wave drains (vmcnt(0)) before
-// the signal and every load of the words is also sc1 (MI355X_MICROARCH.md, hand-off table,
-// first row).  The drain is inline asm so the compiler cannot drop it.
+// Hand-off primitives: relaxed agent-scope atomics lower to global loads / stores with sc1
+// (L1 bypassed, coherent across XCDs); the drain is inline asm so the compiler keeps it.
 __device__ __forceinline__ void st64(uint64_t *p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -129,54 +116,48 @@ __device__ __forceinline__ uint64_t ld64(const uint64_t *p) {
 __device__ __forceinline__ uint32_t ld32(const uint32_t *p) {
   return __hip_atomic_load(const_cast<uint32_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ void drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-
-// exclusive prefix of v over threads (thread order); *total = sum
-__device__ uint64_t block_excl_scan(uint64_t v, uint64_t *total, Red &R) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  uint64_t inc = v;
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint64_t u = shfl64(inc, lane >= o ? lane - o : lane);
-    if (lane >= o) inc += u;
-  }
-  __syncthreads();
-  if (lane == 63) R.b[w] = inc;
-  __syncthreads();
-  uint64_t before = 0, tot = 0;
-  for (int i = 0; i < NW; i++) {
-    if (i < w) before += R.b[i];
-    tot += R.b[i];
-  }
-  __syncthreads();
-  *total = tot;
-  return before + inc - v;
+__device__ __forceinline__ void st128(uint4 *p, const uint4 &v) {
+  uint64_t *q = reinterpret_cast<uint64_t *>(p);
+  st64(q, ((uint64_t)v.y << 32) | v.x);
+  st64(q + 1, ((uint64_t)v.w << 32) | v.z);
 }
+__device__ __forceinline__ uint4 ld128(const uint4 *p) {
+  const uint64_t *q = reinterpret_cast<const uint64_t *>(p);
+  const uint64_t a = ld64(q), b = ld64(q + 1);
+  return make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
+}
+__device__ __forceinline__ void drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ uint64_t gran(uint32_t tag, uint32_t data) { return ((uint64_t)tag << 32) | data; }
 
 __device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
   for (int o = 32; o >= 1; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o, 64);
   return v;
 }
 
-// The bvec held by the controller workgroup: LDS bitmap of alive static positions, per-bin
-// alive counts with a Fenwick tree over them, bin starts and begin bounds (bvec.cpp's bins
-// after insert_finalize).  Every query is answered by each wave on its own from LDS (binary
-// searches, Fenwick walks, one-wave popcount scans), so a query costs no workgroup barrier;
+__device__ __forceinline__ bool better(double v, uint64_t p, double bv, uint64_t bp) {
+  return v > bv || (v == bv && p < bp);
+}
+
+// The bvec held by the controller workgroup: bitmap of alive static positions (LDS or
+// global), per-bin alive counts with a Fenwick tree over them, bin starts and begin bounds
+// (bvec.cpp's bins after insert_finalize).  Queries are answered by each wave on its own;
 // callers keep queries uniform and put a barrier between kills and the next query.  The
-// O(log) forms are checked against the host bvec in tests/native/bvec_check.cpp (FastAcc).
+// closed forms are checked against the host bvec in tests/native/bvec_check.cpp.
 struct DevBvec {
   uint32_t *bits;
+  bool gb;  // bits in global memory: sc1 loads (the atomics that clear bits act in L2)
   uint32_t *cn;
-  uint32_t *fw;          // Fenwick tree, fw[1..nb]
-  const uint32_t *lo;    // LDS copy, nb + 1
-  const uint64_t *bnd;   // LDS copy, nb
-  const uint64_t *plen;  // global: length by static position (non-decreasing inside a bin)
-  uint64_t nb, lg;       // lg: highest power of two <= nb
-  WinTab h{~0ull, ~0ull, ~0u, ~0u, 0, 0, 0, 0};  // the current centre's static window data
+  uint32_t *fw;
+  const uint32_t *lo;
+  const uint64_t *bnd;
+  const uint64_t *plen;  // global: length by static position
+  uint64_t nb, lg;
+  WinTab h{~0ull, ~0ull, ~0u, ~0u, 0, 0, 0, 0};
 
   __device__ uint64_t nbins() const { return nb; }
-  // accessor interface of bvec_core.hpp
+  __device__ uint32_t word(uint64_t w) const { return gb ? ld32(bits + w) : bits[w]; }
   __device__ uint64_t cnt(uint64_t b) { return b < nb ? cn[b] : 0; }
-  __device__ void index_of(uint64_t point, uint64_t *plow, uint64_t *phigh) {  // bvec.cpp:38-53
+  __device__ void index_of(uint64_t point, uint64_t *plow, uint64_t *phigh) {
     bv_index_of_sorted(bnd, nb, point, plow, phigh);
   }
   __device__ uint64_t prefix(uint64_t b) { return bv_fw_prefix(fw, b < nb ? b : nb); }
@@ -196,11 +177,11 @@ struct DevBvec {
     return (int64_t)b;
   }
   __device__ uint32_t masked_word(uint64_t w, uint64_t p0, uint64_t p1) const {
-    uint32_t word = bits[w];
+    uint32_t x = word(w);
     const uint64_t s = w << 5;
-    if (s < p0) word &= ~0u << (p0 - s);
-    if (s + 32 > p1) word &= (p1 - s) >= 32 ? ~0u : ((1u << (p1 - s)) - 1u);
-    return word;
+    if (s < p0) x &= ~0u << (p0 - s);
+    if (s + 32 > p1) x &= (p1 - s) >= 32 ? ~0u : ((1u << (p1 - s)) - 1u);
+    return x;
   }
   __device__ uint64_t alive_in(uint64_t p0, uint64_t p1) const {  // alive positions in [p0, p1)
     if (p0 >= p1) return 0;
@@ -208,6 +189,37 @@ struct DevBvec {
     uint32_t n = 0;
     for (uint64_t w = w0 + (threadIdx.x & 63); w < w1; w += 64) n += (uint32_t)__popc(masked_word(w, p0, p1));
     return wave_sum32(n);
+  }
+  // first / last alive position of [p, q) (one wave, uniform result), ~0 if none
+  __device__ uint64_t next_alive(uint64_t p, uint64_t q) const {
+    const int lane = threadIdx.x & 63;
+    for (uint64_t base = p >> 5; p < q && (base << 5) < q; base += 64) {
+      const uint64_t w = base + (uint64_t)lane;
+      const uint32_t x = (w << 5) < q ? masked_word(w, p, q) : 0u;
+      const uint64_t bal = __ballot(x != 0);
+      if (bal) {
+        const int L = __builtin_ctzll(bal);
+        const uint32_t y = (uint32_t)__shfl((int)x, L, 64);
+        return ((base + (uint64_t)L) << 5) + (uint64_t)__builtin_ctz(y);
+      }
+    }
+    return NONE64;
+  }
+  __device__ uint64_t prev_alive(uint64_t p, uint64_t q) const {
+    if (p >= q) return NONE64;
+    const int lane = threadIdx.x & 63;
+    const int64_t wfirst = (int64_t)(p >> 5);
+    for (int64_t top = (int64_t)((q - 1) >> 5); top >= wfirst; top -= 64) {
+      const int64_t w = top - lane;
+      const uint32_t x = w >= wfirst ? masked_word((uint64_t)w, p, q) : 0u;
+      const uint64_t bal = __ballot(x != 0);
+      if (bal) {
+        const int L = __builtin_ctzll(bal);  // lowest lane = highest word
+        const uint32_t y = (uint32_t)__shfl((int)x, L, 64);
+        return ((uint64_t)(top - L) << 5) + (uint64_t)(31 - __builtin_clz(y));
+      }
+    }
+    return NONE64;
   }
   // first position of [a, z) whose length is >= L (strict: > L)
   __device__ uint64_t len_bound(uint64_t a, uint64_t z, uint64_t L, bool strict) const {
@@ -237,8 +249,8 @@ struct DevBvec {
     const uint64_t w0 = p0 >> 5, w1 = (p1 + 31) >> 5;
     for (uint64_t base = w0; base < w1; base += 64) {
       const uint64_t w = base + lane;
-      const uint32_t word = w < w1 ? masked_word(w, p0, p1) : 0u;
-      const uint32_t pc = (uint32_t)__popc(word);
+      const uint32_t x = w < w1 ? masked_word(w, p0, p1) : 0u;
+      const uint32_t pc = (uint32_t)__popc(x);
       uint32_t inc = pc;
       for (int o = 1; o < 64; o <<= 1) {
         const uint32_t u = (uint32_t)__shfl_up((int)inc, o, 64);
@@ -248,17 +260,17 @@ struct DevBvec {
       if (c < tot) {
         const uint64_t hit = __ballot(inc > c);
         const int L = __builtin_ctzll(hit);
-        uint32_t x = (uint32_t)__shfl((int)word, L, 64);
+        uint32_t y = (uint32_t)__shfl((int)x, L, 64);
         const uint32_t before = (uint32_t)__shfl((int)(inc - pc), L, 64);
-        for (uint64_t k = c - before; k > 0; k--) x &= x - 1;
-        return ((base + (uint64_t)L) << 5) + (uint64_t)__builtin_ctz(x);
+        for (uint64_t k = c - before; k > 0; k--) y &= y - 1;
+        return ((base + (uint64_t)L) << 5) + (uint64_t)__builtin_ctz(y);
       }
       c -= tot;
     }
-    return ~0ull;
+    return NONE64;
   }
   __device__ uint64_t bin_of(uint64_t p) const {  // single-thread binary search
-    uint64_t a = 0, z = nb;  // lo[a] <= p < lo[z]
+    uint64_t a = 0, z = nb;                        // lo[a] <= p < lo[z]
     while (z - a > 1) {
       const uint64_t m = (a + z) / 2;
       if (lo[m] <= p) a = m;
@@ -273,37 +285,17 @@ struct DevBvec {
     atomicSub(&cn[b], 1u);
     for (uint64_t i = b + 1; i <= nb; i += i & (~i + 1)) atomicSub(&fw[i], 1u);
   }
-  __device__ void invalidate() {}
 };
 
-// Column sums of rows[0..M) (static positions) added into sum[0..B) (LDS).  Thread (chunk c,
-// row group g) accumulates chunk c of rows g, g + ng, ... in registers and adds its totals once,
-// so the LDS atomics per step do not grow with the number of new members.
-template <typename T>
-__device__ void add_rows_acc(const RowRef &R, const uint32_t *rows, uint32_t M, int nch, uint64_t *sum) {
-  constexpr int per = 16 / (int)sizeof(T);
-  const int ng = nch < NT ? NT / nch : 1;
-  for (int item = threadIdx.x; item < nch * ng; item += NT) {
-    const int c = item % nch, grp = item / nch;
-    uint64_t a[per];
-#pragma unroll
-    for (int e = 0; e < per; e++) a[e] = 0;
-#pragma unroll 4
-    for (uint32_t q = (uint32_t)grp; q < M; q += (uint32_t)ng) {
-      const uint4 v = R.chunk(rows[q], c);
-      const T *pv = reinterpret_cast<const T *>(&v);
-#pragma unroll
-      for (int e = 0; e < per; e++) a[e] += pv[e];
-    }
-#pragma unroll
-    for (int e = 0; e < per; e++)
-      if (a[e]) atomicAdd((unsigned long long *)&sum[c * per + e], (unsigned long long)a[e]);
-  }
-}
-
-__device__ __forceinline__ bool better(double v, uint64_t p, double bv, uint64_t bp) {
-  return v > bv || (v == bv && p < bp);
-}
+// The controller's cache of the current cluster's first members (LDS)
+struct MemberCache {
+  uint32_t *pos;
+  uint64_t *key;
+  uint64_t *info;  // 3 per entry: mag, sumsq, len
+  WinTab *wt;
+  uint4 *row;      // rp chunks per entry (nch + 1: the pad spreads rows over the LDS banks)
+  int rp;
+};
 
 __device__ uint64_t lower_len(const uint64_t *len_s, uint64_t a, uint64_t z, uint64_t L, bool strict) {
   while (a < z) {
@@ -336,52 +328,332 @@ __global__ __launch_bounds__(256) void wintab_kernel(uint64_t n, const uint64_t 
   }
 }
 
+// One candidate against the centre held in LDS (feat->compute(*pt, *p) of get_close):
+// returns the decision, *cv = combo 0.
 template <typename T>
-__global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
-  extern __shared__ __attribute__((aligned(16))) uint4 dyn[];
-  __shared__ Red R;
-  __shared__ uint32_t s_flag[NT];
-  __shared__ uint32_t s_mpos[MCAP];  // current cluster: static positions and tie keys (first MCAP)
-  __shared__ uint64_t s_mkey[MCAP];
-  __shared__ uint32_t s_wcnt[NW];
+__device__ __forceinline__ int classify_cand(const Acc<T> &acc, const PInfo &pi, const PInfo &pc, int B,
+                                             const DevClassifier &C, double *cv) {
+  const PS s = acc.finish(pi.mag, pc.mag);
+  double raw[MC_MAX_SINGLE];
+#pragma unroll
+  for (int i = 0; i < MC_MAX_SINGLE; i++) raw[i] = i < C.c.n_single ? raw_fast(C.c.lookup[i], s, pi, pc, B) : 0.0;
+  return classify_raw(C, raw, cv, nullptr);
+}
+
+// ============================================================================================
+// Workers (WG 1 .. G-1): chunk c of the static order belongs to worker c mod (G - 1).  With
+// A.res > 0 the rows of a worker's chunks are loaded into its LDS once (chunk-major, so lane t
+// reads row t's chunks conflict-free) and never read from memory again.
+// LDS: record words | alive flags (fcap) | resident rows (res * nch * NT uint4)
+// ============================================================================================
+template <typename T, int NCH>
+__device__ __forceinline__ void worker(const AccArgs &A, const DevClassifier &C, uint4 *dyn) {
   __shared__ double s_bv[NW];
   __shared__ uint64_t s_bp[NW];
-  __shared__ uint32_t s_go;
-  __shared__ uint64_t s_rec[4];
+  __shared__ uint32_t s_nfl, s_nscan, s_go;
   __shared__ int s_abort;
-  const uint32_t G = gridDim.x, g = blockIdx.x;
+  constexpr int NC = NCH > 0 ? NCH : 1;
+  const uint32_t GW = gridDim.x - 1, w = blockIdx.x - 1;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  uint4 *clds = dyn;  // centre chunks
-  const RowRef Rs{A.hs, 1, A.npad};
+  const int nch = NCH > 0 ? NCH : A.nch;
+  const int rec_words = (int)A.rec_g;
+  uint32_t *srec = reinterpret_cast<uint32_t *>(dyn);
+  const uint4 *clds = dyn;  // centre row = record words 0 .. 4 nch
+  uint8_t *lal = reinterpret_cast<uint8_t *>(dyn + (rec_words + 3) / 4);
+  uint4 *lrow = reinterpret_cast<uint4 *>(lal + (A.fcap + 15) / 16 * 16);
+  // alive flags of the positions this worker owns (chunks w, w + GW, ...), local index
+  // (chunk / GW) * NT + offset: flagged candidates are cleared by their owner thread, and so
+  // are the controller's pops and erases, which arrive with the step records
+  for (uint64_t i = threadIdx.x; i < A.fcap; i += NT) lal[i] = 1;
+  const int res = A.res;
+  uint64_t rmag[2] = {0, 0}, rsq[2] = {0, 0}, rlen[2] = {0, 0};  // resident magnitudes (res <= 2 kept here)
+  for (int i = 0; i < res; i++) {
+    const uint64_t pos = ((uint64_t)w + (uint64_t)i * GW) * NT + threadIdx.x;
+    for (int k = 0; k < nch; k++)
+      lrow[((uint64_t)i * nch + k) * NT + threadIdx.x] = pos < A.N ? A.hs[(uint64_t)k * A.npad + pos] : make_uint4(0, 0, 0, 0);
+    if (i < 2 && pos < A.N) {
+      rmag[i] = A.mag_s[pos];
+      rsq[i] = A.sumsq_s[pos];
+      rlen[i] = A.len_s[pos];
+    }
+  }
+  if (threadIdx.x == 0) s_abort = 0;
+  __syncthreads();
+  uint32_t kcur = 0, seen = 0;
+  for (;;) {
+    // ---- wait for the next step's record (wave 0) --------------------------------------
+    if (wv == 0) {
+      const uint64_t t0 = now();
+      const uint32_t want = seen + 1;
+      int state = 0;  // 0 waiting, 1 got it, 2 abort
+      uint32_t got = want;
+      // steps are published in order: poll the next step's slot itself (its granules carry
+      // the step); a worker that finds the slot rewritten for a later step fell RING steps
+      // behind and catches up through `go`
+      bool late = false;
+      const uint64_t *rn = A.ring + (uint64_t)(want % RING) * A.rec_g;
+      for (uint32_t it = 1;; it++) {
+        bool ok = true, ahead = false;
+        for (int j = lane; j < rec_words; j += 64) {
+          const uint64_t x = ld64(rn + j);
+          const uint32_t t = (uint32_t)(x >> 32);
+          ok &= t == want;
+          ahead |= (int32_t)(t - want) > 0;
+          srec[j] = (uint32_t)x;
+        }
+        if (__ballot(!ok) == 0) {
+          state = 1;
+          break;
+        }
+        if (__ballot(ahead) != 0) {
+          late = true;
+          break;
+        }
+        if ((it & 255) == 0 && timed_out(A, t0)) {
+          state = 2;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      while (late && state == 0) {
+        uint32_t v = 0;
+        if (lane == 0) {
+          for (uint32_t it = 1; (v = ld32(A.go)) == seen; it++) {
+            if ((it & 255) == 0 && timed_out(A, t0)) break;
+            __builtin_amdgcn_s_sleep(1);
+          }
+        }
+        v = (uint32_t)__shfl((int)v, 0, 64);
+        if (v == seen) {
+          state = 2;
+          break;
+        }
+        const uint64_t *r = A.ring + (uint64_t)(v % RING) * A.rec_g;
+        bool ok = true;
+        for (int j = lane; j < rec_words; j += 64) {
+          const uint64_t x = ld64(r + j);
+          ok &= (uint32_t)(x >> 32) == v;
+          srec[j] = (uint32_t)x;
+        }
+        if (__ballot(!ok) == 0) {
+          state = 1;
+          got = v;
+        }
+        // else: that slot is being rewritten for a later step: read `go` again
+      }
+      if (lane == 0) {
+        s_abort = state == 2;
+        s_go = got;
+      }
+    }
+    __syncthreads();
+    if (s_abort) {
+      if (threadIdx.x == 0) atomicMax((unsigned long long *)&A.out[3], 99ull);
+      return;
+    }
+    seen = s_go;
+    uint64_t t_seen = 0;
+    if (A.trace && threadIdx.x == 0) t_seen = now();
+    const uint32_t *hdr = srec + 4 * nch;
+    if (hdr[0] == NONE) return;  // accumulation finished
+    const uint64_t P_S = hdr[1], P_E = hdr[2];
+    const uint32_t kend = hdr[3];
+    const PInfo pc{(uint64_t)hdr[4 + KINL] | ((uint64_t)hdr[5 + KINL] << 32),
+                   (uint64_t)hdr[6 + KINL] | ((uint64_t)hdr[7 + KINL] << 32),
+                   (uint64_t)hdr[8 + KINL] | ((uint64_t)hdr[9 + KINL] << 32)};
+    // the controller's kills since the last record applied here: each thread clears the
+    // flags of the positions it owns (offset = its thread index), so no barrier is needed
+    {
+      const uint32_t kinl0 = kend > (uint32_t)KINL ? kend - KINL : 0;
+      for (uint32_t e = kcur; e < kend; e++) {
+        const uint32_t p = e >= kinl0 ? hdr[4 + KINL - (kend - e)] : ld32(A.klog + e);
+        const uint64_t ch = p / NT;
+        if (ch % GW == w && (p % NT) == (uint32_t)threadIdx.x) lal[(ch / GW) * NT + threadIdx.x] = 0;
+      }
+      kcur = kend;
+    }
+    // ---- the chunks of the window this worker owns: Trainer::get_close ----------------
+    const uint64_t c0 = P_S / NT, c1 = P_E / NT;
+    const uint32_t nact = (uint32_t)(c1 - c0 + 1 < (uint64_t)GW ? c1 - c0 + 1 : (uint64_t)GW);
+    const uint32_t mine = (w + GW - (uint32_t)(c0 % GW)) % GW;
+    if (mine >= nact) continue;
+    if (threadIdx.x == 0) {
+      s_nfl = 0;
+      s_nscan = 0;
+    }
+    __syncthreads();
+    double best_v = -1.0;
+    uint64_t best_p = NONE64;
+    uint32_t nscan = 0;
+    const uint64_t base = (uint64_t)w * A.fcap;
+    // a slot of this worker's flagged list; position and magnitudes (the caller stores the row)
+    auto flag_slot = [&](uint64_t pos, const PInfo &pi) -> uint64_t {
+      const uint64_t slot = base + atomicAdd(&s_nfl, 1u);
+      st32(A.fpos + slot, (uint32_t)pos);
+      st64(A.finfo + slot * 3 + 0, pi.mag);
+      st64(A.finfo + slot * 3 + 1, pi.sumsq);
+      st64(A.finfo + slot * 3 + 2, pi.len);
+      return slot;
+    };
+    for (uint64_t ch = c0 + mine; ch <= c1; ch += GW) {
+      const uint64_t li = ch / GW;  // local chunk index
+      const uint64_t pos = ch * NT + threadIdx.x;
+      uint8_t *la = lal + li * NT + threadIdx.x;
+      if (!(pos >= P_S && pos <= P_E && *la)) continue;
+      nscan++;
+      Acc<T> acc;
+      double cv;
+      if ((int64_t)li < res) {  // resident rows (LDS)
+        const uint4 *rr = lrow + li * (uint64_t)nch * NT + threadIdx.x;
+        if constexpr (NCH > 0) {
+#pragma unroll
+          for (int k = 0; k < NC; k++) acc.add(rr[(uint64_t)k * NT], clds[k]);
+        } else {
+          for (int k = 0; k < nch; k++) acc.add(rr[(uint64_t)k * NT], clds[k]);
+        }
+        const PInfo pi = li < 2 ? PInfo{rmag[li], rsq[li], rlen[li]} : PInfo{A.mag_s[pos], A.sumsq_s[pos], A.len_s[pos]};
+        const int d = classify_cand<T>(acc, pi, pc, A.B, C, &cv);
+        if (d) {
+          *la = 0;
+          const uint64_t slot = flag_slot(pos, pi);
+          for (int k = 0; k < nch; k++) st128(A.frow + slot * nch + k, rr[(uint64_t)k * NT]);
+        }
+      } else {  // streaming: the rows come from memory
+        const uint4 *col = A.hs + pos;
+        if constexpr (NCH > 0) {
+          uint4 v[NC];
+#pragma unroll
+          for (int k = 0; k < NC; k++) v[k] = col[(uint64_t)k * A.npad];
+          const PInfo pi{A.mag_s[pos], A.sumsq_s[pos], A.len_s[pos]};
+#pragma unroll
+          for (int k = 0; k < NC; k++) acc.add(v[k], clds[k]);
+          const int d = classify_cand<T>(acc, pi, pc, A.B, C, &cv);
+          if (d) {
+            *la = 0;
+            const uint64_t slot = flag_slot(pos, pi);
+#pragma unroll
+            for (int k = 0; k < NC; k++) st128(A.frow + slot * NC + k, v[k]);
+          }
+        } else {
+#pragma unroll 8
+          for (int k = 0; k < nch; k++) acc.add(col[(uint64_t)k * A.npad], clds[k]);
+          const PInfo pi{A.mag_s[pos], A.sumsq_s[pos], A.len_s[pos]};
+          const int d = classify_cand<T>(acc, pi, pc, A.B, C, &cv);
+          if (d) {
+            *la = 0;
+            const uint64_t slot = flag_slot(pos, pi);
+            for (int k = 0; k < nch; k++) st128(A.frow + slot * nch + k, col[(uint64_t)k * A.npad]);
+          }
+        }
+      }
+      if (cv > -1.0 && better(cv, pos, best_v, best_p)) {
+        best_v = cv;
+        best_p = pos;
+      }
+    }
+    uint64_t t_scanned = 0;
+    if (A.trace && threadIdx.x == 0) t_scanned = now();
+    // first maximum of this worker; scanned count
+    for (int o = 32; o >= 1; o >>= 1) {
+      const double ov = __shfl_xor(best_v, o, 64);
+      const uint64_t op = shfl_xor64(best_p, o);
+      if (better(ov, op, best_v, best_p)) {
+        best_v = ov;
+        best_p = op;
+      }
+    }
+    nscan = wave_sum32(nscan);
+    if (lane == 0) {
+      s_bv[wv] = best_v;
+      s_bp[wv] = best_p;
+      atomicAdd(&s_nscan, nscan);
+    }
+    drain();  // this wave's flagged-record stores are complete before the partial announces them
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double v = s_bv[0];
+      uint64_t p = s_bp[0];
+      for (int i = 1; i < NW; i++)
+        if (better(s_bv[i], s_bp[i], v, p)) {
+          v = s_bv[i];
+          p = s_bp[i];
+        }
+      uint64_t *q = A.partials + (uint64_t)w * PART_G;
+      const uint64_t vb = (uint64_t)__double_as_longlong(v);
+      st64(q + 0, gran(seen, (uint32_t)(vb >> 32)));
+      st64(q + 1, gran(seen, (uint32_t)vb));
+      st64(q + 2, gran(seen, p == NONE64 ? NONE : (uint32_t)p));
+      st64(q + 3, gran(seen, s_nfl));
+      st64(q + 4, gran(seen, s_nscan));
+      if (A.trace && mine == nact - 1 && seen < TRACE_STEPS) {
+        uint64_t *tr = A.trace + (uint64_t)seen * 8;
+        tr[2] = t_seen;
+        tr[3] = t_scanned;
+        tr[4] = now();
+        tr[7] = nact;
+      }
+    }
+  }
+}
 
-  // ---------------- controller state (WG 0) ----------------------------------------------
-  uint4 *Fl = dyn + A.nch;
-  uint64_t *msum = reinterpret_cast<uint64_t *>(dyn + 2 * A.nch);
+// ============================================================================================
+// Controller (WG 0).  LDS: integer mean row | column sums | bvec (counts, Fenwick tree, bin
+// starts, begin bounds, bitmap unless global) | member cache
+// ============================================================================================
+template <typename T, int NCH>
+__device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
+  __shared__ uint64_t s_red[3 * NW];
+  __shared__ double s_bv[NW];
+  __shared__ uint64_t s_bp[NW];
+  __shared__ uint32_t s_flag[NT];  // per active worker: offset of its flagged list
+  __shared__ uint64_t s_q[4];
+  __shared__ uint32_t s_klast[KINL];
+  __shared__ int s_abort;
+  __shared__ uint64_t s_sumF;
+  constexpr int NC = NCH > 0 ? NCH : 1;
+  const uint32_t GW = gridDim.x - 1;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int nch = NCH > 0 ? NCH : A.nch;
+  const RowRef Rs{A.hs, 1, A.npad};
+  const int rec_words = (int)A.rec_g;
+  uint8_t *Fl = reinterpret_cast<uint8_t *>(dyn);  // integer mean row
+  uint64_t *msum = reinterpret_cast<uint64_t *>(Fl + (size_t)nch * 16);
   uint32_t *cnt = reinterpret_cast<uint32_t *>(msum + A.B);
   uint32_t *fw = cnt + ((A.nb + 1) & ~1u);
   uint32_t *lo = fw + ((A.nb + 2) & ~1u);
   uint64_t *bnd = reinterpret_cast<uint64_t *>(lo + ((A.nb + 2) & ~1u));
-  uint32_t *bits = reinterpret_cast<uint32_t *>(bnd + A.nb);
-  // every workgroup: alive flags of the positions it owns (chunks g, g + G, ...), local index
-  // (chunk / G) * NT + offset.  Flagged candidates are cleared by the owner; the controller's
-  // pops and erases arrive through the kill log.
-  uint8_t *lal = reinterpret_cast<uint8_t *>(bits + (A.N + 31) / 32);
-  for (uint64_t i = threadIdx.x; i < A.fcap; i += NT) lal[i] = 1;
-  uint32_t kcur = 0;  // kill-log entries applied so far
+  uint32_t *lbits = reinterpret_cast<uint32_t *>(bnd + A.nb);
+  const uint64_t nwords = (A.N + 31) / 32;
+  MemberCache mc;
+  {
+    uint8_t *p = reinterpret_cast<uint8_t *>(lbits + (A.gbits ? 0 : (nwords + 3) / 4 * 4));
+    mc.rp = nch + 1;
+    mc.row = reinterpret_cast<uint4 *>(p);
+    p += (size_t)A.mrow * mc.rp * 16;
+    mc.wt = reinterpret_cast<WinTab *>(p);
+    p += (size_t)A.mrow * sizeof(WinTab);
+    mc.info = reinterpret_cast<uint64_t *>(p);
+    p += (size_t)A.mrow * 24;
+    mc.key = reinterpret_cast<uint64_t *>(p);
+    p += (size_t)A.mrow * 8;
+    mc.pos = reinterpret_cast<uint32_t *>(p);
+  }
+  for (int i = threadIdx.x; i < nch * 16; i += NT) Fl[i] = 0;  // the mean row's padding stays zero
+  if (threadIdx.x == 0) s_abort = 0;
   uint64_t lg = 1;
   while (lg * 2 <= A.nb) lg *= 2;
-  DevBvec bv{bits, cnt, fw, lo, bnd, A.len_s, A.nb, lg};
-  const bool ctl = g == 0;
-  // controller registers (uniform within WG 0)
-  uint32_t last = NONE;      // current centre (static position)
-  uint64_t cl_start = 0;     // first member index of the current cluster
-  uint64_t M = 0;            // members of the current cluster
+  DevBvec bv{A.gbits ? A.gbits : lbits, A.gbits != nullptr, cnt, fw, lo, bnd, A.len_s, A.nb, lg};
+  uint32_t last = NONE;   // current centre (static position)
+  uint32_t last_q = 0;    // its member index in the current cluster
+  uint64_t cl_start = 0;  // first member index of the current cluster
+  uint64_t M = 0;         // members of the current cluster
   uint64_t ncl = 0, nsteps = 0, ncand = 0;
   uint32_t step = 0;
   uint64_t err = 0;
-  uint32_t kn = 0;                                   // kill-log length
-  uint64_t t_win = 0, t_wait = 0, t_coll = 0, t_mark = 0;  // controller phase time, 100 MHz ticks
-  uint64_t t_sub[4] = {0, 0, 0, 0};  // collect: reduce, gather+kill, column sums, closest
+  uint32_t kn = 0;  // kill-log length
+  uint64_t t_wait = 0, t_coll = 0, t_mark = 0;
+  uint64_t t_sub[4] = {0, 0, 0, 0};  // collect: reduce, gather + kill, column sums + mean, closest
+  uint64_t t_ws[4] = {0, 0, 0, 0};   // window: centre window data, window, record, -
 
   auto finish_cluster = [&]() {
     if (threadIdx.x == 0) {
@@ -392,304 +664,188 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
     cl_start += M;
     M = 0;
   };
-  auto new_cluster = [&](uint64_t pos) {  // accumulate's `current = {last}`
+  // accumulate's `current = {last}`: member 0 of a new cluster, its row, sums and window data
+  auto new_cluster = [&](uint64_t pos) {
     if (threadIdx.x == 0) {
-      A.mem_pos[cl_start] = (uint32_t)pos;
-      A.mkeys[cl_start] = 0;
-      s_mpos[0] = (uint32_t)pos;
-      s_mkey[0] = 0;
+      st32(A.mem_pos + cl_start, (uint32_t)pos);
+      st64(A.mkeys + cl_start, 0);
+      if (A.mrow) {
+        mc.pos[0] = (uint32_t)pos;
+        mc.key[0] = 0;
+        mc.info[0] = A.mag_s[pos];
+        mc.info[1] = A.sumsq_s[pos];
+        mc.info[2] = A.len_s[pos];
+        mc.wt[0] = A.wtab[pos];
+      }
     }
+    if (A.mrow)
+      for (int c = threadIdx.x; c < nch; c += NT) mc.row[c] = Rs.chunk(pos, c);
     for (int b = threadIdx.x; b < A.B; b += NT) msum[b] = elem<T>(Rs, pos, b);
     M = 1;
+    last_q = 0;
+    drain();
     __syncthreads();
+  };
+  auto log_kill = [&](uint64_t p) {  // thread 0: a pop / erase, for the workers
+    st32(A.klog + kn, (uint32_t)p);
+    s_klast[kn % KINL] = (uint32_t)p;
   };
   auto pop = [&]() -> uint64_t {  // bvec::pop (bvec.cpp:26-37): static position or ~0
     const int64_t b = bv.first_nonempty();
-    if (b < 0) return ~0ull;
+    if (b < 0) return NONE64;
     const uint64_t p = bv.select((uint64_t)b, 0);
     if (threadIdx.x == 0) {
       bv.kill_one(p);
-      st32(A.klog + kn, (uint32_t)p);
+      log_kill(p);
     }
     kn++;
     __syncthreads();
-    bv.invalidate();
     return p;
   };
+  // data word j of the record for the current `last` (centre row words, then the header)
+  auto rec_word = [&](int j, bool have, uint64_t S, uint64_t E) -> uint32_t {
+    const bool cached = last_q < A.mrow;
+    if (j < 4 * nch) {
+      if (last == NONE) return 0;
+      const uint4 v = cached ? mc.row[(size_t)last_q * mc.rp + j / 4] : Rs.chunk(last, j / 4);
+      return (j & 3) == 0 ? v.x : (j & 3) == 1 ? v.y : (j & 3) == 2 ? v.z : v.w;
+    }
+    const int h = j - 4 * nch;
+    if (h == 0) return have ? last : NONE;
+    if (h == 1) return (uint32_t)S;
+    if (h == 2) return (uint32_t)E;
+    if (h == 3) return kn;
+    if (h < 4 + KINL) {  // kill-log entry kn - KINL + (h - 4)
+      const int64_t e = (int64_t)kn - KINL + (h - 4);
+      return e >= 0 ? s_klast[e % KINL] : NONE;
+    }
+    if (last == NONE) return 0;
+    const int f = (h - 4 - KINL) / 2, hi = (h - 4 - KINL) & 1;
+    const uint64_t v =
+        cached ? mc.info[(size_t)last_q * 3 + f] : (f == 0 ? A.mag_s[last] : f == 1 ? A.sumsq_s[last] : A.len_s[last]);
+    return hi ? (uint32_t)(v >> 32) : (uint32_t)v;
+  };
 
-  if (ctl) {
-    // bvec after insert_finalize: every static position alive
-    for (uint64_t i = threadIdx.x; i <= A.nb; i += NT) lo[i] = A.bin_lo[i];
-    for (uint64_t i = threadIdx.x; i < A.nb; i += NT) {
-      bnd[i] = A.bounds[i];
-      cnt[i] = A.bin_lo[i + 1] - A.bin_lo[i];
+  // bvec after insert_finalize: every static position alive
+  for (uint64_t i = threadIdx.x; i <= A.nb; i += NT) lo[i] = A.bin_lo[i];
+  for (uint64_t i = threadIdx.x; i < A.nb; i += NT) {
+    bnd[i] = A.bounds[i];
+    cnt[i] = A.bin_lo[i + 1] - A.bin_lo[i];
+  }
+  __syncthreads();
+  for (uint64_t i = threadIdx.x + 1; i <= A.nb; i += NT) {  // Fenwick node i covers bins (i - lowbit(i), i]
+    uint32_t t = 0;
+    for (uint64_t b = i - (i & (~i + 1)); b < i; b++) t += cnt[b];
+    fw[i] = t;
+  }
+  if (!A.gbits)  // (a global bitmap is initialised by the launcher)
+    for (uint64_t x = threadIdx.x; x < nwords; x += NT) {
+      const uint64_t rem = A.N - x * 32;
+      lbits[x] = rem >= 32 ? ~0u : ((1u << rem) - 1u);
     }
-    __syncthreads();
-    for (uint64_t i = threadIdx.x + 1; i <= A.nb; i += NT) {  // Fenwick node i covers bins (i - lowbit(i), i]
-      uint32_t t = 0;
-      for (uint64_t b = i - (i & (~i + 1)); b < i; b++) t += cnt[b];
-      fw[i] = t;
-    }
-    const uint64_t nwords = (A.N + 31) / 32;
-    for (uint64_t w = threadIdx.x; w < nwords; w += NT) {
-      const uint64_t rem = A.N - w * 32;
-      bits[w] = rem >= 32 ? ~0u : ((1u << rem) - 1u);
-    }
-    if (threadIdx.x == 0) A.cl_off[0] = 0;
-    __syncthreads();
+  if (threadIdx.x == 0) A.cl_off[0] = 0;
+  __syncthreads();
+  {
     const uint64_t p = pop();  // MS: Point<T>* last = points.pop()
-    if (p != ~0ull) {
+    if (p != NONE64) {
       last = (uint32_t)p;
       new_cluster(p);
     }
   }
 
-  uint32_t seen = 0;
   for (;;) {
-    // ============ controller: advance the accumulate loop to the next scan step ============
-    if (ctl) {
-      if (A.prof && threadIdx.x == 0) t_mark = __builtin_amdgcn_s_memrealtime();
-      uint64_t S = 0, E = 0;
-      bool have = false;
-      while (last != NONE && !err) {
-        bv.h = A.wtab[last];
+    // ============ advance the accumulate loop to the next scan step ========================
+    if (A.prof && threadIdx.x == 0) t_mark = now();
+    uint64_t S = 0, E = 0;
+    bool have = false;
+    while (last != NONE && !err) {
+      const WinTab wt = last_q < A.mrow ? mc.wt[last_q] : A.wtab[last];  // the centre's window data
+      if (A.prof && threadIdx.x == 0) {
+        drain();
+        const uint64_t t = now();
+        t_ws[0] += t - t_mark;
+        t_mark = t;
+      }
+      int64_t count = 0;
+      if (wt.fb < A.nb && wt.bb < A.nb && cnt[wt.fb] > 0 && cnt[wt.bb] > 0) {
+        // nearest-alive form (bv_fast_window): four one-wave queries side by side
+        if (wv < 4) {
+          const uint64_t pf = lo[wt.fb] + wt.kf, qb = lo[wt.bb] + wt.kble;
+          uint64_t r;
+          if (wv == 0) r = bv.next_alive(pf, lo[wt.fb + 1]);
+          else if (wv == 1) r = bv.prev_alive(lo[wt.fb], pf);
+          else if (wv == 2) r = bv.next_alive(qb, lo[wt.bb + 1]);
+          else r = bv.prev_alive(lo[wt.bb], qb);
+          if (lane == 0) s_q[wv] = r;
+        }
+        __syncthreads();
+        bv_fast_window(s_q[0], s_q[1], s_q[2], s_q[3], lo[wt.bb] + wt.kblt, &S, &E);
+        count = (S != NONE64 && E != NONE64 && E >= S) ? 1 : 0;
+        __syncthreads();  // s_q is reused
+      } else {
+        bv.h = wt;
         BPos f, b;
-        bv_get_range(bv, bv.h.bl, bv.h.el, f, b);
+        bv_get_range(bv, wt.bl, wt.el, f, b);
         int e = 0;
-        const int64_t count = bv_window(bv, f, b, &S, &E, &e);
+        count = bv_window(bv, f, b, &S, &E, &e);
         if (e) {
           err = 10 + e;
           break;
         }
-        if (count > 0) {
-          ncand += (uint64_t)count;
-          have = true;
-          break;
-        }
-        // the OpenMP loop ran no iteration: is_min with a NULL result -> pop a new seed
-        const uint64_t p = pop();
-        finish_cluster();
-        last = p == ~0ull ? NONE : (uint32_t)p;
-        if (p != ~0ull) new_cluster(p);
       }
-      step++;
-      if (have) nsteps++;
-      if (threadIdx.x == 0) {
-        // step record: every word carries the step in its upper half (positions < 2^31), so a
-        // reader that finds all four tags equal to the step it was signalled holds an untorn
-        // record even if the slot is being reused
-        uint64_t *r = A.ring + (uint64_t)(step % RING) * 4;
-        const uint64_t tag = (uint64_t)step << 32;
-        drain();  // kill-log entries complete before the record that announces them
-        st64(r + 0, tag | (have ? last : NONE));
-        st64(r + 1, tag | S);
-        st64(r + 2, tag | E);
-        st64(r + 3, tag | kn);
-        // `go` is only a hint for a workgroup that fell RING steps behind: it re-validates the
-        // record's tags after reading it, so no drain is needed between the two
-        st32(A.go, step);
-        if (A.prof) {
-          const uint64_t t = __builtin_amdgcn_s_memrealtime();
-          t_win += t - t_mark;
-          t_mark = t;
-        }
+      if (A.prof && threadIdx.x == 0) {
+        const uint64_t t = now();
+        t_ws[1] += t - t_mark;
+        t_mark = t;
       }
+      if (count > 0) {
+        have = true;
+        break;
+      }
+      // the OpenMP loop ran no iteration: is_min with a NULL result -> pop a new seed
+      const uint64_t p = pop();
+      finish_cluster();
+      last = p == NONE64 ? NONE : (uint32_t)p;
+      if (p != NONE64) new_cluster(p);
     }
-    // ============ everyone: wait for the step ============================================
-    if (threadIdx.x == 0) {
-      s_abort = 0;
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      // steps are published in order: poll the next step's record itself (its words carry
-      // the step); a workgroup that finds the slot already rewritten for a later step fell
-      // RING steps behind and catches up through `go`
-      const uint32_t want = seen + 1;
-      const uint64_t *rn = A.ring + (uint64_t)(want % RING) * 4;
-      bool late = false;
-      for (uint32_t it = 1;; it++) {
-        const uint64_t w0 = ld64(rn + 0), w1 = ld64(rn + 1), w2 = ld64(rn + 2), w3 = ld64(rn + 3);
-        const uint32_t t_0 = (uint32_t)(w0 >> 32), t_1 = (uint32_t)(w1 >> 32), t_2 = (uint32_t)(w2 >> 32),
-                       t_3 = (uint32_t)(w3 >> 32);
-        if (t_0 == want && t_1 == want && t_2 == want && t_3 == want) {
-          s_rec[0] = w0;
-          s_rec[1] = (uint32_t)w1;
-          s_rec[2] = (uint32_t)w2;
-          s_rec[3] = w3;
-          s_go = want;
-          break;
-        }
-        if ((int32_t)(t_0 - want) > 0 || (int32_t)(t_1 - want) > 0 || (int32_t)(t_2 - want) > 0 ||
-            (int32_t)(t_3 - want) > 0) {
-          late = true;
-          break;
-        }
-        if ((it & 255) == 0 && timed_out(A, t0)) {
-          s_abort = 1;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      while (late) {
-        uint32_t v;
-        for (uint32_t it = 1; (v = ld32(A.go)) == seen; it++) {
-          if ((it & 255) == 0 && timed_out(A, t0)) break;  // deadline checked every 256 polls
-          __builtin_amdgcn_s_sleep(1);
-        }
-        if (v == seen) {
-          s_abort = 1;
-          break;
-        }
-        const uint64_t *r = A.ring + (uint64_t)(v % RING) * 4;
-        const uint64_t w0 = ld64(r + 0), w1 = ld64(r + 1), w2 = ld64(r + 2), w3 = ld64(r + 3);
-        if ((w0 >> 32) == v && (w1 >> 32) == v && (w2 >> 32) == v && (w3 >> 32) == v) {
-          s_rec[0] = w0;
-          s_rec[1] = (uint32_t)w1;
-          s_rec[2] = (uint32_t)w2;
-          s_rec[3] = w3;
-          s_go = v;
-          break;
-        }
-        // that slot is being rewritten for a later step: read `go` again
-      }
+    step++;
+    if (have) nsteps++;
+    // publish the step record, one granule per lane of wave 0, every granule tagged with the
+    // step; the kill-log entries are drained first (a late reader finds them there)
+    if (wv == 0) {
+      uint64_t *r = A.ring + (uint64_t)(step % RING) * A.rec_g;
+      drain();
+      for (int j = lane; j < rec_words; j += 64) st64(r + j, gran(step, rec_word(j, have, S, E)));
+      // `go` is only a hint for a worker that fell RING steps behind: it re-validates the
+      // record's tags after reading it
+      if (lane == 0) st32(A.go, step);
     }
-    __syncthreads();
-    if (s_abort) {
-      if (threadIdx.x == 0) atomicMax((unsigned long long *)&A.out[3], 99ull);
-      return;
+    if (A.prof && threadIdx.x == 0) {
+      const uint64_t t = now();
+      t_ws[2] += t - t_mark;
+      t_mark = t;
+      if (A.trace && step < TRACE_STEPS) A.trace[(uint64_t)step * 8 + 0] = t;
     }
-    seen = s_go;
-    struct {
-      uint32_t centre;
-      uint64_t S, E;
-      uint32_t step;
-    } P{(uint32_t)s_rec[0], s_rec[1], s_rec[2], seen};
-    const uint32_t kend = (uint32_t)s_rec[3];
-    if (P.centre == NONE) break;
+    if (!have) break;  // the record told the workers to stop
 
-    // ============ workgroups owning chunks of the window: scan them (Trainer::get_close) ===
-    // Chunk c0 + i belongs to workgroup (c0 + i) mod G; only the nact workgroups owning a
-    // chunk of [S, E] take part in the step (and arrive), the others wait for the next go.
-    const uint64_t c0 = P.S / NT, c1 = P.E / NT;
-    const uint32_t nact = (uint32_t)(c1 - c0 + 1 < (uint64_t)G ? c1 - c0 + 1 : (uint64_t)G);
-    const uint32_t mine = (g + G - (uint32_t)(c0 % G)) % G;
-    if (mine < nact) {
-    // The centre's chunks (staged in LDS below) and magnitudes depend only on the step record:
-    // loaded before the kill log is applied, so they share one round trip with the log's.
-    // (Prefetching the first chunk of candidate rows too would hold 64 more VGPRs across the
-    // barrier: the kernel then spills.)
-    const uint64_t ch0 = c0 + mine;
-    uint4 cpre = make_uint4(0, 0, 0, 0);
-    if (threadIdx.x < A.nch) cpre = Rs.chunk(P.centre, threadIdx.x);
-    const PInfo pc{A.mag_s[P.centre], A.sumsq_s[P.centre], A.len_s[P.centre]};
-    for (uint64_t i = kcur + threadIdx.x; i < kend; i += NT) {  // controller kills since last time
-      const uint32_t p = ld32(A.klog + i);
-      const uint64_t ch = p / NT;
-      if (ch % G == g) lal[(ch / G) * NT + p % NT] = 0;
-    }
-    kcur = kend;
-    if (threadIdx.x < A.nch) clds[threadIdx.x] = cpre;
-    for (int c = NT + threadIdx.x; c < A.nch; c += NT) clds[c] = Rs.chunk(P.centre, c);
-    __syncthreads();
-    double best_v = -1.0;
-    uint64_t best_p = ~0ull;
-    uint32_t nfl = 0;  // this workgroup's flagged count (uniform)
-    for (uint64_t ch = ch0; ch <= c1; ch += G) {
-      const uint64_t pos = ch * NT + threadIdx.x;
-      uint8_t *la = lal + (ch / G) * NT + threadIdx.x;
-      const bool valid = pos >= P.S && pos <= P.E && *la;
-      int d = 0;
-      if (valid) {
-        Acc<T> acc;
-        const uint4 *col = A.hs + pos;
-        PInfo pi;
-        if (A.nch == 16) {
-          uint4 v[16];
-#pragma unroll
-          for (int k = 0; k < 16; k++) v[k] = col[(uint64_t)k * A.npad];
-          pi = PInfo{A.mag_s[pos], A.sumsq_s[pos], A.len_s[pos]};
-#pragma unroll
-          for (int k = 0; k < 16; k++) acc.add(v[k], clds[k]);
-        } else {
-#pragma unroll 8
-          for (int k = 0; k < A.nch; k++) acc.add(col[(uint64_t)k * A.npad], clds[k]);
-          pi = PInfo{A.mag_s[pos], A.sumsq_s[pos], A.len_s[pos]};
-        }
-        const PS s = acc.finish(pi.mag, pc.mag);
-        double raw[MC_MAX_SINGLE];
-#pragma unroll
-        for (int i = 0; i < MC_MAX_SINGLE; i++)
-          raw[i] = i < C.c.n_single ? raw_fast(C.c.lookup[i], s, pi, pc, A.B) : 0.0;  // compute(*pt, *p)
-        double cv;
-        d = classify_raw(C, raw, &cv, nullptr);
-        if (cv > -1.0 && better(cv, pos, best_v, best_p)) {
-          best_v = cv;
-          best_p = pos;
-        }
-        if (d) *la = 0;
-      }
-      // ordered compaction of this chunk's flagged positions (ascending position)
-      const uint64_t bal = __ballot(d);
-      if (lane == 0) s_wcnt[wv] = (uint32_t)__popcll(bal);
-      __syncthreads();
-      uint32_t before = nfl;
-      uint32_t tot = 0;
-      for (int i = 0; i < NW; i++) {
-        if (i < wv) before += s_wcnt[i];
-        tot += s_wcnt[i];
-      }
-      if (d) st32(A.flist + (uint64_t)g * A.fcap + before + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull)), (uint32_t)pos);
-      nfl += tot;
-      __syncthreads();
-    }
-    for (int o = 32; o >= 1; o >>= 1) {
-      const double ov = __shfl_xor(best_v, o, 64);
-      const uint64_t op = shfl_xor64(best_p, o);
-      if (better(ov, op, best_v, best_p)) {
-        best_v = ov;
-        best_p = op;
-      }
-    }
-    if (lane == 0) {
-      s_bv[wv] = best_v;
-      s_bp[wv] = best_p;
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // flag / alive stores of every wave drained
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      double v = s_bv[0];
-      uint64_t p = s_bp[0];
-      for (int i = 1; i < NW; i++)
-        if (better(s_bv[i], s_bp[i], v, p)) {
-          v = s_bv[i];
-          p = s_bp[i];
-        }
-      // every wave's list / alive stores were drained before the barrier: the tagged partial
-      // words are the signal
-      uint64_t *q = A.partials[g].w;
-      const uint64_t tag = (uint64_t)P.step << 32, vb = (uint64_t)__double_as_longlong(v);
-      st64(q + 0, tag | (vb >> 32));
-      st64(q + 1, tag | (vb & 0xffffffffull));
-      st64(q + 2, tag | (p == ~0ull ? (uint64_t)NONE : p));
-      st64(q + 3, tag | nfl);
-    }
-    }  // active workgroup
-    if (!ctl) continue;
-
-    // ============ controller: collect the step (get_close's reduction + get_mean) =========
-    // thread t polls the partial of the t-th active workgroup until its four words carry this
-    // step (s_abort is 0 here: set only on a failed wait, which returns)
+    // ============ collect the step (get_close's reduction + get_mean) ======================
+    const uint64_t c0 = S / NT, c1 = E / NT;
+    const uint32_t nact = (uint32_t)(c1 - c0 + 1 < (uint64_t)GW ? c1 - c0 + 1 : (uint64_t)GW);
+    // thread t polls the partial of the t-th active worker until its granules carry the step
     double bv_ = -1.0;
-    uint64_t bp_ = ~0ull, cnt_w = 0;
+    uint64_t bp_ = NONE64;
+    uint32_t cnt_w = 0, scan_w = 0;
     if (threadIdx.x < nact) {
-      const uint64_t *q = A.partials[(c0 + threadIdx.x) % G].w;
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      const uint64_t *q = A.partials + (uint64_t)((c0 + threadIdx.x) % GW) * PART_G;
+      const uint64_t t0 = now();
       for (uint32_t it = 1;; it++) {
-        const uint64_t w0 = ld64(q + 0), w1 = ld64(q + 1), w2 = ld64(q + 2), w3 = ld64(q + 3);
-        if ((uint32_t)(w0 >> 32) == P.step && (uint32_t)(w1 >> 32) == P.step && (uint32_t)(w2 >> 32) == P.step &&
-            (uint32_t)(w3 >> 32) == P.step) {
+        const uint64_t w0 = ld64(q + 0), w1 = ld64(q + 1), w2 = ld64(q + 2), w3 = ld64(q + 3), w4 = ld64(q + 4);
+        if ((uint32_t)(w0 >> 32) == step && (uint32_t)(w1 >> 32) == step && (uint32_t)(w2 >> 32) == step &&
+            (uint32_t)(w3 >> 32) == step && (uint32_t)(w4 >> 32) == step) {
           bv_ = __longlong_as_double((long long)((w0 << 32) | (w1 & 0xffffffffull)));
-          const uint32_t p32 = (uint32_t)w2;
-          bp_ = p32 == NONE ? ~0ull : (uint64_t)p32;
+          bp_ = (uint32_t)w2 == NONE ? NONE64 : (uint64_t)(uint32_t)w2;
           cnt_w = (uint32_t)w3;
+          scan_w = (uint32_t)w4;
           break;
         }
         if ((it & 255) == 0 && timed_out(A, t0)) {
@@ -700,19 +856,17 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
       }
     }
     if (A.prof && threadIdx.x == 0) {
-      const uint64_t t = __builtin_amdgcn_s_memrealtime();
+      const uint64_t t = now();
       t_wait += t - t_mark;
       t_mark = t;
     }
-    __syncthreads();
-    if (s_abort) {
-      if (threadIdx.x == 0) atomicMax((unsigned long long *)&A.out[3], 99ull);
-      return;
+    // block reduction: exclusive prefix of the flagged counts (offsets of the lists in worker
+    // order), the first maximum, the scanned total
+    uint32_t inc = cnt_w;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t u = (uint32_t)__shfl_up((int)inc, o, 64);
+      if (lane >= o) inc += u;
     }
-    // first maximum over workgroups, flagged counts and their offsets
-    uint64_t nflag;
-    const uint64_t off_w = block_excl_scan(cnt_w, &nflag, R);
-    if (threadIdx.x < nact) s_flag[threadIdx.x] = (uint32_t)off_w;  // nact <= G <= NT
     for (int o = 32; o >= 1; o >>= 1) {
       const double ov = __shfl_xor(bv_, o, 64);
       const uint64_t op = shfl_xor64(bp_, o);
@@ -721,173 +875,341 @@ __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
         bp_ = op;
       }
     }
+    const uint32_t wscan = wave_sum32(scan_w);
+    if (lane == 63) s_red[wv] = inc;
     if (lane == 0) {
       s_bv[wv] = bv_;
       s_bp[wv] = bp_;
+      s_red[NW + wv] = wscan;
     }
     __syncthreads();
+    if (A.trace && threadIdx.x == 0 && step < TRACE_STEPS) A.trace[(uint64_t)step * 8 + 5] = now();
+    if (s_abort) {
+      if (threadIdx.x == 0) atomicMax((unsigned long long *)&A.out[3], 99ull);
+      return;
+    }
+    uint64_t nflag = 0, before = 0, nsc = 0;
     double best_val = s_bv[0];
     uint64_t best_pos = s_bp[0];
-    for (int i = 1; i < NW; i++)
-      if (better(s_bv[i], s_bp[i], best_val, best_pos)) {
+    for (int i = 0; i < NW; i++) {
+      if (i < wv) before += s_red[i];
+      nflag += s_red[i];
+      nsc += s_red[NW + i];
+      if (i && better(s_bv[i], s_bp[i], best_val, best_pos)) {
         best_val = s_bv[i];
         best_pos = s_bp[i];
       }
+    }
+    ncand += nsc;
+    if (threadIdx.x < nact) s_flag[threadIdx.x] = (uint32_t)(before + inc - cnt_w);
+    __syncthreads();
     uint64_t tq = 0;
     if (A.prof && threadIdx.x == 0) {
-      tq = __builtin_amdgcn_s_memrealtime();
+      tq = now();
       t_sub[0] += tq - t_mark;
     }
     if (nflag > 0) {
-      // remove_available: the flagged positions join the cluster (keys keep bvec order)
+      // remove_available: the flagged positions join the cluster (their keys order them like
+      // the bvec walk: step, then position); rows and magnitudes come with the flagged records
       const uint64_t mb = cl_start + M;
       for (uint64_t i = threadIdx.x; i < nflag; i += NT) {
-        uint32_t a = 0, z = nact;  // last active workgroup with offset <= i
+        uint32_t a = 0, z = nact;  // last active worker with offset <= i
         while (z - a > 1) {
           const uint32_t m = (a + z) / 2;
           if (s_flag[m] <= i) a = m;
           else z = m;
         }
-        const uint32_t p = ld32(A.flist + (uint64_t)((c0 + a) % G) * A.fcap + (i - s_flag[a]));
-        const uint64_t key = ((uint64_t)P.step << 32) | p;
-        A.mem_pos[mb + i] = p;
-        A.mkeys[mb + i] = key;
-        if (M + i < MCAP) {
-          s_mpos[M + i] = p;
-          s_mkey[M + i] = key;
+        const uint64_t slot = (uint64_t)((c0 + a) % GW) * A.fcap + (i - s_flag[a]);
+        const uint32_t p = ld32(A.fpos + slot);
+        const uint64_t mg = ld64(A.finfo + slot * 3 + 0), sq = ld64(A.finfo + slot * 3 + 1),
+                       ln = ld64(A.finfo + slot * 3 + 2);
+        const uint64_t key = ((uint64_t)step << 32) | p;
+        const uint64_t q = M + i;
+        st32(A.mem_pos + mb + i, p);
+        st64(A.mkeys + mb + i, key);
+        if (q < A.mrow) {
+          mc.pos[q] = p;
+          mc.key[q] = key;
+          mc.info[q * 3 + 0] = mg;
+          mc.info[q * 3 + 1] = sq;
+          mc.info[q * 3 + 2] = ln;
+          mc.wt[q] = A.wtab[p];
+          for (int k = 0; k < nch; k++) mc.row[q * mc.rp + k] = ld128(A.frow + slot * nch + k);
+        } else {  // beyond the cache: column sums straight from the row
+          constexpr int per = 16 / (int)sizeof(T);
+          for (int k = 0; k < nch; k++) {
+            const uint4 v = ld128(A.frow + slot * nch + k);
+            const T *pv = reinterpret_cast<const T *>(&v);
+#pragma unroll
+            for (int e = 0; e < per; e++)
+              if (pv[e]) atomicAdd((unsigned long long *)&msum[k * per + e], (unsigned long long)pv[e]);
+          }
         }
         bv.kill_one(p);
       }
+      drain();
       __syncthreads();
       if (A.prof && threadIdx.x == 0) {
-        const uint64_t t = __builtin_amdgcn_s_memrealtime();
+        const uint64_t t = now();
         t_sub[1] += t - tq;
         tq = t;
       }
-      // row indices from LDS when the cluster fits there: the chunk loads are then the only
-      // global round trip
-      const bool in_lds = M + nflag <= MCAP;
-      add_rows_acc<T>(Rs, in_lds ? s_mpos + M : A.mem_pos + mb, (uint32_t)nflag, A.nch, msum);
+      // column sums of the cached new members (one thread per bin), then the integer mean
+      // F_b = floor(S_b / M) and its total (features.hpp: get_mean as a SAD reduction)
+      const uint64_t q0 = M, q1 = M + nflag < A.mrow ? M + nflag : (uint64_t)A.mrow;
       M += nflag;
+      uint64_t part = 0;
+      for (int b = threadIdx.x; b < A.B; b += NT) {
+        uint64_t s = msum[b];
+        for (uint64_t q = q0; q < q1; q++) s += reinterpret_cast<const T *>(mc.row + q * mc.rp)[b];
+        msum[b] = s;
+        const uint64_t F = (s >> 32) == 0 ? (uint64_t)((uint32_t)s / (uint32_t)M) : s / M;
+        reinterpret_cast<T *>(Fl)[b] = (T)F;
+        part += F;
+      }
+      for (int o = 32; o >= 1; o >>= 1) part += shfl_xor64(part, o);
+      if (threadIdx.x == 0) s_sumF = 0;
+      __syncthreads();
+      if (lane == 0 && part) atomicAdd((unsigned long long *)&s_sumF, (unsigned long long)part);
       __syncthreads();
       if (A.prof && threadIdx.x == 0) {
-        const uint64_t t = __builtin_amdgcn_s_memrealtime();
+        const uint64_t t = now();
         t_sub[2] += t - tq;
         tq = t;
       }
-      const uint64_t win0 = mean_closest_fast<T, NT>(Rs, in_lds ? s_mpos : A.mem_pos + cl_start,
-                                                     in_lds ? s_mkey : A.mkeys + cl_start, (uint32_t)M,
-                                                     A.mag_s, A.B, A.nch, msum, Fl);
-      if (threadIdx.x == 0) R.r0 = win0;  // the winner is thread 0's; make it uniform
+      // Trainer::closest: first minimum of distance_d over the members (ties by key)
+      const uint64_t sumF = s_sumF;
+      const uint4 *F4 = reinterpret_cast<const uint4 *>(Fl);
+      double bd = __builtin_inf();
+      uint64_t bk = NONE64, bq = 0;
+      for (uint64_t q = threadIdx.x; q < M; q += NT) {
+        Acc<T> acc;
+        uint64_t mp, key;
+        if (q < A.mrow) {
+          const uint4 *row = mc.row + q * mc.rp;
+          if constexpr (NCH > 0) {
+#pragma unroll
+            for (int k = 0; k < NC; k++) acc.add(row[k], F4[k]);
+          } else {
+            for (int k = 0; k < nch; k++) acc.add(row[k], F4[k]);
+          }
+          mp = mc.info[q * 3];
+          key = mc.key[q];
+        } else {
+          const uint64_t r = ld32(A.mem_pos + cl_start + q);
+          for (int k = 0; k < nch; k++) acc.add(Rs.chunk(r, k), F4[k]);
+          mp = A.mag_s[r];
+          key = ld64(A.mkeys + cl_start + q);
+        }
+        const PS s = acc.finish(mp, sumF);
+        const double frac = (double)(2 * s.smin) / (double)(mp + sumF);
+        const double d = __builtin_fma(-frac, frac, 1.0) * 10000.0;
+        if (d < bd || (d == bd && key < bk)) {
+          bd = d;
+          bk = key;
+          bq = q;
+        }
+      }
+      for (int o = 32; o >= 1; o >>= 1) {
+        const double od = __shfl_xor(bd, o, 64);
+        const uint64_t ok = shfl_xor64(bk, o), oq = shfl_xor64(bq, o);
+        if (od < bd || (od == bd && ok < bk)) {
+          bd = od;
+          bk = ok;
+          bq = oq;
+        }
+      }
+      if (lane == 0) {
+        s_bv[wv] = bd;
+        s_red[2 * NW + wv] = bk;
+        s_bp[wv] = bq;
+      }
       __syncthreads();
-      const uint64_t win = R.r0;
-      __syncthreads();
-      if (A.prof && threadIdx.x == 0) t_sub[3] += __builtin_amdgcn_s_memrealtime() - tq;
-      last = (uint32_t)win;
-      bv.invalidate();
-    } else if (best_pos != ~0ull) {
+      double d = s_bv[0];
+      uint64_t k = s_red[2 * NW], win = s_bp[0];
+      for (int i = 1; i < NW; i++)
+        if (s_bv[i] < d || (s_bv[i] == d && s_red[2 * NW + i] < k)) {
+          d = s_bv[i];
+          k = s_red[2 * NW + i];
+          win = s_bp[i];
+        }
+      last_q = (uint32_t)win;
+      last = win < A.mrow ? mc.pos[win] : ld32(A.mem_pos + cl_start + win);
+      __syncthreads();  // s_bv / s_bp are reused by the next step
+      if (A.prof && threadIdx.x == 0) t_sub[3] += now() - tq;
+    } else if (best_pos != NONE64) {
       // is_min with a result: the best candidate seeds the next cluster (bvec::erase)
       if (threadIdx.x == 0) {
         bv.kill_one(best_pos);
-        st32(A.klog + kn, (uint32_t)best_pos);
+        log_kill(best_pos);
       }
       kn++;
       __syncthreads();
-      bv.invalidate();
       finish_cluster();
       last = (uint32_t)best_pos;
       new_cluster(best_pos);
     } else {
       const uint64_t p = pop();
       finish_cluster();
-      last = p == ~0ull ? NONE : (uint32_t)p;
-      if (p != ~0ull) new_cluster(p);
+      last = p == NONE64 ? NONE : (uint32_t)p;
+      if (p != NONE64) new_cluster(p);
     }
-    __syncthreads();
     if (A.prof && threadIdx.x == 0) {
-      const uint64_t t = __builtin_amdgcn_s_memrealtime();
+      const uint64_t t = now();
       t_coll += t - t_mark;
+      if (A.trace && step < TRACE_STEPS) A.trace[(uint64_t)step * 8 + 6] = t;
     }
   }
-  if (ctl && threadIdx.x == 0) {
+  if (threadIdx.x == 0) {
     A.out[0] = ncl;
     A.out[1] = nsteps;
     A.out[2] = ncand;
     if (err) atomicMax((unsigned long long *)&A.out[3], (unsigned long long)err);
     A.out[4] = cl_start;
-    A.out[5] = t_win;
+    A.out[5] = t_ws[0] + t_ws[1] + t_ws[2];
     A.out[6] = t_wait;
     A.out[7] = t_coll;
     for (int i = 0; i < 4; i++) A.out[8 + i] = t_sub[i];
+    for (int i = 0; i < 4; i++) A.out[12 + i] = t_ws[i];
   }
+}
+
+// NCH: compile-time chunks per row (0: A.nch at run time).
+template <typename T, int NCH>
+__global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
+  extern __shared__ __attribute__((aligned(16))) uint4 dyn[];
+  if (blockIdx.x == 0) controller<T, NCH>(A, dyn);
+  else worker<T, NCH>(A, C, dyn);
+}
+
+__global__ void bits_init_kernel(uint32_t *bits, uint64_t n) {
+  const uint64_t nwords = (n + 31) / 32;
+  for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nwords; w += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t rem = n - w * 32;
+    bits[w] = rem >= 32 ? ~0u : ((1u << rem) - 1u);
+  }
+}
+
+struct AccPlan {
+  const void *fn = nullptr;
+  int res = 0;         // chunks per worker resident in its LDS (0: streaming)
+  bool gbits = false;  // bitmap in global memory
+  uint32_t mrow = 0;   // member cache entries
+  size_t lds = 0;
+  uint32_t G = 0;
+  uint64_t fcap = 0;
+  uint32_t rec_g = 0;
+};
+
+// Grid: one workgroup per CU (a multiple of the 8 XCDs): the controller and G - 1 workers.
+uint32_t accum_grid(const mc_ctx *c) {
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess) cus = 256;
+  uint32_t G = (uint32_t)cus / 8 * 8;
+  if (G > (uint32_t)NT + 1) G = NT;
+  if (G < 8) G = 8;
+  return G;
+}
+
+// Variant and LDS layouts for this context; false when the configuration cannot run on the
+// device.  Both roles get the same dynamic LDS (one workgroup per CU either way).
+bool accum_plan(const mc_ctx *c, uint32_t nb, AccPlan *pl) {
+  if (c->width != 1 && c->width != 2) return false;
+  if (c->cls.align) return false;
+  if (c->norder >= (1ull << 31)) return false;
+  const int nch = (int)((c->B * c->width + 15) / 16);
+  const uint32_t G = accum_grid(c), GW = G - 1;
+  const uint64_t chunks = (c->norder + NT - 1) / NT;
+  const uint64_t per_w = (chunks + GW - 1) / GW;
+  pl->G = G;
+  pl->fcap = per_w * NT;
+  pl->rec_g = (uint32_t)(4 * nch + REC_HDR);
+  pl->fn = c->width == 1 ? (nch == 16 ? reinterpret_cast<const void *>(&accum_kernel<uint8_t, 16>)
+                                      : reinterpret_cast<const void *>(&accum_kernel<uint8_t, 0>))
+                         : reinterpret_cast<const void *>(&accum_kernel<uint16_t, 0>);
+  const size_t static_lds = 8 * 1024;  // both roles' __shared__ words, with margin
+  const size_t cap = 160 * 1024 - static_lds;
+  // worker: record words, alive flags, resident rows
+  const size_t wfix = (size_t)(pl->rec_g + 3) / 4 * 16 + (pl->fcap + 15) / 16 * 16;
+  const size_t chunk_bytes = (size_t)nch * NT * 16;
+  pl->res = (!getenv("MC_ACCUM_STREAM") && wfix + per_w * chunk_bytes <= cap) ? (int)per_w : 0;
+  // controller: mean row, column sums, bvec (+ bitmap unless global), member cache
+  auto cfix = [&](bool gbits) {
+    size_t s = (size_t)nch * 16 + (size_t)c->B * 8;
+    s += (size_t)((nb + 1) & ~1u) * 4 + 2 * (size_t)((nb + 2) & ~1u) * 4 + (size_t)nb * 8;
+    if (!gbits) s += (size_t)((c->norder + 31) / 32 + 3) / 4 * 16;
+    return s;
+  };
+  const size_t per_entry = (size_t)(nch + 1) * 16 + sizeof(WinTab) + 24 + 8 + 4;
+  for (int gb = 0; gb < 2; gb++) {
+    const size_t f = cfix(gb != 0);
+    if (f >= cap) continue;
+    const uint64_t m = std::min<uint64_t>(1024, (cap - f) / per_entry);
+    if (m >= 64 || (gb == 1 && m >= 1)) {
+      pl->gbits = gb != 0;
+      pl->mrow = (uint32_t)m;
+      pl->lds = std::max(f + m * per_entry, wfix + (size_t)pl->res * chunk_bytes);
+      return true;
+    }
+  }
+  return false;
 }
 
 }  // namespace
 
-// Grid: one workgroup per CU, a multiple of the 8 XCDs.
-static uint32_t accum_grid(const mc_ctx *c) {
-  int cus = 0;
-  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess) cus = 256;
-  uint32_t G = (uint32_t)cus / 8 * 8;
-  if (G > (uint32_t)NT) G = NT;
-  if (G < 8) G = 8;
-  return G;
-}
-// positions owned by one workgroup (its chunks g, g + G, ...)
-static uint64_t accum_fcap(const mc_ctx *c, uint32_t G) {
-  const uint64_t chunks = (c->norder + NT - 1) / NT;
-  return ((chunks + G - 1) / G) * NT;
-}
-
-// LDS bytes: controller state + the per-workgroup alive flags (all workgroups get the same
-// allocation)
-static size_t accum_lds(const mc_ctx *c, uint32_t nb, uint32_t G) {
-  const int nch = (int)((c->B * c->width + 15) / 16);
-  return (size_t)2 * nch * 16 + (size_t)c->B * 8 + (size_t)((nb + 1) & ~1u) * 4 + (size_t)((nb + 2) & ~1u) * 8 +
-         (size_t)nb * 8 + (c->norder + 31) / 32 * 4 + accum_fcap(c, G);
-}
-
 bool accum_supported(const mc_ctx *c, uint32_t nb) {
-  if (c->width != 1 && c->width != 2) return false;
-  if (c->cls.align) return false;
-  if (c->norder >= (1ull << 31)) return false;
-  // + static LDS (reductions, member mirror) and headroom
-  return accum_lds(c, nb, accum_grid(c)) + 24 * 1024 <= 160 * 1024;
+  AccPlan pl;
+  return accum_plan(c, nb, &pl);
 }
 
 int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, uint32_t nb, double sim,
                  uint32_t *d_mem_pos, uint64_t *d_mkeys, uint32_t *d_cl_centre, uint64_t *d_cl_off, uint64_t *d_out) {
-  const uint32_t G = accum_grid(c);
-  const size_t lds = accum_lds(c, nb, G);
-  const void *fn = c->width == 1 ? reinterpret_cast<const void *>(&accum_kernel<uint8_t>)
-                                 : reinterpret_cast<const void *>(&accum_kernel<uint16_t>);
-  MCG_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  AccPlan pl;
+  if (!accum_plan(c, nb, &pl)) {
+    set_error("device-resident accumulation does not take this configuration");
+    return MC_ERR_UNSUPPORTED;
+  }
+  const uint32_t G = pl.G, GW = G - 1;
+  const int nch = (int)((c->B * c->width + 15) / 16);
+  MCG_CHECK(hipFuncSetAttribute(pl.fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.lds));
   int per_cu = 0;
-  MCG_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, NT, lds));
+  MCG_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pl.fn, NT, pl.lds));
   if (per_cu < 1) {
     set_error("accumulation kernel does not fit on a CU");
     return MC_ERR_HIP;
   }
-  const uint64_t fcap = accum_fcap(c, G);
-  const size_t hand = 256 + (size_t)RING * 32;  // go, step ring
-  const size_t part_bytes = ((size_t)G * sizeof(AccPartial) + 255) / 256 * 256;
-  const size_t flist_bytes = ((size_t)G * fcap * 4 + 255) / 256 * 256;
-  if (ensure(c->s_a, hand) || ensure(c->s_b, part_bytes + c->n * sizeof(WinTab)) ||
-      ensure(c->s_c, flist_bytes + c->norder * 4 + 16))
+  const uint64_t fcap = pl.fcap;
+  // s_a: go word + step ring; s_b: partials + window table (+ global bitmap); s_c: flagged
+  // positions + kill log + flagged magnitudes + flagged rows; s_h: trace
+  const size_t ring_bytes = 256 + (size_t)RING * pl.rec_g * 8;
+  const size_t part_bytes = ((size_t)GW * PART_G * 8 + 255) / 256 * 256;
+  const size_t wtab_bytes = (c->norder * sizeof(WinTab) + 255) / 256 * 256;
+  const size_t bits_bytes = pl.gbits ? ((c->norder + 31) / 32 * 4 + 255) / 256 * 256 : 0;
+  const size_t fpos_bytes = ((size_t)GW * fcap * 4 + 255) / 256 * 256;
+  const size_t klog_bytes = (c->norder * 4 + 16 + 255) / 256 * 256;
+  const size_t finfo_bytes = (size_t)GW * fcap * 24;
+  const size_t frow_bytes = (size_t)GW * fcap * nch * 16;
+  if (ensure(c->s_a, ring_bytes) || ensure(c->s_b, part_bytes + wtab_bytes + bits_bytes) ||
+      ensure(c->s_c, fpos_bytes + klog_bytes + finfo_bytes + frow_bytes))
     return MC_ERR_OOM;
   WinTab *d_wtab = (WinTab *)((char *)c->s_b.p + part_bytes);
+  uint32_t *d_bits = pl.gbits ? (uint32_t *)((char *)c->s_b.p + part_bytes + wtab_bytes) : nullptr;
   timed_begin(c);
   wintab_kernel<<<(int)std::min<uint64_t>((c->n + 255) / 256, 2048), 256, 0, c->stream>>>(
       c->norder, (const uint64_t *)c->len_s.p, d_bin_lo, d_bounds, nb, sim, d_wtab);
   MCG_CHECK(hipGetLastError());
+  if (d_bits) {
+    bits_init_kernel<<<(int)std::min<uint64_t>(c->norder / 32 / 256 + 1, 1024), 256, 0, c->stream>>>(d_bits, c->norder);
+    MCG_CHECK(hipGetLastError());
+  }
   timed_end(c, F_FINAL);
-  MCG_CHECK(hipMemsetAsync(c->s_a.p, 0, hand, c->stream));
-  MCG_CHECK(hipMemsetAsync(c->s_b.p, 0, part_bytes, c->stream));  // no partial carries a step tag yet
+  MCG_CHECK(hipMemsetAsync(c->s_a.p, 0, ring_bytes, c->stream));  // no record carries a step tag yet
+  MCG_CHECK(hipMemsetAsync(c->s_b.p, 0, part_bytes, c->stream));  // ... nor a partial
   AccArgs A;
   memset(&A, 0, sizeof A);
   A.hs = (const uint4 *)c->hs.p;
   A.npad = c->npad;
-  A.nch = (int)((c->B * c->width + 15) / 16);
+  A.nch = nch;
   A.B = c->B;
   A.mag_s = (const uint64_t *)c->mag_s.p;
   A.sumsq_s = (const uint64_t *)c->sumsq_s.p;
@@ -896,14 +1218,20 @@ int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, 
   A.nb = nb;
   A.bin_lo = d_bin_lo;
   A.bounds = d_bounds;
-  A.sim = sim;
   A.wtab = d_wtab;
+  A.gbits = d_bits;
   A.go = (uint32_t *)c->s_a.p;
   A.ring = (uint64_t *)((char *)c->s_a.p + 256);
-  A.partials = (AccPartial *)c->s_b.p;
-  A.flist = (uint32_t *)c->s_c.p;
-  A.klog = (uint32_t *)((char *)c->s_c.p + flist_bytes);
+  A.rec_g = pl.rec_g;
+  A.partials = (uint64_t *)c->s_b.p;
+  char *sc = (char *)c->s_c.p;
+  A.fpos = (uint32_t *)sc;
+  A.klog = (uint32_t *)(sc + fpos_bytes);
+  A.finfo = (uint64_t *)(sc + fpos_bytes + klog_bytes);
+  A.frow = (uint4 *)(sc + fpos_bytes + klog_bytes + finfo_bytes);
   A.fcap = fcap;
+  A.res = pl.res;
+  A.mrow = pl.mrow;
   A.mem_pos = d_mem_pos;
   A.mkeys = d_mkeys;
   A.cl_centre = d_cl_centre;
@@ -911,10 +1239,19 @@ int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, 
   A.out = d_out;
   A.budget = 20ull * 100000000ull;  // a single hand-off never takes 20 s: give up, report error 99
   A.prof = getenv("MC_ACCUM_PROFILE") ? 1 : 0;
+  A.trace = nullptr;
+  if (getenv("MC_ACCUM_PROFILE") && atoi(getenv("MC_ACCUM_PROFILE")) >= 2) {
+    if (ensure(c->s_h, TRACE_STEPS * 64)) return MC_ERR_OOM;
+    MCG_CHECK(hipMemsetAsync(c->s_h.p, 0, TRACE_STEPS * 64, c->stream));
+    A.trace = (uint64_t *)c->s_h.p;
+  }
+  if (getenv("MC_ACCUM_PROFILE"))
+    fprintf(stderr, "[accum] variant: width %d nch %d resident chunks/worker %d global-bitmap %d member-cache %u lds %zu G %u\n",
+            c->width, nch, pl.res, (int)pl.gbits, pl.mrow, pl.lds, G);
   DevClassifier cls = c->cls;
   void *args[] = {&A, &cls};
   timed_begin(c);
-  MCG_CHECK(hipLaunchCooperativeKernel(fn, dim3(G), dim3(NT), args, (unsigned)lds, c->stream));
+  MCG_CHECK(hipLaunchCooperativeKernel(pl.fn, dim3(G), dim3(NT), args, (unsigned)pl.lds, c->stream));
   timed_end(c, F_SCAN);
   return MC_OK;
 }

@@ -175,4 +175,24 @@ BV_HD inline int64_t bv_window(A &a, const BPos &b, const BPos &e, uint64_t *S, 
   return count;
 }
 
+// Fast form of get_range + window (the device controller's common case): when both edge
+// bins -- fb = index_of(len * sim).low and bb = index_of(len / sim).high -- hold alive
+// elements, bv_inner_index_of's ranks turn into "nearest alive position" queries on the
+// alive bitmap (static positions are rank-ordered inside and across bins):
+//   nf = first alive in [lo[fb] + kf, lo[fb+1])     pf = last alive in [lo[fb], lo[fb] + kf)
+//   nx = first alive in [lo[bb] + kble, lo[bb+1])   pv = last alive in [lo[bb], lo[bb] + kble)
+// (kf / kblt / kble: static positions of the bin shorter than / not longer than the window
+// lengths, WinTab).  front = min(lb, size - 1) is nf, or pf when no alive element is long
+// enough; back is the last alive element (pv) when none is longer than len / sim (ub == size),
+// pv when one has exactly that length (ub > lb: pv >= lo[bb] + kblt), else the next longer
+// one (nx).  bv_window's count is rank(back) - rank(front) + 1, so the window holds
+// candidates iff E >= S.  NONE = ~0.  tests/native/bvec_check.cpp compares this with
+// bv_get_range + bv_window.
+BV_HD inline void bv_fast_window(uint64_t nf, uint64_t pf, uint64_t nx, uint64_t pv, uint64_t lt_pos, uint64_t *S,
+                                 uint64_t *E) {
+  *S = nf != ~0ull ? nf : pf;
+  if (nx == ~0ull) *E = pv;
+  else *E = (pv != ~0ull && pv >= lt_pos) ? pv : nx;
+}
+
 }  // namespace mcg

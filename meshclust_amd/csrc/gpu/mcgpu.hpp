@@ -109,7 +109,7 @@ struct mc_ctx {
   mcg::Buf ident_s, al_a, al_b, al_out;
   mcg::Buf acc_out;  // device-resident accumulation: counters / error word
   // scratch
-  mcg::Buf s_a, s_b, s_c, s_d, s_e, s_f, s_g;
+  mcg::Buf s_a, s_b, s_c, s_d, s_e, s_f, s_g, s_h;
   std::vector<void *> pinned;
   // timers: event pairs recorded around kernels, resolved lazily after the next stream sync
   hipEvent_t ev0 = nullptr, ev1 = nullptr;

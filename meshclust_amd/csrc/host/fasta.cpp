@@ -11,6 +11,8 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <immintrin.h>
+
 #include <algorithm>
 #include <cctype>
 #include <cstring>
@@ -131,42 +133,87 @@ namespace {
 struct Chunk {
   struct Rec {
     size_t hdr, hdr_len;  // header line in the mapped file
-    size_t off, len;      // one-digit bytes in `bytes`
+    size_t off, len;      // chunk-local byte offset and length of the one-digit string
+    uint64_t w_off;       // chunk-local first word in `pk`
     bool ready;           // isBaseReady: some line followed the header (or EOF did)
   };
   std::vector<Rec> recs;
-  std::vector<uint8_t> bytes;
+  std::vector<uint32_t> pk;       // packed words, records word-aligned
   std::vector<int32_t> seg;
   std::vector<uint64_t> nseg;     // segment pairs per record
   std::vector<uint64_t> exc_pos;  // chunk-local byte positions
   std::vector<uint8_t> exc_val;
-  uint64_t words = 0;
+  uint64_t bytes = 0;
   std::string err;
 };
 
+// A/C/G/T in either case -> 0..3 (a record made only of these needs no segmentation work:
+// one N-free run, encodeNucleotides maps every byte); everything else -> 255
+struct FastTable {
+  uint8_t v[256];
+  FastTable() {
+    memset(v, 255, sizeof v);
+    v['A'] = v['a'] = 0;
+    v['C'] = v['c'] = 1;
+    v['G'] = v['g'] = 2;
+    v['T'] = v['t'] = 3;
+  }
+};
+const FastTable kFast;
+
+// A record of plain bases (A/C/G/T in either case) -> 2-bit words appended to pk (base j of
+// the record at bits 2*(j % 16) of word j / 16).  32 bases per AVX2 step: the code of a byte
+// is ((c >> 1) ^ (c >> 2)) & 3 (A/a C/c G/g T/t -> 0 1 2 3); the byte is plain iff c | 0x20
+// equals "acgt"[code]; pext gathers the 2-bit fields.  False (pk unchanged) if some byte is
+// not plain.
+bool encode_plain(const uint8_t *b, size_t L, std::vector<uint32_t> &pk) {
+  const size_t w0 = pk.size();
+  pk.resize(w0 + (L + 15) / 16);
+  uint32_t *out = pk.data() + w0;
+  const __m256i lower = _mm256_set1_epi8(0x20), three = _mm256_set1_epi8(3);
+  const __m256i tbl = _mm256_setr_epi8('a', 'c', 'g', 't', 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,  //
+                                       'a', 'c', 'g', 't', 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0);
+  size_t i = 0;
+  for (; i + 32 <= L; i += 32) {
+    const __m256i v = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(b + i));
+    const __m256i c = _mm256_and_si256(_mm256_xor_si256(_mm256_srli_epi16(v, 1), _mm256_srli_epi16(v, 2)), three);
+    const __m256i ok = _mm256_cmpeq_epi8(_mm256_shuffle_epi8(tbl, c), _mm256_or_si256(v, lower));
+    if ((uint32_t)_mm256_movemask_epi8(ok) != 0xffffffffu) {
+      pk.resize(w0);
+      return false;
+    }
+    alignas(32) uint64_t q[4];
+    _mm256_store_si256(reinterpret_cast<__m256i *>(q), c);
+    const uint64_t m = 0x0303030303030303ull;
+    out[i / 16] = (uint32_t)(_pext_u64(q[0], m) | (_pext_u64(q[1], m) << 16));
+    out[i / 16 + 1] = (uint32_t)(_pext_u64(q[2], m) | (_pext_u64(q[3], m) << 16));
+  }
+  uint32_t acc = 0;
+  int sh = 0;
+  for (; i < L; i++) {
+    const uint32_t v = kFast.v[b[i]];
+    if (v > 3) {
+      pk.resize(w0);
+      return false;
+    }
+    acc |= v << sh;
+    sh += 2;
+    if (sh == 32) {
+      out[i / 16] = acc;
+      acc = 0;
+      sh = 0;
+    }
+  }
+  if (sh) out[(L - 1) / 16] = acc;
+  return true;
+}
+
 inline bool line_start(const char *buf, size_t i) { return i == 0 || buf[i - 1] == '\n' || buf[i - 1] == '\r'; }
 
-// Records of buf[a, z) with safe_getline's line semantics (ChromListMaker.cpp:23-47): lines
-// end at "\n", "\r\n", a lone "\r", or EOF.  A line starting with '>' opens a record whose
-// header is the whole line; other lines are appended to the current record.  `eof`: the chunk
-// ends the file (the final empty read sets isBaseReady of the last record).
-void split_chunk(const char *buf, size_t a, size_t z, bool first, bool eof, const std::string &path, Chunk &ck) {
-  Chunk::Rec *cur = nullptr;
-  auto on_line = [&](size_t p, size_t len) {
-    if (len > 0 && buf[p] == '>') {
-      ck.recs.push_back({p, len, ck.bytes.size(), 0, false});
-      cur = &ck.recs.back();
-    } else {
-      if (!cur) {
-        if (len == 0) return;  // blank lines before the first header
-        if (first) throw Error("sequence data before the first '>' header in " + path, 1);
-        throw Error("internal: chunk does not start at a record", 1);
-      }
-      ck.bytes.insert(ck.bytes.end(), buf + p, buf + p + len);
-      cur->len += len;
-      cur->ready = true;
-    }
-  };
+// Calls on_line(pos, len) for the lines of buf[a, z) with safe_getline's semantics
+// (ChromListMaker.cpp:23-47): lines end at "\n", "\r\n", a lone "\r", or the end.
+template <class F>
+inline void for_lines(const char *buf, size_t a, size_t z, F &&on_line) {
   size_t pos = a;
   while (pos < z) {
     const char *p = buf + pos;
@@ -185,34 +232,92 @@ void split_chunk(const char *buf, size_t a, size_t z, bool first, bool eof, cons
       pos = z;
     }
   }
-  if (eof && cur) cur->ready = true;
 }
 
-void finish_chunk(Chunk &ck) {
-  ck.nseg.resize(ck.recs.size());
-  std::vector<int32_t> segs;
-  for (size_t r = 0; r < ck.recs.size(); r++) {
-    auto &rec = ck.recs[r];
-    if (!rec.ready) throw Error("The header and the sequence must be set before calling finalize", 1);
-    process_record(ck.bytes.data() + rec.off, rec.len, segs);
-    ck.seg.insert(ck.seg.end(), segs.begin(), segs.end());
-    ck.nseg[r] = segs.size() / 2;
-    const uint8_t *b = ck.bytes.data() + rec.off;
-    for (size_t i = 0; i < rec.len; i++)
-      if (b[i] > 3) {
-        ck.exc_pos.push_back(rec.off + i);
-        ck.exc_val.push_back(b[i]);
-      }
-    ck.words += (rec.len + 15) / 16;
+// Chromosome::help's segments for an N-free record of length L >= 20 (removeN: one run
+// [0, L-1]; mergeSegments keeps it; makeSegmentList: 1 Mb fragments, Chromosome.cpp:228-258)
+inline void plain_segments(int64_t L, std::vector<int32_t> &seg) {
+  const int64_t segLength = 1000000;
+  if (L > segLength) {
+    const int64_t fragNum = L / segLength;
+    for (int64_t h = 0; h < fragNum; h++) {
+      seg.push_back((int32_t)(h * segLength));
+      seg.push_back((int32_t)(h == fragNum - 1 ? L - 1 : h * segLength + segLength - 1));
+    }
+  } else {
+    seg.push_back(0);
+    seg.push_back((int32_t)(L - 1));
   }
 }
 
-// up to 16 one-digit bytes -> one word (bytes outside 0..3 pack as their low two bits; the
-// exception list restores them)
-inline uint32_t pack16(const uint8_t *b, size_t n) {
-  uint32_t w = 0;
-  for (size_t j = 0; j < n; j++) w |= (uint32_t)(b[j] & 3) << (2 * j);
-  return w;
+// Records of buf[a, z): a line starting with '>' opens a record whose header is the whole
+// line; other lines are appended to the current record.  `eof`: the chunk ends the file (the
+// final empty read sets isBaseReady of the last record).  A record's lines are gathered, then
+// plain records (A/C/G/T only, at least 20 bases: one N-free segment) are packed by
+// encode_plain; any other record goes through process_record.  A chunk without '\r' splits
+// lines at '\n' alone.
+void parse_chunk(const char *buf, size_t a, size_t z, bool first, bool eof, const std::string &path, Chunk &ck) {
+  Chunk::Rec *cur = nullptr;
+  std::vector<uint8_t> tmp;
+  std::vector<int32_t> segs;
+  auto close = [&]() {
+    if (!cur) return;
+    auto &r = *cur;
+    r.off = ck.bytes;
+    r.len = tmp.size();
+    ck.bytes += r.len;
+    if (r.len >= 20 && encode_plain(tmp.data(), tmp.size(), ck.pk)) {
+      const size_t s0 = ck.seg.size();
+      plain_segments((int64_t)r.len, ck.seg);
+      ck.nseg.push_back((ck.seg.size() - s0) / 2);
+    } else {
+      if (!r.ready) throw Error("The header and the sequence must be set before calling finalize", 1);
+      process_record(tmp.data(), tmp.size(), segs);
+      ck.seg.insert(ck.seg.end(), segs.begin(), segs.end());
+      ck.nseg.push_back(segs.size() / 2);
+      for (size_t j = 0; j < tmp.size(); j += 16) {
+        uint32_t x = 0;
+        for (size_t t = 0; t < 16 && j + t < tmp.size(); t++) {
+          const uint8_t c = tmp[j + t];
+          x |= (uint32_t)(c & 3) << (2 * t);
+          if (c > 3) {
+            ck.exc_pos.push_back(r.off + j + t);
+            ck.exc_val.push_back(c);
+          }
+        }
+        ck.pk.push_back(x);
+      }
+    }
+    tmp.clear();
+    cur = nullptr;
+  };
+  auto on_line = [&](size_t p, size_t len) {
+    if (len > 0 && buf[p] == '>') {
+      close();
+      ck.recs.push_back({p, len, 0, 0, (uint64_t)ck.pk.size(), false});
+      cur = &ck.recs.back();
+      return;
+    }
+    if (!cur) {
+      if (len == 0) return;  // blank lines before the first header
+      if (first) throw Error("sequence data before the first '>' header in " + path, 1);
+      throw Error("internal: chunk does not start at a record", 1);
+    }
+    tmp.insert(tmp.end(), buf + p, buf + p + len);
+    cur->ready = true;
+  };
+  if (memchr(buf + a, '\r', z - a)) {
+    for_lines(buf, a, z, on_line);
+  } else {
+    for (size_t pos = a; pos < z;) {
+      const char *nl = (const char *)memchr(buf + pos, '\n', z - pos);
+      const size_t e = nl ? (size_t)(nl - buf) : z;
+      on_line(pos, e - pos);
+      pos = e + 1;
+    }
+  }
+  if (cur && eof) cur->ready = true;
+  close();
 }
 
 }  // namespace
@@ -254,10 +359,7 @@ void parse_fasta_files(const std::vector<std::string> &files, Dataset &ds, int t
 #pragma omp parallel for schedule(dynamic, 1) num_threads(threads)
     for (int t = 0; t < T; t++) {
       try {
-        if (cut[t] < cut[t + 1]) {
-          split_chunk(buf, cut[t], cut[t + 1], t == 0, cut[t + 1] == n, path, ck[t]);
-          finish_chunk(ck[t]);
-        }
+        if (cut[t] < cut[t + 1]) parse_chunk(buf, cut[t], cut[t + 1], t == 0, cut[t + 1] == n, path, ck[t]);
       } catch (const std::exception &e) {
         ck[t].err = e.what();
       }
@@ -274,11 +376,11 @@ void parse_fasta_files(const std::vector<std::string> &files, Dataset &ds, int t
     uint64_t lsum = 0;
     for (int t = 0; t < T; t++) {
       rec0[t + 1] = rec0[t] + ck[t].recs.size();
-      byte0[t + 1] = byte0[t] + ck[t].bytes.size();
-      word0[t + 1] = word0[t] + ck[t].words;
+      byte0[t + 1] = byte0[t] + ck[t].bytes;
+      word0[t + 1] = word0[t] + ck[t].pk.size();
       seg0[t + 1] = seg0[t] + ck[t].seg.size() / 2;
       exc0[t + 1] = exc0[t] + ck[t].exc_pos.size();
-      lsum += ck[t].bytes.size();
+      lsum += ck[t].bytes;
     }
     const uint64_t nr = rec0[T], nwords = word0[T];
     ds.headers.resize(nr);
@@ -298,19 +400,18 @@ void parse_fasta_files(const std::vector<std::string> &files, Dataset &ds, int t
 #pragma omp parallel for schedule(dynamic, 1) num_threads(threads)
     for (int t = 0; t < T; t++) {
       const Chunk &c = ck[t];
-      uint64_t w = word0[t], sg = seg0[t];
+      uint64_t sg = seg0[t];
       for (size_t r = 0; r < c.recs.size(); r++) {
         const auto &rec = c.recs[r];
         const uint64_t id = rec0[t] + r;
         ds.headers[id].assign(buf + rec.hdr, rec.hdr_len);
         ds.lengths[id] = rec.len;
         ds.seq_off[id + 1] = byte0[t] + rec.off + rec.len;
-        const uint8_t *b = c.bytes.data() + rec.off;
-        for (size_t j = 0; j < rec.len; j += 16) ds.packed[w++] = pack16(b + j, std::min<size_t>(16, rec.len - j));
-        ds.pk_off[id + 1] = w;
+        ds.pk_off[id + 1] = word0[t] + (r + 1 < c.recs.size() ? c.recs[r + 1].w_off : c.pk.size());
         sg += c.nseg[r];
         ds.seg_off[id + 1] = sg;
       }
+      if (!c.pk.empty()) memcpy(ds.packed.data() + word0[t], c.pk.data(), c.pk.size() * 4);
       std::copy(c.seg.begin(), c.seg.end(), ds.seg.begin() + 2 * seg0[t]);
       for (size_t q = 0; q < c.exc_pos.size(); q++) {
         ds.exc_pos[exc0[t] + q] = byte0[t] + c.exc_pos[q];

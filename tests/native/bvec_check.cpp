@@ -139,7 +139,7 @@ struct FastAcc {
 
 int main() {
   std::mt19937_64 rng(777);
-  long checks = 0;
+  long checks = 0, fast_checks = 0;
   for (int t = 0; t < 300; t++) {
     const size_t n = t < 20 ? (size_t)t + 1 : (size_t)(rng() % 6000) + 1;
     std::vector<uint64_t> len(n);
@@ -201,6 +201,41 @@ int main() {
           printf("FAST MISMATCH t=%d it=%d\n", t, it);
           return 1;
         }
+        // the device controller's nearest-alive form (both edge bins non-empty)
+        {
+          uint64_t lo_, hi_;
+          mcg::bv_index_of_sorted(bv.begin_bounds(), fa.nbins(), bl, &lo_, &hi_);
+          const uint64_t fb = lo_;
+          mcg::bv_index_of_sorted(bv.begin_bounds(), fa.nbins(), el, &lo_, &hi_);
+          const uint64_t bb = hi_;
+          if (fa.cnt(fb) > 0 && fa.cnt(bb) > 0) {
+            const auto &sl = bv.static_lengths();
+            const uint64_t pf0 = std::lower_bound(sl.begin() + blo[fb], sl.begin() + blo[fb + 1], bl) - sl.begin();
+            const uint64_t plt = std::lower_bound(sl.begin() + blo[bb], sl.begin() + blo[bb + 1], el) - sl.begin();
+            const uint64_t ple = std::upper_bound(sl.begin() + blo[bb], sl.begin() + blo[bb + 1], el) - sl.begin();
+            auto next_alive = [&](uint64_t a, uint64_t z) -> uint64_t {
+              for (uint64_t p = a; p < z; p++)
+                if (fa.alive[p]) return p;
+              return ~0ull;
+            };
+            auto prev_alive = [&](uint64_t a, uint64_t z) -> uint64_t {
+              for (uint64_t p = z; p > a; p--)
+                if (fa.alive[p - 1]) return p - 1;
+              return ~0ull;
+            };
+            uint64_t S4 = 0, E4 = 0;
+            mcg::bv_fast_window(next_alive(pf0, blo[fb + 1]), prev_alive(blo[fb], pf0), next_alive(ple, blo[bb + 1]),
+                                prev_alive(blo[bb], ple), plt, &S4, &E4);
+            const bool has = E4 != ~0ull && S4 != ~0ull && E4 >= S4;
+            if (derr || has != (c2 > 0) || (has && (S4 != S2 || E4 != E2))) {
+              printf("NEAREST-ALIVE MISMATCH t=%d it=%d: core err %d count %lld S %llu E %llu / fast S %llu E %llu\n", t,
+                     it, derr, (long long)c2, (unsigned long long)S2, (unsigned long long)E2, (unsigned long long)S4,
+                     (unsigned long long)E4);
+              return 1;
+            }
+            fast_checks++;
+          }
+        }
         checks++;
       }
       // mutate
@@ -237,6 +272,6 @@ int main() {
       }
     }
   }
-  printf("OK %ld checks\n", checks);
+  printf("OK %ld checks (%ld nearest-alive)\n", checks, fast_checks);
   return 0;
 }
