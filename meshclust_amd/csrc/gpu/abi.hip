@@ -167,7 +167,7 @@ int mc_ctx_destroy(mc_ctx *c) {
   (void)hipStreamSynchronize(c->stream);
   for (Buf *b : {&c->codes, &c->seq_off, &c->seg, &c->seg_off, &c->packed, &c->pk_off, &c->impure, &c->hist, &c->mag, &c->sumsq, &c->len, &c->order,
                  &c->alive, &c->members, &c->member_keys, &c->partials, &c->scan_dev, &c->flags_out, &c->s_a, &c->s_b,
-                 &c->s_c, &c->s_d, &c->s_e, &c->s_f, &c->s_g, &c->s_h, &c->hs, &c->mag_s, &c->sumsq_s, &c->len_s, &c->ticket,
+                 &c->s_c, &c->s_d, &c->s_e, &c->s_f, &c->s_g, &c->s_h, &c->s_i, &c->s_j, &c->hs, &c->mag_s, &c->sumsq_s, &c->len_s, &c->ticket,
                  &c->msum, &c->ident_s, &c->al_a, &c->al_b, &c->al_out, &c->acc_out})
     release(*b);
   if (c->h_scan) (void)hipHostFree(c->h_scan);
@@ -384,6 +384,22 @@ int mc_set_classifier(mc_ctx *c, const mc_classifier *cls) {
   }
   c->cls.c = *cls;
   c->cls.align = align ? 1 : 0;
+  // the trainer's feature set (Feature::add_feature order: Feature.cpp:7-31) -> classify_std
+  c->cls.layout = 0;
+  const uint16_t want[5] = {MC_FEAT_LD, MC_FEAT_INTERSECTION, MC_FEAT_MANHATTAN, MC_FEAT_PEARSON, MC_FEAT_KULCZYNSKI2};
+  const int kinds[4] = {MC_COMBO_SELF, MC_COMBO_SQUARED, MC_COMBO_SELF, MC_COMBO_SQUARED};
+  const int lens[4] = {2, 2, 1, 2};
+  const int idx[4][2] = {{0, 1}, {0, 2}, {3, 0}, {0, 4}};
+  if (!align && (cls->n_single == 4 || cls->n_single == 5) && cls->n_combo == cls->n_single - 1) {
+    bool ok = true;
+    for (int i = 0; i < cls->n_single; i++) ok &= cls->lookup[i] == want[i];
+    for (int j = 0; j < cls->n_combo; j++) {
+      ok &= cls->combo_kind[j] == kinds[j] && cls->combo_len[j] == lens[j];
+      for (int e = 0; e < lens[j]; e++) ok &= cls->combo_idx[j][e] == idx[j][e];
+    }
+    if (ok) c->cls.layout = cls->n_single == 4 ? 3 : 4;
+  }
+  if (getenv("MC_CLASSIFY_GENERIC")) c->cls.layout = 0;  // diagnostics: the generic form only
   c->has_cls = true;
   return MC_OK;
 }
@@ -753,7 +769,7 @@ int mc_accumulate(mc_ctx *c, const uint32_t *bin_lo, const uint64_t *bounds, uin
   }
   if (getenv("MC_ACCUM_PROFILE")) {
     fprintf(stderr, "[accum] steps %llu window %.3f (centre data %.3f window %.3f record %.3f) wait %.3f collect %.3f "
-            "(reduce %.3f gather+kill %.3f sums+mean %.3f closest %.3f) ms\n",
+            "(stragglers+reduce %.3f column sums %.3f mean %.3f closest %.3f) ms\n",
             (unsigned long long)out[1], out[5] / 1e5, out[12] / 1e5, out[13] / 1e5, out[14] / 1e5, out[6] / 1e5,
             out[7] / 1e5, out[8] / 1e5, out[9] / 1e5, out[10] / 1e5, out[11] / 1e5);
     if (atoi(getenv("MC_ACCUM_PROFILE")) >= 2 && c->s_h.p) {

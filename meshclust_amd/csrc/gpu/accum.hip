@@ -29,8 +29,11 @@
 // in handoff-1to1):
 //   controller -> workers   the step record: centre row + magnitudes, window S..E, kill-log
 //                           length and its last KINL entries (pops / erases)
-//   workers -> controller   the flagged candidates (position, magnitudes, row: sc1 stores,
-//                           drained), then a 5-granule partial {max, position, flagged, scanned}
+//   workers -> controller   an 8-granule partial {max, position, flagged, scanned, the first
+//                           INL flagged positions} (further flagged positions in a list, sc1
+//                           stores drained before the partial); the controller loads the
+//                           flagged rows from the read-only static layout itself, while it is
+//                           still waiting for the slower workers
 // Every spin has a deadline (error 99: never a hang).
 #include <algorithm>
 #include <cstdlib>
@@ -51,7 +54,10 @@ constexpr uint32_t RING = 64;          // step records kept for workgroups that 
 constexpr uint32_t TRACE_STEPS = 4096;
 constexpr int KINL = 4;                // kill-log entries carried inline in a step record
 constexpr int REC_HDR = 14;            // centre, S, E, kn, KINL kills, mag / sumsq / len (2 each)
-constexpr int PART_G = 8;              // granules per partial (5 used)
+constexpr int PART_G = 8;              // granules per partial
+constexpr int INL = 3;                 // flagged positions carried inline in a partial
+constexpr uint32_t PLIST = 1024;       // flagged positions of one step listed in the controller's LDS
+constexpr uint32_t GMAX = 256;         // workgroups: the controller polls the G - 1 workers' partials with one thread each
 
 // Static part of a centre's bvec window (bvec::get_range, bvec.cpp:245-278), per static
 // position: the window lengths, the bins index_of picks, and how many static positions of
@@ -61,6 +67,13 @@ struct WinTab {
   uint32_t fb, bb;          // index_of(bl).low, index_of(el).high
   uint32_t kf, kblt, kble;  // static positions of bin fb with length < bl; of bin bb < el, <= el
   uint32_t pad;
+};
+
+// What the controller needs of a static position when it joins a cluster: magnitudes and
+// window data, one 64-byte line (its row is in the row-major static copy `hr`)
+struct MInfo {
+  uint64_t mag, sumsq, len, pad;
+  WinTab wt;
 };
 
 struct AccArgs {
@@ -74,7 +87,8 @@ struct AccArgs {
   uint32_t nb;
   const uint32_t *bin_lo;  // nb + 1 static starts
   const uint64_t *bounds;  // nb begin_bounds
-  const WinTab *wtab;      // per static position
+  const MInfo *minfo;      // per static position
+  const uint4 *hr;         // rows in static order, row-major (nch chunks each)
   uint32_t *gbits;         // alive bitmap in global memory (n too large for LDS), else null
   // hand-off
   uint64_t *ring;  // RING records of rec_g granules
@@ -82,9 +96,7 @@ struct AccArgs {
   uint32_t *klog;      // static positions killed by the controller (pop / erase), append-only
   uint32_t *go;        // latest published step (for a workgroup that fell RING steps behind)
   uint64_t *partials;  // G * PART_G granules
-  uint32_t *fpos;      // worker w's flagged positions at w * fcap
-  uint64_t *finfo;     // ... their mag / sumsq / len (3 words each)
-  uint4 *frow;         // ... their rows (nch chunks each)
+  uint32_t *fpos;      // worker w's flagged positions beyond the INL inline ones, at w * fcap
   uint64_t fcap;
   int res;        // chunks per worker whose rows live in its LDS (0: rows stream from memory)
   uint32_t mrow;  // member cache entries (LDS)
@@ -115,16 +127,6 @@ __device__ __forceinline__ uint64_t ld64(const uint64_t *p) {
 }
 __device__ __forceinline__ uint32_t ld32(const uint32_t *p) {
   return __hip_atomic_load(const_cast<uint32_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st128(uint4 *p, const uint4 &v) {
-  uint64_t *q = reinterpret_cast<uint64_t *>(p);
-  st64(q, ((uint64_t)v.y << 32) | v.x);
-  st64(q + 1, ((uint64_t)v.w << 32) | v.z);
-}
-__device__ __forceinline__ uint4 ld128(const uint4 *p) {
-  const uint64_t *q = reinterpret_cast<const uint64_t *>(p);
-  const uint64_t a = ld64(q), b = ld64(q + 1);
-  return make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
 }
 __device__ __forceinline__ void drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 __device__ __forceinline__ uint64_t gran(uint32_t tag, uint32_t data) { return ((uint64_t)tag << 32) | data; }
@@ -307,9 +309,12 @@ __device__ uint64_t lower_len(const uint64_t *len_s, uint64_t a, uint64_t z, uin
 }
 
 __global__ __launch_bounds__(256) void wintab_kernel(uint64_t n, const uint64_t *__restrict__ len_s,
+                                                     const uint64_t *__restrict__ mag_s,
+                                                     const uint64_t *__restrict__ sumsq_s,
                                                      const uint32_t *__restrict__ bin_lo,
                                                      const uint64_t *__restrict__ bnd, uint32_t nb, double sim,
-                                                     WinTab *__restrict__ out) {
+                                                     const uint4 *__restrict__ hs, uint64_t npad, int nch,
+                                                     MInfo *__restrict__ out, uint4 *__restrict__ hr) {
   for (uint64_t id = (uint64_t)blockIdx.x * 256 + threadIdx.x; id < n; id += (uint64_t)gridDim.x * 256) {
     const uint64_t L = len_s[id];  // id = static position
     WinTab w;
@@ -324,7 +329,14 @@ __global__ __launch_bounds__(256) void wintab_kernel(uint64_t n, const uint64_t 
     w.kblt = (uint32_t)(lower_len(len_s, bin_lo[w.bb], bin_lo[w.bb + 1], w.el, false) - bin_lo[w.bb]);
     w.kble = (uint32_t)(lower_len(len_s, bin_lo[w.bb], bin_lo[w.bb + 1], w.el, true) - bin_lo[w.bb]);
     w.pad = 0;
-    out[id] = w;
+    MInfo m;
+    m.mag = mag_s[id];
+    m.sumsq = sumsq_s[id];
+    m.len = L;
+    m.pad = 0;
+    m.wt = w;
+    out[id] = m;
+    for (int c = 0; c < nch; c++) hr[id * nch + c] = hs[(uint64_t)c * npad + id];
   }
 }
 
@@ -334,6 +346,7 @@ template <typename T>
 __device__ __forceinline__ int classify_cand(const Acc<T> &acc, const PInfo &pi, const PInfo &pc, int B,
                                              const DevClassifier &C, double *cv) {
   const PS s = acc.finish(pi.mag, pc.mag);
+  if (C.layout) return classify_std(C, s, pi, pterms(pi.mag, pi.sumsq, B), pc, pterms(pc.mag, pc.sumsq, B), B, cv);
   double raw[MC_MAX_SINGLE];
 #pragma unroll
   for (int i = 0; i < MC_MAX_SINGLE; i++) raw[i] = i < C.c.n_single ? raw_fast(C.c.lookup[i], s, pi, pc, B) : 0.0;
@@ -350,7 +363,7 @@ template <typename T, int NCH>
 __device__ __forceinline__ void worker(const AccArgs &A, const DevClassifier &C, uint4 *dyn) {
   __shared__ double s_bv[NW];
   __shared__ uint64_t s_bp[NW];
-  __shared__ uint32_t s_nfl, s_nscan, s_go;
+  __shared__ uint32_t s_nfl, s_nscan, s_go, s_inl[INL];
   __shared__ int s_abort;
   constexpr int NC = NCH > 0 ? NCH : 1;
   const uint32_t GW = gridDim.x - 1, w = blockIdx.x - 1;
@@ -367,6 +380,7 @@ __device__ __forceinline__ void worker(const AccArgs &A, const DevClassifier &C,
   for (uint64_t i = threadIdx.x; i < A.fcap; i += NT) lal[i] = 1;
   const int res = A.res;
   uint64_t rmag[2] = {0, 0}, rsq[2] = {0, 0}, rlen[2] = {0, 0};  // resident magnitudes (res <= 2 kept here)
+  PTerms rterm[2] = {{0, 0, 0.0}, {0, 0, 0.0}};
   for (int i = 0; i < res; i++) {
     const uint64_t pos = ((uint64_t)w + (uint64_t)i * GW) * NT + threadIdx.x;
     for (int k = 0; k < nch; k++)
@@ -375,6 +389,7 @@ __device__ __forceinline__ void worker(const AccArgs &A, const DevClassifier &C,
       rmag[i] = A.mag_s[pos];
       rsq[i] = A.sumsq_s[pos];
       rlen[i] = A.len_s[pos];
+      rterm[i] = pterms(rmag[i], rsq[i], A.B);
     }
   }
   if (threadIdx.x == 0) s_abort = 0;
@@ -461,6 +476,7 @@ __device__ __forceinline__ void worker(const AccArgs &A, const DevClassifier &C,
     const PInfo pc{(uint64_t)hdr[4 + KINL] | ((uint64_t)hdr[5 + KINL] << 32),
                    (uint64_t)hdr[6 + KINL] | ((uint64_t)hdr[7 + KINL] << 32),
                    (uint64_t)hdr[8 + KINL] | ((uint64_t)hdr[9 + KINL] << 32)};
+    const PTerms tq = pterms(pc.mag, pc.sumsq, A.B);  // the centre's pair-independent terms
     // the controller's kills since the last record applied here: each thread clears the
     // flags of the positions it owns (offset = its thread index), so no barrier is needed
     {
@@ -486,14 +502,12 @@ __device__ __forceinline__ void worker(const AccArgs &A, const DevClassifier &C,
     uint64_t best_p = NONE64;
     uint32_t nscan = 0;
     const uint64_t base = (uint64_t)w * A.fcap;
-    // a slot of this worker's flagged list; position and magnitudes (the caller stores the row)
-    auto flag_slot = [&](uint64_t pos, const PInfo &pi) -> uint64_t {
-      const uint64_t slot = base + atomicAdd(&s_nfl, 1u);
-      st32(A.fpos + slot, (uint32_t)pos);
-      st64(A.finfo + slot * 3 + 0, pi.mag);
-      st64(A.finfo + slot * 3 + 1, pi.sumsq);
-      st64(A.finfo + slot * 3 + 2, pi.len);
-      return slot;
+    // a flagged candidate: its position goes inline into the partial (the first INL) or to
+    // this worker's list; the controller reads rows and magnitudes itself (read-only data)
+    auto flag_pos = [&](uint64_t pos) {
+      const uint32_t idx = atomicAdd(&s_nfl, 1u);
+      if (idx < (uint32_t)INL) s_inl[idx] = (uint32_t)pos;
+      else st32(A.fpos + base + idx, (uint32_t)pos);
     };
     for (uint64_t ch = c0 + mine; ch <= c1; ch += GW) {
       const uint64_t li = ch / GW;  // local chunk index
@@ -511,12 +525,17 @@ __device__ __forceinline__ void worker(const AccArgs &A, const DevClassifier &C,
         } else {
           for (int k = 0; k < nch; k++) acc.add(rr[(uint64_t)k * NT], clds[k]);
         }
-        const PInfo pi = li < 2 ? PInfo{rmag[li], rsq[li], rlen[li]} : PInfo{A.mag_s[pos], A.sumsq_s[pos], A.len_s[pos]};
-        const int d = classify_cand<T>(acc, pi, pc, A.B, C, &cv);
+        int d;
+        if (li < 2 && C.layout) {
+          d = classify_std(C, acc.finish(rmag[li], pc.mag), PInfo{rmag[li], rsq[li], rlen[li]}, rterm[li], pc, tq, A.B,
+                           &cv);
+        } else {
+          const PInfo pi = li < 2 ? PInfo{rmag[li], rsq[li], rlen[li]} : PInfo{A.mag_s[pos], A.sumsq_s[pos], A.len_s[pos]};
+          d = classify_cand<T>(acc, pi, pc, A.B, C, &cv);
+        }
         if (d) {
           *la = 0;
-          const uint64_t slot = flag_slot(pos, pi);
-          for (int k = 0; k < nch; k++) st128(A.frow + slot * nch + k, rr[(uint64_t)k * NT]);
+          flag_pos(pos);
         }
       } else {  // streaming: the rows come from memory
         const uint4 *col = A.hs + pos;
@@ -527,22 +546,17 @@ __device__ __forceinline__ void worker(const AccArgs &A, const DevClassifier &C,
           const PInfo pi{A.mag_s[pos], A.sumsq_s[pos], A.len_s[pos]};
 #pragma unroll
           for (int k = 0; k < NC; k++) acc.add(v[k], clds[k]);
-          const int d = classify_cand<T>(acc, pi, pc, A.B, C, &cv);
-          if (d) {
+          if (classify_cand<T>(acc, pi, pc, A.B, C, &cv)) {
             *la = 0;
-            const uint64_t slot = flag_slot(pos, pi);
-#pragma unroll
-            for (int k = 0; k < NC; k++) st128(A.frow + slot * NC + k, v[k]);
+            flag_pos(pos);
           }
         } else {
 #pragma unroll 8
           for (int k = 0; k < nch; k++) acc.add(col[(uint64_t)k * A.npad], clds[k]);
           const PInfo pi{A.mag_s[pos], A.sumsq_s[pos], A.len_s[pos]};
-          const int d = classify_cand<T>(acc, pi, pc, A.B, C, &cv);
-          if (d) {
+          if (classify_cand<T>(acc, pi, pc, A.B, C, &cv)) {
             *la = 0;
-            const uint64_t slot = flag_slot(pos, pi);
-            for (int k = 0; k < nch; k++) st128(A.frow + slot * nch + k, col[(uint64_t)k * A.npad]);
+            flag_pos(pos);
           }
         }
       }
@@ -568,7 +582,7 @@ __device__ __forceinline__ void worker(const AccArgs &A, const DevClassifier &C,
       s_bp[wv] = best_p;
       atomicAdd(&s_nscan, nscan);
     }
-    drain();  // this wave's flagged-record stores are complete before the partial announces them
+    drain();  // this wave's flagged-list stores are complete before the partial announces them
     __syncthreads();
     if (threadIdx.x == 0) {
       double v = s_bv[0];
@@ -585,6 +599,7 @@ __device__ __forceinline__ void worker(const AccArgs &A, const DevClassifier &C,
       st64(q + 2, gran(seen, p == NONE64 ? NONE : (uint32_t)p));
       st64(q + 3, gran(seen, s_nfl));
       st64(q + 4, gran(seen, s_nscan));
+      for (int j = 0; j < INL; j++) st64(q + 5 + j, gran(seen, (uint32_t)j < s_nfl ? s_inl[j] : NONE));
       if (A.trace && mine == nact - 1 && seen < TRACE_STEPS) {
         uint64_t *tr = A.trace + (uint64_t)seen * 8;
         tr[2] = t_seen;
@@ -605,7 +620,8 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
   __shared__ uint64_t s_red[3 * NW];
   __shared__ double s_bv[NW];
   __shared__ uint64_t s_bp[NW];
-  __shared__ uint32_t s_flag[NT];  // per active worker: offset of its flagged list
+  __shared__ uint32_t s_new;  // members taken into the cluster this step
+  __shared__ uint32_t s_plist[PLIST];  // ... their positions
   __shared__ uint64_t s_q[4];
   __shared__ uint32_t s_klast[KINL];
   __shared__ int s_abort;
@@ -614,7 +630,6 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
   const uint32_t GW = gridDim.x - 1;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int nch = NCH > 0 ? NCH : A.nch;
-  const RowRef Rs{A.hs, 1, A.npad};
   const int rec_words = (int)A.rec_g;
   uint8_t *Fl = reinterpret_cast<uint8_t *>(dyn);  // integer mean row
   uint64_t *msum = reinterpret_cast<uint64_t *>(Fl + (size_t)nch * 16);
@@ -639,7 +654,10 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
     mc.pos = reinterpret_cast<uint32_t *>(p);
   }
   for (int i = threadIdx.x; i < nch * 16; i += NT) Fl[i] = 0;  // the mean row's padding stays zero
-  if (threadIdx.x == 0) s_abort = 0;
+  if (threadIdx.x == 0) {
+    s_abort = 0;
+    s_new = 0;
+  }
   uint64_t lg = 1;
   while (lg * 2 <= A.nb) lg *= 2;
   DevBvec bv{A.gbits ? A.gbits : lbits, A.gbits != nullptr, cnt, fw, lo, bnd, A.len_s, A.nb, lg};
@@ -650,9 +668,10 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
   uint64_t ncl = 0, nsteps = 0, ncand = 0;
   uint32_t step = 0;
   uint64_t err = 0;
-  uint32_t kn = 0;  // kill-log length
+  uint32_t kn = 0;      // kill-log length
+  uint32_t kn_pub = 0;  // ... when the last record was published
   uint64_t t_wait = 0, t_coll = 0, t_mark = 0;
-  uint64_t t_sub[4] = {0, 0, 0, 0};  // collect: reduce, gather + kill, column sums + mean, closest
+  uint64_t t_sub[4] = {0, 0, 0, 0};  // collect: reduce (stragglers), column sums, mean, closest
   uint64_t t_ws[4] = {0, 0, 0, 0};   // window: centre window data, window, record, -
 
   auto finish_cluster = [&]() {
@@ -670,17 +689,18 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
       st32(A.mem_pos + cl_start, (uint32_t)pos);
       st64(A.mkeys + cl_start, 0);
       if (A.mrow) {
+        const MInfo mi = A.minfo[pos];
         mc.pos[0] = (uint32_t)pos;
         mc.key[0] = 0;
-        mc.info[0] = A.mag_s[pos];
-        mc.info[1] = A.sumsq_s[pos];
-        mc.info[2] = A.len_s[pos];
-        mc.wt[0] = A.wtab[pos];
+        mc.info[0] = mi.mag;
+        mc.info[1] = mi.sumsq;
+        mc.info[2] = mi.len;
+        mc.wt[0] = mi.wt;
       }
     }
     if (A.mrow)
-      for (int c = threadIdx.x; c < nch; c += NT) mc.row[c] = Rs.chunk(pos, c);
-    for (int b = threadIdx.x; b < A.B; b += NT) msum[b] = elem<T>(Rs, pos, b);
+      for (int c = threadIdx.x; c < nch; c += NT) mc.row[c] = A.hr[pos * nch + c];
+    for (int b = threadIdx.x; b < A.B; b += NT) msum[b] = reinterpret_cast<const T *>(A.hr + pos * nch)[b];
     M = 1;
     last_q = 0;
     drain();
@@ -707,7 +727,7 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
     const bool cached = last_q < A.mrow;
     if (j < 4 * nch) {
       if (last == NONE) return 0;
-      const uint4 v = cached ? mc.row[(size_t)last_q * mc.rp + j / 4] : Rs.chunk(last, j / 4);
+      const uint4 v = cached ? mc.row[(size_t)last_q * mc.rp + j / 4] : A.hr[(uint64_t)last * nch + j / 4];
       return (j & 3) == 0 ? v.x : (j & 3) == 1 ? v.y : (j & 3) == 2 ? v.z : v.w;
     }
     const int h = j - 4 * nch;
@@ -724,6 +744,36 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
     const uint64_t v =
         cached ? mc.info[(size_t)last_q * 3 + f] : (f == 0 ? A.mag_s[last] : f == 1 ? A.sumsq_s[last] : A.len_s[last]);
     return hi ? (uint32_t)(v >> 32) : (uint32_t)v;
+  };
+
+  // member qm of the current cluster is static position p, flagged in this step (key step << 32
+  // | p orders members like the bvec walk): member list, cache entry (row, magnitudes, window
+  // data from the read-only static arrays) or column sums past the cache, and the bvec kill
+  auto take = [&](uint64_t qm, uint32_t p) {
+    const uint64_t key = ((uint64_t)step << 32) | p;
+    st32(A.mem_pos + cl_start + qm, p);
+    st64(A.mkeys + cl_start + qm, key);
+    const uint4 *hrow = A.hr + (uint64_t)p * nch;
+    if (qm < A.mrow) {
+      const MInfo mi = A.minfo[p];
+      mc.pos[qm] = p;
+      mc.key[qm] = key;
+      mc.info[qm * 3 + 0] = mi.mag;
+      mc.info[qm * 3 + 1] = mi.sumsq;
+      mc.info[qm * 3 + 2] = mi.len;
+      mc.wt[qm] = mi.wt;
+      for (int k = 0; k < nch; k++) mc.row[qm * mc.rp + k] = hrow[k];
+    } else {
+      constexpr int per = 16 / (int)sizeof(T);
+      for (int k = 0; k < nch; k++) {
+        const uint4 v = hrow[k];
+        const T *pv = reinterpret_cast<const T *>(&v);
+#pragma unroll
+        for (int e = 0; e < per; e++)
+          if (pv[e]) atomicAdd((unsigned long long *)&msum[k * per + e], (unsigned long long)pv[e]);
+      }
+    }
+    bv.kill_one(p);
   };
 
   // bvec after insert_finalize: every static position alive
@@ -759,7 +809,7 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
     uint64_t S = 0, E = 0;
     bool have = false;
     while (last != NONE && !err) {
-      const WinTab wt = last_q < A.mrow ? mc.wt[last_q] : A.wtab[last];  // the centre's window data
+      const WinTab wt = last_q < A.mrow ? mc.wt[last_q] : A.minfo[last].wt;  // the centre's window data
       if (A.prof && threadIdx.x == 0) {
         drain();
         const uint64_t t = now();
@@ -814,12 +864,13 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
     // step; the kill-log entries are drained first (a late reader finds them there)
     if (wv == 0) {
       uint64_t *r = A.ring + (uint64_t)(step % RING) * A.rec_g;
-      drain();
+      if (kn != kn_pub) drain();  // kill-log entries written since the last record
       for (int j = lane; j < rec_words; j += 64) st64(r + j, gran(step, rec_word(j, have, S, E)));
       // `go` is only a hint for a worker that fell RING steps behind: it re-validates the
       // record's tags after reading it
       if (lane == 0) st32(A.go, step);
     }
+    kn_pub = kn;
     if (A.prof && threadIdx.x == 0) {
       const uint64_t t = now();
       t_ws[2] += t - t_mark;
@@ -831,28 +882,51 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
     // ============ collect the step (get_close's reduction + get_mean) ======================
     const uint64_t c0 = S / NT, c1 = E / NT;
     const uint32_t nact = (uint32_t)(c1 - c0 + 1 < (uint64_t)GW ? c1 - c0 + 1 : (uint64_t)GW);
-    // thread t polls the partial of the t-th active worker until its granules carry the step
+    // thread t polls the partial of the t-th active worker until its granules carry the step,
+    // then lists that worker's flagged positions (a slot from an LDS counter: member order is
+    // irrelevant, the keys step << 32 | position order them like the bvec walk)
     double bv_ = -1.0;
     uint64_t bp_ = NONE64;
     uint32_t cnt_w = 0, scan_w = 0;
-    if (threadIdx.x < nact) {
-      const uint64_t *q = A.partials + (uint64_t)((c0 + threadIdx.x) % GW) * PART_G;
+    if (threadIdx.x < nact) {  // (nact <= G - 1 < NT)
+      const uint32_t wk = (uint32_t)((c0 + threadIdx.x) % GW);
+      const uint64_t *q = A.partials + (uint64_t)wk * PART_G;
       const uint64_t t0 = now();
+      uint64_t g8[PART_G];
       for (uint32_t it = 1;; it++) {
-        const uint64_t w0 = ld64(q + 0), w1 = ld64(q + 1), w2 = ld64(q + 2), w3 = ld64(q + 3), w4 = ld64(q + 4);
-        if ((uint32_t)(w0 >> 32) == step && (uint32_t)(w1 >> 32) == step && (uint32_t)(w2 >> 32) == step &&
-            (uint32_t)(w3 >> 32) == step && (uint32_t)(w4 >> 32) == step) {
-          bv_ = __longlong_as_double((long long)((w0 << 32) | (w1 & 0xffffffffull)));
-          bp_ = (uint32_t)w2 == NONE ? NONE64 : (uint64_t)(uint32_t)w2;
-          cnt_w = (uint32_t)w3;
-          scan_w = (uint32_t)w4;
-          break;
+        // one granule per poll (less traffic in the CU's memory queue); all of them, each
+        // checked, once that one carries the step
+        bool ok = (uint32_t)(ld64(q + 4 + INL) >> 32) == step;
+        if (ok) {
+#pragma unroll
+          for (int j = 0; j < 5 + INL; j++) {
+            g8[j] = ld64(q + j);
+            ok &= (uint32_t)(g8[j] >> 32) == step;
+          }
         }
+        if (ok) break;
         if ((it & 255) == 0 && timed_out(A, t0)) {
           s_abort = 1;
           break;
         }
         __builtin_amdgcn_s_sleep(1);
+      }
+      if (!s_abort) {
+        bv_ = __longlong_as_double((long long)((g8[0] << 32) | (g8[1] & 0xffffffffull)));
+        bp_ = (uint32_t)g8[2] == NONE ? NONE64 : (uint64_t)(uint32_t)g8[2];
+        cnt_w = (uint32_t)g8[3];
+        scan_w = (uint32_t)g8[4];
+        // this worker's flagged positions into the step's list (a slot per position)
+        for (uint32_t j = 0; j < cnt_w; j++) {
+          const uint32_t p = j < (uint32_t)INL ? (uint32_t)g8[5 + j] : ld32(A.fpos + (uint64_t)wk * A.fcap + j);
+          const uint32_t slot = atomicAdd(&s_new, 1u);
+          if (slot < PLIST) {
+            s_plist[slot] = p;
+          } else {  // a list overflow: this thread takes the member itself (past the cache)
+            take(M + slot, p);
+            drain();
+          }
+        }
       }
     }
     if (A.prof && threadIdx.x == 0) {
@@ -860,13 +934,7 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
       t_wait += t - t_mark;
       t_mark = t;
     }
-    // block reduction: exclusive prefix of the flagged counts (offsets of the lists in worker
-    // order), the first maximum, the scanned total
-    uint32_t inc = cnt_w;
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t u = (uint32_t)__shfl_up((int)inc, o, 64);
-      if (lane >= o) inc += u;
-    }
+    // block reduction: the first maximum, the flagged and scanned totals
     for (int o = 32; o >= 1; o >>= 1) {
       const double ov = __shfl_xor(bv_, o, 64);
       const uint64_t op = shfl_xor64(bp_, o);
@@ -875,24 +943,24 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
         bp_ = op;
       }
     }
-    const uint32_t wscan = wave_sum32(scan_w);
-    if (lane == 63) s_red[wv] = inc;
+    const uint32_t wscan = wave_sum32(scan_w), wflag = wave_sum32(cnt_w);
     if (lane == 0) {
       s_bv[wv] = bv_;
       s_bp[wv] = bp_;
+      s_red[wv] = wflag;
       s_red[NW + wv] = wscan;
     }
+    if (threadIdx.x == 0) s_sumF = 0;
     __syncthreads();
     if (A.trace && threadIdx.x == 0 && step < TRACE_STEPS) A.trace[(uint64_t)step * 8 + 5] = now();
     if (s_abort) {
       if (threadIdx.x == 0) atomicMax((unsigned long long *)&A.out[3], 99ull);
       return;
     }
-    uint64_t nflag = 0, before = 0, nsc = 0;
+    uint64_t nflag = 0, nsc = 0;
     double best_val = s_bv[0];
     uint64_t best_pos = s_bp[0];
     for (int i = 0; i < NW; i++) {
-      if (i < wv) before += s_red[i];
       nflag += s_red[i];
       nsc += s_red[NW + i];
       if (i && better(s_bv[i], s_bp[i], best_val, best_pos)) {
@@ -901,75 +969,57 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
       }
     }
     ncand += nsc;
-    if (threadIdx.x < nact) s_flag[threadIdx.x] = (uint32_t)(before + inc - cnt_w);
-    __syncthreads();
     uint64_t tq = 0;
     if (A.prof && threadIdx.x == 0) {
       tq = now();
       t_sub[0] += tq - t_mark;
     }
     if (nflag > 0) {
-      // remove_available: the flagged positions join the cluster (their keys order them like
-      // the bvec walk: step, then position); rows and magnitudes come with the flagged records
-      const uint64_t mb = cl_start + M;
-      for (uint64_t i = threadIdx.x; i < nflag; i += NT) {
-        uint32_t a = 0, z = nact;  // last active worker with offset <= i
-        while (z - a > 1) {
-          const uint32_t m = (a + z) / 2;
-          if (s_flag[m] <= i) a = m;
-          else z = m;
-        }
-        const uint64_t slot = (uint64_t)((c0 + a) % GW) * A.fcap + (i - s_flag[a]);
-        const uint32_t p = ld32(A.fpos + slot);
-        const uint64_t mg = ld64(A.finfo + slot * 3 + 0), sq = ld64(A.finfo + slot * 3 + 1),
-                       ln = ld64(A.finfo + slot * 3 + 2);
-        const uint64_t key = ((uint64_t)step << 32) | p;
-        const uint64_t q = M + i;
-        st32(A.mem_pos + mb + i, p);
-        st64(A.mkeys + mb + i, key);
-        if (q < A.mrow) {
-          mc.pos[q] = p;
-          mc.key[q] = key;
-          mc.info[q * 3 + 0] = mg;
-          mc.info[q * 3 + 1] = sq;
-          mc.info[q * 3 + 2] = ln;
-          mc.wt[q] = A.wtab[p];
-          for (int k = 0; k < nch; k++) mc.row[q * mc.rp + k] = ld128(A.frow + slot * nch + k);
-        } else {  // beyond the cache: column sums straight from the row
-          constexpr int per = 16 / (int)sizeof(T);
-          for (int k = 0; k < nch; k++) {
-            const uint4 v = ld128(A.frow + slot * nch + k);
-            const T *pv = reinterpret_cast<const T *>(&v);
+      // remove_available: the new members, one thread each, all their loads in flight at once
+      // (member i on thread i + 64: wave 0, which publishes the next record, keeps no
+      // outstanding stores for that record's drain to wait on)
+      for (uint64_t i = (threadIdx.x + NT - 64) % NT; i < nflag && i < PLIST; i += NT) take(M + i, s_plist[i]);
+      if (M + nflag > A.mrow) drain();  // members past the cache are read back from mem_pos / mkeys
+      __syncthreads();
+      // column sums of the cached new members: thread (word w of a row, member slice sl) adds
+      // up its 32-bit word over the slice's members, then one LDS atomic per bin and thread
+      const uint64_t q0 = M, q1 = M + nflag < A.mrow ? M + nflag : (uint64_t)A.mrow;
+      M += nflag;
+      {
+        constexpr int per = 4 / (int)sizeof(T);  // bins per 32-bit word
+        const int wpr = (A.B + per - 1) / per;
+        const int nsl = wpr >= NT ? 1 : NT / wpr;
+        for (int t = threadIdx.x; t < wpr * nsl; t += NT) {
+          const int wd = t % wpr, sl = t / wpr;
+          uint32_t sum[per];
 #pragma unroll
-            for (int e = 0; e < per; e++)
-              if (pv[e]) atomicAdd((unsigned long long *)&msum[k * per + e], (unsigned long long)pv[e]);
+          for (int e = 0; e < per; e++) sum[e] = 0;
+          for (uint64_t q = q0 + (uint64_t)sl; q < q1; q += (uint64_t)nsl) {
+            const uint32_t x = reinterpret_cast<const uint32_t *>(mc.row + q * mc.rp)[wd];
+#pragma unroll
+            for (int e = 0; e < per; e++) sum[e] += sizeof(T) == 1 ? (x >> (8 * e)) & 0xffu : (x >> (16 * e)) & 0xffffu;
           }
+#pragma unroll
+          for (int e = 0; e < per; e++)
+            if (sum[e] && wd * per + e < A.B) atomicAdd((unsigned long long *)&msum[wd * per + e], (unsigned long long)sum[e]);
         }
-        bv.kill_one(p);
       }
-      drain();
       __syncthreads();
       if (A.prof && threadIdx.x == 0) {
         const uint64_t t = now();
         t_sub[1] += t - tq;
         tq = t;
       }
-      // column sums of the cached new members (one thread per bin), then the integer mean
-      // F_b = floor(S_b / M) and its total (features.hpp: get_mean as a SAD reduction)
-      const uint64_t q0 = M, q1 = M + nflag < A.mrow ? M + nflag : (uint64_t)A.mrow;
-      M += nflag;
+      // the integer mean F_b = floor(S_b / M) and its total (features.hpp: get_mean as a SAD
+      // reduction)
       uint64_t part = 0;
       for (int b = threadIdx.x; b < A.B; b += NT) {
-        uint64_t s = msum[b];
-        for (uint64_t q = q0; q < q1; q++) s += reinterpret_cast<const T *>(mc.row + q * mc.rp)[b];
-        msum[b] = s;
-        const uint64_t F = (s >> 32) == 0 ? (uint64_t)((uint32_t)s / (uint32_t)M) : s / M;
+        const uint64_t sb = msum[b];
+        const uint64_t F = (sb >> 32) == 0 ? (uint64_t)((uint32_t)sb / (uint32_t)M) : sb / M;
         reinterpret_cast<T *>(Fl)[b] = (T)F;
         part += F;
       }
       for (int o = 32; o >= 1; o >>= 1) part += shfl_xor64(part, o);
-      if (threadIdx.x == 0) s_sumF = 0;
-      __syncthreads();
       if (lane == 0 && part) atomicAdd((unsigned long long *)&s_sumF, (unsigned long long)part);
       __syncthreads();
       if (A.prof && threadIdx.x == 0) {
@@ -997,7 +1047,7 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
           key = mc.key[q];
         } else {
           const uint64_t r = ld32(A.mem_pos + cl_start + q);
-          for (int k = 0; k < nch; k++) acc.add(Rs.chunk(r, k), F4[k]);
+          for (int k = 0; k < nch; k++) acc.add(A.hr[r * nch + k], F4[k]);
           mp = A.mag_s[r];
           key = ld64(A.mkeys + cl_start + q);
         }
@@ -1035,7 +1085,8 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
         }
       last_q = (uint32_t)win;
       last = win < A.mrow ? mc.pos[win] : ld32(A.mem_pos + cl_start + win);
-      __syncthreads();  // s_bv / s_bp are reused by the next step
+      if (threadIdx.x == 0) s_new = 0;
+      __syncthreads();  // s_bv / s_bp / s_new are reused by the next step
       if (A.prof && threadIdx.x == 0) t_sub[3] += now() - tq;
     } else if (best_pos != NONE64) {
       // is_min with a result: the best candidate seeds the next cluster (bvec::erase)
@@ -1106,7 +1157,7 @@ uint32_t accum_grid(const mc_ctx *c) {
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess) cus = 256;
   uint32_t G = (uint32_t)cus / 8 * 8;
-  if (G > (uint32_t)NT + 1) G = NT;
+  if (G > GMAX) G = GMAX;
   if (G < 8) G = 8;
   return G;
 }
@@ -1127,7 +1178,7 @@ bool accum_plan(const mc_ctx *c, uint32_t nb, AccPlan *pl) {
   pl->fn = c->width == 1 ? (nch == 16 ? reinterpret_cast<const void *>(&accum_kernel<uint8_t, 16>)
                                       : reinterpret_cast<const void *>(&accum_kernel<uint8_t, 0>))
                          : reinterpret_cast<const void *>(&accum_kernel<uint16_t, 0>);
-  const size_t static_lds = 8 * 1024;  // both roles' __shared__ words, with margin
+  const size_t static_lds = 12 * 1024;  // both roles' __shared__ words, with margin
   const size_t cap = 160 * 1024 - static_lds;
   // worker: record words, alive flags, resident rows
   const size_t wfix = (size_t)(pl->rec_g + 3) / 4 * 16 + (pl->fcap + 15) / 16 * 16;
@@ -1179,24 +1230,25 @@ int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, 
     return MC_ERR_HIP;
   }
   const uint64_t fcap = pl.fcap;
-  // s_a: go word + step ring; s_b: partials + window table (+ global bitmap); s_c: flagged
-  // positions + kill log + flagged magnitudes + flagged rows; s_h: trace
+  // s_a: go word + step ring; s_b: partials (+ global bitmap); s_c: flagged positions + kill
+  // log; s_h: trace; s_i: member info (MInfo per static position); s_j: row-major static rows
   const size_t ring_bytes = 256 + (size_t)RING * pl.rec_g * 8;
   const size_t part_bytes = ((size_t)GW * PART_G * 8 + 255) / 256 * 256;
-  const size_t wtab_bytes = (c->norder * sizeof(WinTab) + 255) / 256 * 256;
   const size_t bits_bytes = pl.gbits ? ((c->norder + 31) / 32 * 4 + 255) / 256 * 256 : 0;
   const size_t fpos_bytes = ((size_t)GW * fcap * 4 + 255) / 256 * 256;
   const size_t klog_bytes = (c->norder * 4 + 16 + 255) / 256 * 256;
-  const size_t finfo_bytes = (size_t)GW * fcap * 24;
-  const size_t frow_bytes = (size_t)GW * fcap * nch * 16;
-  if (ensure(c->s_a, ring_bytes) || ensure(c->s_b, part_bytes + wtab_bytes + bits_bytes) ||
-      ensure(c->s_c, fpos_bytes + klog_bytes + finfo_bytes + frow_bytes))
+  if (ensure(c->s_a, ring_bytes) || ensure(c->s_b, part_bytes + bits_bytes) ||
+      ensure(c->s_c, fpos_bytes + klog_bytes))
     return MC_ERR_OOM;
-  WinTab *d_wtab = (WinTab *)((char *)c->s_b.p + part_bytes);
-  uint32_t *d_bits = pl.gbits ? (uint32_t *)((char *)c->s_b.p + part_bytes + wtab_bytes) : nullptr;
+  if (ensure(c->s_i, c->norder * sizeof(MInfo) + 64) || ensure(c->s_j, c->norder * (size_t)nch * 16 + 64))
+    return MC_ERR_OOM;
+  MInfo *d_minfo = (MInfo *)c->s_i.p;
+  uint4 *d_hr = (uint4 *)c->s_j.p;
+  uint32_t *d_bits = pl.gbits ? (uint32_t *)((char *)c->s_b.p + part_bytes) : nullptr;
   timed_begin(c);
   wintab_kernel<<<(int)std::min<uint64_t>((c->n + 255) / 256, 2048), 256, 0, c->stream>>>(
-      c->norder, (const uint64_t *)c->len_s.p, d_bin_lo, d_bounds, nb, sim, d_wtab);
+      c->norder, (const uint64_t *)c->len_s.p, (const uint64_t *)c->mag_s.p, (const uint64_t *)c->sumsq_s.p, d_bin_lo,
+      d_bounds, nb, sim, (const uint4 *)c->hs.p, c->npad, nch, d_minfo, d_hr);
   MCG_CHECK(hipGetLastError());
   if (d_bits) {
     bits_init_kernel<<<(int)std::min<uint64_t>(c->norder / 32 / 256 + 1, 1024), 256, 0, c->stream>>>(d_bits, c->norder);
@@ -1218,7 +1270,8 @@ int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, 
   A.nb = nb;
   A.bin_lo = d_bin_lo;
   A.bounds = d_bounds;
-  A.wtab = d_wtab;
+  A.minfo = d_minfo;
+  A.hr = d_hr;
   A.gbits = d_bits;
   A.go = (uint32_t *)c->s_a.p;
   A.ring = (uint64_t *)((char *)c->s_a.p + 256);
@@ -1227,8 +1280,6 @@ int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, 
   char *sc = (char *)c->s_c.p;
   A.fpos = (uint32_t *)sc;
   A.klog = (uint32_t *)(sc + fpos_bytes);
-  A.finfo = (uint64_t *)(sc + fpos_bytes + klog_bytes);
-  A.frow = (uint4 *)(sc + fpos_bytes + klog_bytes + finfo_bytes);
   A.fcap = fcap;
   A.res = pl.res;
   A.mrow = pl.mrow;

@@ -209,6 +209,55 @@ __device__ __forceinline__ int classify_raw(const DevClassifier &C, double (&raw
   return sum >= C.thr;
 }
 
+// Per-histogram terms of pearson / kulczynski2 (Feature.cpp:206-220, 273-294) that do not
+// depend on the pair: computed once per candidate (or per centre and step) instead of per pair.
+struct PTerms {
+  int64_t ap;  // (int)round(mag / B)
+  int64_t np;  // sum (p - ap)^2 = sumsq - 2 ap mag + B ap^2 (8/16-bit bins: exact)
+  double da;   // mag / B
+};
+__device__ __forceinline__ PTerms pterms(uint64_t mag, uint64_t sumsq, int B) {
+  const double da = (double)mag / B;
+  const int64_t a = (int)round(da), m = (int64_t)mag, b = B;
+  return PTerms{a, (int64_t)sumsq - 2 * a * m + b * a * a, da};
+}
+
+// classify_raw for the trainer's feature set (DevClassifier::layout 3 / 4), 8/16-bit bins:
+// the same IEEE operations in the same order (raw_fast, normalize_cache, operator(), the fma
+// GLM sum), with the pair-independent terms taken from PTerms -- a few divisions per pair
+// instead of the generic form's selects and loops.
+__device__ __forceinline__ int classify_std(const DevClassifier &C, const PS &s, const PInfo &p, const PTerms &tp,
+                                            const PInfo &q, const PTerms &tq, int B, double *c0) {
+  const mc_classifier &c = C.c;
+  double v[5];
+  v[0] = (double)(p.len > q.len ? p.len - q.len : q.len - p.len);             // LD
+  v[1] = (double)(s.smin * 2) / (double)(p.mag + q.mag);                        // INTERSECTION
+  v[2] = (double)(int32_t)(uint32_t)s.sabs;                                     // MANHATTAN
+  {                                                                             // PEARSON
+    const int64_t dot = (int64_t)s.sdot - tq.ap * (int64_t)p.mag - tp.ap * (int64_t)q.mag + (int64_t)B * tp.ap * tq.ap;
+    const double prod = (double)(int64_t)((uint64_t)tp.np * (uint64_t)tq.np);
+    v[3] = (double)dot / sqrt(0.5 < prod ? prod : 0.5);
+  }
+  const bool kul = C.layout == 4;
+  if (kul) v[4] = (((double)B * (tp.da + tq.da)) / ((2.0 * tp.da) * tq.da)) * (double)s.smin;  // KULCZYNSKI2
+#pragma unroll
+  for (int i = 0; i < 5; i++) {
+    if (i == 4 && !kul) break;
+    const double val = (v[i] - c.mins[i]) / (c.maxs[i] - c.mins[i]);
+    v[i] = c.is_sim[i] ? val : 1 - val;
+  }
+  const double a0 = v[0] * v[1];
+  const double a1 = (v[0] * v[0]) * (v[2] * v[2]);
+  const double a2 = v[3];
+  double sum = c.weights[0];
+  sum = __builtin_fma(c.weights[1], a0, sum);
+  sum = __builtin_fma(c.weights[2], a1, sum);
+  sum = __builtin_fma(c.weights[3], a2, sum);
+  if (kul) sum = __builtin_fma(c.weights[4], (v[0] * v[0]) * (v[4] * v[4]), sum);
+  *c0 = a0;
+  return sum >= C.thr;
+}
+
 template <typename T>
 __device__ __forceinline__ uint4 ld16(const uint8_t *row, int ch) {
   return reinterpret_cast<const uint4 *>(row)[ch];

@@ -28,6 +28,10 @@ struct DevClassifier {
   mc_classifier c;
   double thr;  // round(1/(1+exp(-sum))) == 1  <=>  sum >= thr   (host glibc exp, see abi.hip)
   int align;   // the only feature is MC_FEAT_ALIGN: raw[0] is an NW identity (Trainer.cpp:570-577)
+  // layout 3 / 4: the feature set Trainer::train builds (feat_set = 1, Trainer.cpp:583-588):
+  // lookup [LD, INT, MAN, PEARSON(, KUL)], combos [LD*INT, (LD*MAN)^2, PEARSON(, (LD*KUL)^2)]
+  // with 3 or 4 combos (features.hpp classify_std); 0 = any other (classify_raw)
+  int layout;
 };
 
 // Read-only view of the device histogram matrix passed to kernels by value.
@@ -109,7 +113,7 @@ struct mc_ctx {
   mcg::Buf ident_s, al_a, al_b, al_out;
   mcg::Buf acc_out;  // device-resident accumulation: counters / error word
   // scratch
-  mcg::Buf s_a, s_b, s_c, s_d, s_e, s_f, s_g, s_h;
+  mcg::Buf s_a, s_b, s_c, s_d, s_e, s_f, s_g, s_h, s_i, s_j;
   std::vector<void *> pinned;
   // timers: event pairs recorded around kernels, resolved lazily after the next stream sync
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
