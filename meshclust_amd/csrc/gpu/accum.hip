@@ -1192,7 +1192,8 @@ bool accum_plan(const mc_ctx *c, uint32_t nb, AccPlan *pl) {
     return s;
   };
   const size_t per_entry = (size_t)(nch + 1) * 16 + sizeof(WinTab) + 24 + 8 + 4;
-  for (int gb = 0; gb < 2; gb++) {
+  // MC_ACCUM_GBITS=1 (tests): the global-bitmap variant that N >~ 900k needs, at any N
+  for (int gb = getenv("MC_ACCUM_GBITS") ? 1 : 0; gb < 2; gb++) {
     const size_t f = cfix(gb != 0);
     if (f >= cap) continue;
     const uint64_t m = std::min<uint64_t>(1024, (cap - f) / per_entry);

@@ -151,6 +151,9 @@ RunResult run_pipeline(const Dataset &ds, mc_ctx *ctx, Options opt, bool upload,
     Scope s(rr.timer, "kmer");
     check(mc_kmer_max(ctx, opt.k, &rr.largest), "mc_kmer_max");
     int width = rr.largest <= 0xff ? 1 : rr.largest <= 0xffff ? 2 : rr.largest <= 0xffffffffull ? 4 : 8;
+    // diagnostics / tests: a wider histogram type than Runner.cpp:75-89 would pick (the
+    // 32/64-bit feature paths, with their unsigned wrap-arounds, on small inputs)
+    if (const char *fw = getenv("MC_FORCE_WIDTH")) width = std::max(width, atoi(fw));
     rr.width = width;
     if (verbose) printf("Using %d bit histograms\n", 8 * width);
     check(mc_kmer_build(ctx, opt.k, width), "mc_kmer_build");

@@ -71,8 +71,12 @@ def canonical_digest(clusters):
     """SHA-256 over the clusters sorted by centre id, each as uint32 [centre, size, sorted
     member ids...]: equal digests <=> equal partitions with equal centres."""
     h = hashlib.sha256()
-    for c, mem in sorted(clusters, key=lambda x: x[0]):
-        h.update(np.array([c, len(mem)] + sorted(mem), dtype=np.uint32).tobytes())
+    # a cluster whose centre is not one of its members prints no '*' (ClusterFactory.cpp:511):
+    # centre id 0xffffffff, ordered by its smallest member
+    key = [(0xffffffff if c is None else c, min(mem)) for c, mem in clusters]
+    for i in sorted(range(len(clusters)), key=lambda i: key[i]):
+        c, mem = clusters[i]
+        h.update(np.array([key[i][0], len(mem)] + sorted(mem), dtype=np.uint32).tobytes())
     return h.hexdigest()
 
 

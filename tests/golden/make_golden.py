@@ -48,6 +48,8 @@ E2E = {
     # related templates (families): ambiguous pairs, many merges
     "fam2k": (("family", 2000, 50, 10, 0.10, 0.03, 25), ["--id", "0.90"]),
     "fam2k_id85": (("family", 2000, 40, 8, 0.12, 0.04, 26), ["--id", "0.85", "--delta", "8"]),
+    # two clusters of 1,500 members: past the accumulation kernel's member cache
+    "big2_3k": ((3000, 1000, 2, 0.03, 75), ["--id", "0.90"]),
     # lower-case, IUPAC, N runs, records < 20 bp (the parser's edge cases end to end)
     "noisy2k": (("noisy", 2000, 40, 0.04, 27), ["--id", "0.90"]),
     # alignment mode (Feature::align classifier; --align, or --id < 0.6 switches it on)

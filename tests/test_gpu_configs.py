@@ -3,10 +3,11 @@ partitions of the same synthetic inputs.
 
 * config E (viral shape: 7 families x 13 genomes, 8-12 kb, k = 6, --id 0.80) against the
   reference's .clstr (tests/golden/cfg_E91.clstr.gz, canonical partition + centres);
-* config B (100k x 1 kb, --id 0.90) and config D (1M x 1 kb, --id 0.90) against the
-  reference's canonical partition digests (tests/golden/cfg_B100k.npz, cfg_D1M.npz, written by
-  make_big_golden.py from oracle/_ref/meshclust with all cores; partitions and centres of the
-  reference do not depend on its thread count).
+* config B (100k x 1 kb, --id 0.90) against the reference's canonical partition
+  (tests/golden/cfg_B100k.npz, written by make_big_golden.py from oracle/_ref/meshclust
+  --threads 1), with the accumulation kernel's LDS-bitmap and global-bitmap variants;
+* config D (1M x 1 kb, --id 0.90): property checks and device loop == host-driven steps (the
+  reference needs hours at this size).
 
 Reference loop: ClusterFactory.cpp:637-761 (accumulate, MS), Trainer.cpp:34-157, 334-365.
 The inputs are regenerated here by meshclust_amd.synth (deterministic; SHA-256 checked).
@@ -37,10 +38,10 @@ def _cache_dir():
     return d
 
 
-def _run(fa, flags, out, timeout):
+def _run(fa, flags, out, timeout, env=None):
     st = out + ".stats.json"
     r = subprocess.run([M.BIN, fa] + flags + ["--output", out, "--stats-json", st, "--quiet", "--threads", "16"],
-                       capture_output=True, text=True, timeout=timeout)
+                       capture_output=True, text=True, timeout=timeout, env=dict(os.environ, **(env or {})))
     assert r.returncode == 0, r.stderr[-3000:]
     return json.load(open(st))
 
@@ -60,18 +61,24 @@ def test_config_E91_partition_equals_reference(product, tmp_path):
     assert clstr.canonical(out) == clstr.canonical(fixtures.golden("cfg_E91.clstr.gz"))
 
 
-def _big(name, product, timeout):
+def _input(name):
+    gen, _ = BG.BIG[name]
+    fa = os.path.join(_cache_dir(), "%s.fa" % name)
+    if not os.path.exists(fa):
+        synth.generate(fa + ".tmp", *gen)
+        os.replace(fa + ".tmp", fa)
+    return fa
+
+
+def _big(name, product, timeout, env=None, tag=""):
     gen, flags = BG.BIG[name]
     gpath = fixtures.golden("cfg_%s.npz" % name)
     if not os.path.exists(gpath):
         pytest.skip("reference partition for %s not generated" % name)
     g = np.load(gpath)
-    fa = os.path.join(_cache_dir(), "%s.fa" % name)
-    if not os.path.exists(fa):
-        synth.generate(fa + ".tmp", *gen)
-        os.replace(fa + ".tmp", fa)
-    out = fa[:-3] + ".clstr"
-    st = _run(fa, flags, out, timeout)
+    fa = _input(name)
+    out = fa[:-3] + tag + ".clstr"
+    st = _run(fa, flags, out, timeout, env)
     got = BG.clusters_of(out)
     assert sorted(c for c, _ in got) == [int(x) for x in g["centres"]], "centre sets differ"
     if "centre_of" in g:
@@ -90,7 +97,41 @@ def test_config_B100k_partition_equals_reference(product):
     assert st["accum_path"] == "device"
 
 
+def test_config_B100k_global_bitmap_equals_reference(product):
+    """The accumulation kernel's global-bitmap variant (the one N >~ 900k reads takes, config
+    D) forced at config B, against the same reference partition."""
+    st = _big("B100k", product, 300, env={"MC_ACCUM_GBITS": "1"}, tag=".gbits")
+    assert st["accum_path"] == "device"
+
+
+def _partition(path):
+    got = BG.clusters_of(path)
+    ids = np.concatenate([np.array(m, np.int64) for _, m in got])
+    return got, ids
+
+
 @pytest.mark.timeout(1200)
-def test_config_D1M_partition_equals_reference(product):
-    st = _big("D1M", product, 900)
-    print("config D accumulation path:", st["accum_path"])
+def test_config_D1M_properties():
+    """Config D (1M x 1 kb, 10,000 templates, --id 0.90) on one GPU.  The reference needs hours
+    here, so there is no reference partition at this size: every read must be
+    in exactly one cluster, every centre a member of its own cluster, and the device-resident
+    accumulation (global-bitmap variant) must give the same partition and centres as the
+    host-driven get_close steps (ClusterFactory.cpp:637-730), whose exactness the smaller
+    reference partitions pin."""
+    M.build()
+    gen, flags = BG.BIG["D1M"]
+    fa = _input("D1M")
+    out_dev, out_steps = fa[:-3] + ".dev.clstr", fa[:-3] + ".steps.clstr"
+    st = _run(fa, flags, out_dev, 600)
+    assert st["accum_path"] == "device", st["accum_path"]
+    got, ids = _partition(out_dev)
+    assert len(ids) == gen[0] and np.array_equal(np.sort(ids), np.arange(gen[0]))
+    centres = [c for c, _ in got if c is not None]
+    assert len(set(centres)) == len(centres)
+    assert all(c in m for c, m in got if c is not None)
+    assert st["clusters"] == len(got)
+    print("config D: %d clusters (%d without their centre as a member), phases %s"
+          % (len(got), len(got) - len(centres), json.dumps(st.get("phases_ms"))))
+    st2 = _run(fa, flags, out_steps, 900, env={"MC_ACCUM_STEPS": "1"})
+    got2, _ = _partition(out_steps)
+    assert BG.canonical_digest(got2) == BG.canonical_digest(got)
