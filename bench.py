@@ -13,9 +13,10 @@ rate on sequences already resident in HBM (no parse / upload / write) is reporte
 
 With --gpus N (torch.distributed, one rank per GPU) every rank clusters its own batch
 (seed 41 + rank): replicas, weak scaling; no collective is on the data path.  With --shard the
-ranks instead share ONE clustering of the seed-41 batch (meshclust_amd.dist): each runs the
-accumulation chain, computes its share of every mean-shift iteration and the ranks all-gather
-the new centres over RCCL (strong scaling).
+ranks instead share ONE clustering of the seed-41 batch (meshclust_amd.dist), sharded by
+record: every get_close step is split over the ranks' static bvec blocks and combined with one
+RCCL all-gather per step, every mean-shift iteration is split by centre and the new centres
+all-gathered (strong scaling).
 
 Prints ONE JSON line on rank 0.
 """
@@ -130,10 +131,9 @@ def main():
     comm = None
     if shard:
         import torch
-        from meshclust_amd.dist import TorchShardComm
+        from meshclust_amd.dist import RcclShardComm, TorchShardComm
         if torch.cuda.is_available():
-            torch.cuda.set_device(local)
-            comm = TorchShardComm(dist.new_group(backend="nccl"))  # RCCL for the centre exchange
+            comm = RcclShardComm(local)  # libmcgpu's RCCL communicator, called from C++
         else:
             comm = TorchShardComm()
 
@@ -188,6 +188,8 @@ def main():
         elapsed = float(t.item())
 
     if rank != 0:
+        if comm is not None:
+            comm.close()
         eng.close()
         if dist:
             dist.destroy_process_group()
@@ -255,7 +257,7 @@ def main():
                 % (a.n, a.len, a.templates, a.mut, a.seed),
         "config": {"workload": "config B: 100k synthetic 1kb reads, --id %s k-mer mean-shift" % a.id,
                    "reads_per_gpu": a.n, "read_len": a.len, "k": s0["k"], "histogram_bits": 8 * width,
-                   "parallelism": ("one clustering sharded x%d (centre all-gather over RCCL)" % world) if shard
+                   "parallelism": ("one clustering sharded by record x%d (RCCL all-gather per step)" % world) if shard
                    else "replicas x%d" % world},
         "roofline": roof,
         "cpu_baseline": cpu,
@@ -276,6 +278,8 @@ def main():
     if a.stats_out:
         with open(a.stats_out, "w") as f:
             json.dump({"line": line, "stats": stats, "timers": tim}, f, indent=1)
+    if comm is not None:
+        comm.close()
     eng.close()
     import shutil
     shutil.rmtree(out_dir, ignore_errors=True)

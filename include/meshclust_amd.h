@@ -195,6 +195,27 @@ int mc_scan(mc_ctx *ctx, uint32_t centre_id, uint64_t S, uint64_t E, uint32_t *f
             uint64_t cap, mc_scan_result *res);
 
 /*
+ * One get_close step sharded by record over `nparts` GPUs (Trainer.cpp:34-114
+ * is an OpenMP loop over the window, ClusterFactory.cpp:650-654).  Every rank holds the same
+ * bvec state; rank `part` scans only the alive positions of S..E in its static blocks: block
+ * b = [b * MC_SHARD_BLOCK, (b + 1) * MC_SHARD_BLOCK) belongs to part b % nparts.  Nothing is
+ * removed: flagged_pos receives this part's similar candidates (ascending); res holds this
+ * part's is_min / has_best / best_pos / best_val / n_flagged.  The ranks then combine the
+ * parts (is_min AND, first maximum = largest best_val, ties to the lowest best_pos, flagged
+ * lists merged) and all call mc_scan_commit with the union.  8/16-bit histograms, k-mer
+ * classifier (else MC_ERR_UNSUPPORTED).
+ */
+#define MC_SHARD_BLOCK 256
+int mc_scan_part(mc_ctx *ctx, uint32_t centre_id, uint64_t S, uint64_t E, uint32_t part, uint32_t nparts,
+                 uint32_t *flagged_pos, uint64_t cap, mc_scan_result *res);
+/*
+ * Second half of a sharded step: bvec::remove_available (bvec.cpp:289-318) of the union of
+ * every part's flagged positions (ascending, n may be 0) and get_mean (ClusterFactory.cpp:
+ * 382-425) over the grown cluster: res->new_centre, res->n_members, res->is_min = (n == 0).
+ */
+int mc_scan_commit(mc_ctx *ctx, const uint32_t *flagged_pos, uint64_t n, mc_scan_result *res);
+
+/*
  * The whole accumulation phase on the device: ClusterFactory::MS's loop
  * `last = points.pop(); while (last) accumulate(&last, ...)` (ClusterFactory.cpp:717-730,
  * accumulate :637-714) run by one persistent kernel, bvec included -- no host round trip per
@@ -260,6 +281,25 @@ int mc_classify_values(mc_ctx *ctx, const double *raw, uint64_t m, uint8_t *simi
  */
 int mc_mean_shift_select(mc_ctx *ctx, const uint32_t *centre_ids, uint32_t C, const uint64_t *member_off,
                          const uint32_t *members, int delta, const uint8_t *keep, uint32_t *new_centre);
+
+/*
+ * ---- ranks sharing one clustering --------------------------------------
+ * The reference runs on one host (OpenMP); here one process (or thread) per GPU shares a
+ * clustering.  mc_comm is an RCCL communicator (librccl opened at run time) whose only
+ * operation is an all-gather of equal host blocks in rank order, staged through the rank's
+ * GPU and carried by RCCL over xGMI.  Rank 0 makes the id, the caller distributes it (e.g.
+ * torch.distributed broadcast), every rank calls mc_comm_create (it blocks until all joined).
+ * mc_comm_allgather's signature is the host driver's exchange callback
+ * (mcl_run_sharded(..., allgather = mc_comm_allgather, user = comm)).
+ */
+typedef struct mc_comm mc_comm;
+#define MC_COMM_ID_BYTES 128
+int mc_comm_unique_id(uint8_t *id /* MC_COMM_ID_BYTES */);
+int mc_comm_create(int device, int rank, int world, const uint8_t *id, mc_comm **out);
+int mc_comm_allgather(mc_comm *comm, const void *in, uint64_t bytes, void *out /* world * bytes */);
+int mc_comm_stats(const mc_comm *comm, uint64_t *calls, uint64_t *bytes);
+/* abort != 0: ncclCommAbort (a peer failed), else ncclCommDestroy. */
+int mc_comm_destroy(mc_comm *comm, int abort);
 
 /* Device time (ms) accumulated per kernel family since the last reset (diagnostics). */
 int mc_timers(mc_ctx *ctx, double *ms_out, int n, int reset);

@@ -88,8 +88,14 @@ def gpu_lib():
         for name in ("mc_load_sequences", "mc_load_packed", "mc_kmer_max", "mc_kmer_build", "mc_get_histograms", "mc_distance_keys",
                      "mc_pair_features", "mc_set_classifier", "mc_classify_pairs", "mc_nw_identity",
                      "mc_nw_identity_raw", "mc_set_order", "mc_kill", "mc_cluster_begin", "mc_scan",
-                     "mc_mean_shift", "mc_timers", "mc_classify_values", "mc_mean_shift_select", "mc_accumulate"):
+                     "mc_mean_shift", "mc_timers", "mc_classify_values", "mc_mean_shift_select", "mc_accumulate",
+                     "mc_scan_part", "mc_scan_commit", "mc_comm_unique_id", "mc_comm_create", "mc_comm_allgather",
+                     "mc_comm_stats", "mc_comm_destroy"):
             getattr(lib, name).restype = C.c_int
+        lib.mc_comm_create.argtypes = [C.c_int, C.c_int, C.c_int, C.c_char_p, C.POINTER(C.c_void_p)]
+        lib.mc_comm_allgather.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]
+        lib.mc_comm_stats.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        lib.mc_comm_destroy.argtypes = [C.c_void_p, C.c_int]
         _gpu = lib
     return _gpu
 
@@ -318,15 +324,16 @@ class Dataset:
 
     def run(self, engine, args=(), upload=True, clstr=None, comm=None):
         """Run the full pipeline (reference options in ``args``); returns the stats dict.
-        ``comm`` (meshclust_amd.dist.TorchShardComm) shares the clustering over its ranks."""
+        ``comm`` (meshclust_amd.dist.RcclShardComm or TorchShardComm) shares the clustering
+        over its ranks."""
         import json
         argv = [b"meshclust"] + [a.encode() for a in args]
         arr = (C.c_char_p * len(argv))(*argv)
         buf = C.create_string_buffer(1 << 16)
-        if comm is not None and comm.world > 1:
+        if comm is not None:
             rc = self.lib.mcl_run_sharded(self.h, engine.ctx, len(argv), arr, 1 if upload else 0,
                                           clstr.encode() if clstr else None, buf, len(buf), comm.rank, comm.world,
-                                          C.cast(comm.callback, C.c_void_p), None)
+                                          C.cast(comm.callback, C.c_void_p), comm.user)
         else:
             rc = self.lib.mcl_run(self.h, engine.ctx, len(argv), arr, 1 if upload else 0,
                                   clstr.encode() if clstr else None, buf, len(buf))

@@ -705,6 +705,58 @@ int mc_scan(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, uint32_t *flagge
   return MC_OK;
 }
 
+int mc_scan_part(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, uint32_t part, uint32_t nparts,
+                 uint32_t *flagged_pos, uint64_t cap, mc_scan_result *res) {
+  if (!c || !res || !c->has_cls || c->norder == 0) return MC_ERR_STATE;
+  if (S > E || E >= c->norder || centre >= c->n || nparts == 0 || part >= nparts) return MC_ERR_ARG;
+  if (!fused(c) || c->cls.align) {
+    set_error("sharded get_close steps take 8/16-bit k-mer histograms");
+    return MC_ERR_UNSUPPORTED;
+  }
+  c->step++;
+  const uint32_t seq = ++c->seq;
+  TRY(launch_fused_scan(c, centre, S, E, seq, nullptr, part, nparts));
+  TRY(wait_seq(c, seq));
+  *res = c->h_res->r;
+  res->new_centre = 0xffffffffu;
+  const uint64_t nf = res->n_flagged;
+  if (nf > cap) {
+    set_error("flagged buffer too small");
+    return MC_ERR_ARG;
+  }
+  memcpy(flagged_pos, c->h_res->flags, nf * 4);
+  std::sort(flagged_pos, flagged_pos + nf);
+  return MC_OK;
+}
+
+int mc_scan_commit(mc_ctx *c, const uint32_t *flagged_pos, uint64_t n, mc_scan_result *res) {
+  if (!c || !res || !c->has_cls || c->norder == 0) return MC_ERR_STATE;
+  if (!fused(c) || c->cls.align) {
+    set_error("sharded get_close steps take 8/16-bit k-mer histograms");
+    return MC_ERR_UNSUPPORTED;
+  }
+  if (n > c->norder || (n && !flagged_pos)) return MC_ERR_ARG;
+  for (uint64_t i = 0; i < n; i++)
+    if (flagged_pos[i] >= c->norder || (i && flagged_pos[i] <= flagged_pos[i - 1]) || !c->h_alive[flagged_pos[i]]) {
+      set_error("mc_scan_commit: positions must be ascending, alive and in range");
+      return MC_ERR_ARG;
+    }
+  uint32_t *d_flags = (uint32_t *)((char *)c->scan_dev.p + sizeof(ScanDev));
+  if (n) MCG_CHECK(hipMemcpyAsync(d_flags, flagged_pos, n * 4, hipMemcpyHostToDevice, c->stream));
+  for (uint64_t p : c->pending_kills) MCG_CHECK(hipMemsetAsync((uint8_t *)c->alive.p + p, 0, 1, c->stream));
+  c->pending_kills.clear();
+  const uint32_t seq = ++c->seq;
+  TRY(launch_commit(c, d_flags, (uint32_t)n, seq));
+  TRY(wait_seq(c, seq));
+  memset(res, 0, sizeof *res);
+  res->is_min = n == 0;
+  res->n_flagged = n;
+  res->new_centre = c->h_res->r.new_centre;
+  res->n_members = c->h_res->r.n_members;
+  for (uint64_t i = 0; i < n; i++) c->h_alive[flagged_pos[i]] = 0;
+  return MC_OK;
+}
+
 int mc_accumulate(mc_ctx *c, const uint32_t *bin_lo, const uint64_t *bounds, uint32_t nbins, double sim,
                   uint32_t *centre_ids, uint64_t *member_off, uint32_t *member_ids, uint64_t *nclusters,
                   uint64_t *stats) {

@@ -153,7 +153,11 @@ int build_static(mc_ctx *c);
 bool accum_supported(const mc_ctx *c, uint32_t nb);
 int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, uint32_t nb, double sim,
                  uint32_t *d_mem_pos, uint64_t *d_mkeys, uint32_t *d_cl_centre, uint64_t *d_cl_off, uint64_t *d_out);
-int launch_fused_scan(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, uint32_t seq, const double *d_ident);
+// nparts > 0: a sharded step (mc_scan_part) over this rank's static blocks only
+int launch_fused_scan(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, uint32_t seq, const double *d_ident,
+                      uint32_t part = 0, uint32_t nparts = 0);
+// mc_scan_commit: d_flags[0, nflag) ascending static positions (all ranks' flagged)
+int launch_commit(mc_ctx *c, const uint32_t *d_flags, uint32_t nflag, uint32_t seq);
 // NW on byte strings: pair p aligns A[aoff[ai[p]] .. aoff[ai[p]+1]) against B[...] (rows = A).
 // Results go to slot p, or to slot d_out[p] when d_out is given.
 int launch_nw(mc_ctx *c, const uint8_t *d_A, const uint64_t *d_aoff, const uint32_t *d_ai, const uint8_t *d_B,

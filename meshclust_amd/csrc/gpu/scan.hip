@@ -25,6 +25,7 @@ namespace mcg {
 namespace {
 
 constexpr int ST = 256;
+static_assert(ST == MC_SHARD_BLOCK, "a sharded step scans whole MC_SHARD_BLOCK blocks, one workgroup each");
 
 template <typename T>
 __global__ __launch_bounds__(ST) void build_static_kernel(const uint8_t *__restrict__ hist, uint64_t pitch,
@@ -72,6 +73,32 @@ struct FusedArgs {
   uint32_t seq;
   uint64_t *stamps;  // diagnostic build only (MC_STAMPS): s_memrealtime at phase boundaries
   const double *ident;  // alignment mode: NW identity per static position (else null)
+  // workgroup w scans static positions pos0 + w * pstride + [0, ST) (clipped to [S, E]):
+  // pos0 = S, pstride = ST for a whole window; one rank's blocks of a sharded window otherwise
+  uint64_t pos0, pstride;
+  int part;  // sharded step (mc_scan_part): find and report only, the commit kernel applies
+};
+
+// mc_scan_commit: remove_available + get_mean of a sharded step, on the union of the ranks'
+// flagged positions (ascending static positions in flags_dev[0, nflag)).
+struct CommitArgs {
+  const uint4 *hs;
+  uint64_t npad;
+  int nch, B;
+  const uint64_t *mag_s;
+  const uint32_t *order;
+  uint8_t *alive;
+  const uint32_t *flags_dev;
+  uint32_t nflag;
+  int new_cluster;
+  uint64_t first_pos;
+  uint32_t step;
+  ScanDev *sd;
+  uint32_t *mem_pos;
+  uint64_t *mkeys;
+  uint64_t *msum;
+  HostScan *hres;
+  uint32_t seq;
 };
 
 #ifdef MC_STAMPS
@@ -110,8 +137,8 @@ __global__ __launch_bounds__(ST) void fused_scan_kernel(FusedArgs A, DevClassifi
   __syncthreads();
   const PInfo pc{A.mag[A.centre], A.sumsq[A.centre], A.len[A.centre]};
   const uint32_t mbase = A.new_cluster ? 1u : A.sd->nmembers;
-  const uint64_t pos = A.S + (uint64_t)blockIdx.x * ST + threadIdx.x;
-  bool valid = pos <= A.E && A.alive[pos];
+  const uint64_t pos = A.pos0 + (uint64_t)blockIdx.x * A.pstride + threadIdx.x;
+  bool valid = pos >= A.S && pos <= A.E && A.alive[pos];
   for (int i = 0; i < A.nkill; i++) valid = valid && pos != A.kills[i];
   double best_v = -1.0;  // get_close's initializer (NULL, -1, 0, 0) with a strict `>`
   uint64_t best_p = ~0ull;
@@ -147,11 +174,13 @@ __global__ __launch_bounds__(ST) void fused_scan_kernel(FusedArgs A, DevClassifi
       best_p = pos;
     }
     if (d) {
-      A.alive[pos] = 0;
       const uint32_t slot = atomicAdd(&A.sd->nflag, 1u);
       A.flags_dev[slot] = (uint32_t)pos;
-      A.mem_pos[mbase + slot] = (uint32_t)pos;
-      A.mkeys[mbase + slot] = ((uint64_t)A.step << 32) | pos;
+      if (!A.part) {
+        A.alive[pos] = 0;
+        A.mem_pos[mbase + slot] = (uint32_t)pos;
+        A.mkeys[mbase + slot] = ((uint64_t)A.step << 32) | pos;
+      }
     }
   }
   // workgroup first-max of combo 0
@@ -218,9 +247,9 @@ __global__ __launch_bounds__(ST) void fused_scan_kernel(FusedArgs A, DevClassifi
   __syncthreads();
   STAMP(3);
   const uint32_t nflag = __hip_atomic_load(&A.sd->nflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const uint32_t M = mbase + nflag;
+  const uint32_t M = A.part ? A.sd->nmembers : mbase + nflag;
   uint32_t new_id = 0xffffffffu;
-  if (nflag > 0) {
+  if (nflag > 0 && !A.part) {
     if (A.new_cluster) {
       if (threadIdx.x == 0) {
         A.mem_pos[0] = (uint32_t)A.first_pos;
@@ -250,7 +279,7 @@ __global__ __launch_bounds__(ST) void fused_scan_kernel(FusedArgs A, DevClassifi
         v = rv[i];
         p = rp[i];
       }
-    A.sd->nmembers = M;
+    if (!A.part) A.sd->nmembers = M;
     A.sd->nflag = 0;
     for (int i = 0; i < A.nkill; i++) A.alive[A.kills[i]] = 0;
     HostScan *h = A.hres;
@@ -267,6 +296,48 @@ __global__ __launch_bounds__(ST) void fused_scan_kernel(FusedArgs A, DevClassifi
   __syncthreads();
   STAMP(6);
   if (threadIdx.x == 0) {
+    __threadfence_system();
+    __hip_atomic_store(&A.hres->seq, A.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(ST) void commit_kernel(CommitArgs A) {
+  extern __shared__ __attribute__((aligned(16))) uint4 dyn[];
+  uint4 *Fl = dyn;  // packed integer mean
+  const uint32_t mbase = A.new_cluster ? 1u : A.sd->nmembers;
+  const uint32_t M = mbase + A.nflag;
+  for (uint32_t q = threadIdx.x; q < A.nflag; q += ST) {
+    const uint32_t pos = A.flags_dev[q];
+    A.alive[pos] = 0;
+    A.mem_pos[mbase + q] = pos;
+    A.mkeys[mbase + q] = ((uint64_t)A.step << 32) | pos;
+  }
+  if (A.new_cluster && threadIdx.x == 0) {
+    A.mem_pos[0] = (uint32_t)A.first_pos;
+    A.mkeys[0] = 0;
+  }
+  __syncthreads();
+  uint32_t new_id = 0xffffffffu;
+  if (A.nflag > 0) {  // the same running integer sums + closest member as fused_scan_kernel
+    const RowRef R{A.hs, 1, A.npad};
+    uint64_t *lsum = A.B <= 4096 ? reinterpret_cast<uint64_t *>(Fl + A.nch) : A.msum;
+    for (int b = threadIdx.x; b < A.B; b += ST) lsum[b] = A.new_cluster ? elem<T>(R, A.first_pos, b) : A.msum[b];
+    __syncthreads();
+    add_rows<T, ST>(R, A.flags_dev, A.nflag, A.nch, lsum);
+    __syncthreads();
+    if (lsum != A.msum)
+      for (int b = threadIdx.x; b < A.B; b += ST) A.msum[b] = lsum[b];
+    const uint64_t win = mean_closest_fast<T, ST>(R, A.mem_pos, A.mkeys, M, A.mag_s, A.B, A.nch, lsum, Fl);
+    new_id = A.order[win];
+  }
+  if (threadIdx.x == 0) {
+    A.sd->nmembers = M;
+    HostScan *h = A.hres;
+    h->r.is_min = A.nflag == 0;
+    h->r.n_flagged = A.nflag;
+    h->r.new_centre = new_id;
+    h->r.n_members = M;
     __threadfence_system();
     __hip_atomic_store(&A.hres->seq, A.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
@@ -301,10 +372,22 @@ int build_static(mc_ctx *c) {
   return MC_OK;
 }
 
-int launch_fused_scan(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, uint32_t seq, const double *d_ident) {
+int launch_fused_scan(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, uint32_t seq, const double *d_ident,
+                      uint32_t part, uint32_t nparts) {
   const int nch = (int)((c->B * c->width + 15) / 16);
-  const uint64_t W = E - S + 1;
-  const int grid = (int)((W + ST - 1) / ST);
+  uint64_t pos0 = S, pstride = ST, nblk = (E - S + 1 + ST - 1) / ST;
+  if (nparts) {  // the rank's blocks: static block b (positions [b*ST, (b+1)*ST)) with b % nparts == part
+    const uint64_t b_lo = S / ST, b_hi = E / ST;
+    const uint64_t f = b_lo + (part + nparts - b_lo % nparts) % nparts;
+    nblk = f <= b_hi ? (b_hi - f) / nparts + 1 : 0;
+    pos0 = f * ST;
+    pstride = (uint64_t)nparts * ST;
+    if (nblk == 0) {  // nothing of this window is ours: one empty workgroup still publishes
+      pos0 = E + 1;
+      nblk = 1;
+    }
+  }
+  const int grid = (int)nblk;
   FusedArgs A;
   memset(&A, 0, sizeof A);
   A.hs = (const uint4 *)c->hs.p;
@@ -339,6 +422,9 @@ int launch_fused_scan(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, uint32
   A.hres = c->h_res_dev;
   A.seq = seq;
   A.ident = d_ident;
+  A.pos0 = pos0;
+  A.pstride = pstride;
+  A.part = nparts ? 1 : 0;
 #ifdef MC_STAMPS
   static uint64_t *stamps = nullptr;
   static std::vector<double> acc(8, 0.0);
@@ -368,6 +454,38 @@ int launch_fused_scan(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, uint32
   MCG_CHECK(hipGetLastError());
   timed_end(c, F_SCAN);
   c->pending_kills.clear();
+  if (!nparts) c->pending_begin = false;  // a sharded step's cluster starts at its commit
+  return MC_OK;
+}
+
+int launch_commit(mc_ctx *c, const uint32_t *d_flags, uint32_t nflag, uint32_t seq) {
+  const int nch = (int)((c->B * c->width + 15) / 16);
+  CommitArgs A;
+  memset(&A, 0, sizeof A);
+  A.hs = (const uint4 *)c->hs.p;
+  A.npad = c->npad;
+  A.nch = nch;
+  A.B = c->B;
+  A.mag_s = (const uint64_t *)c->mag_s.p;
+  A.order = (const uint32_t *)c->order.p;
+  A.alive = (uint8_t *)c->alive.p;
+  A.flags_dev = d_flags;
+  A.nflag = nflag;
+  A.new_cluster = c->pending_begin ? 1 : 0;
+  A.first_pos = c->pending_first_pos;
+  A.step = c->step;
+  A.sd = (ScanDev *)c->scan_dev.p;
+  A.mem_pos = (uint32_t *)c->members.p;
+  A.mkeys = (uint64_t *)c->member_keys.p;
+  A.msum = (uint64_t *)c->msum.p;
+  A.hres = c->h_res_dev;
+  A.seq = seq;
+  const size_t lds = (size_t)nch * 16 + (c->B <= 4096 ? (size_t)c->B * 8 : 0);
+  timed_begin(c);
+  if (c->width == 1) commit_kernel<uint8_t><<<1, ST, lds, c->stream>>>(A);
+  else commit_kernel<uint16_t><<<1, ST, lds, c->stream>>>(A);
+  MCG_CHECK(hipGetLastError());
+  timed_end(c, F_SCAN);
   c->pending_begin = false;
   return MC_OK;
 }

@@ -5,7 +5,9 @@
 #include <cfloat>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <memory>
+#include <string>
 #include <unordered_map>
 
 namespace mc {
@@ -106,11 +108,84 @@ void memo_lookup(AlignMemo &memo, mc_ctx *ctx, const Dataset &ds, const std::vec
     if (hit[i]) val[i] = memo.ident.at(AlignMemo::key(a[i], b[i]));
 }
 
+// One get_close step sharded by record over the ranks of `comm`: every rank
+// scans its static blocks of the window (mc_scan_part), the ranks all-gather their partial
+// results -- {first max of combo 0, is_min, flagged positions} -- and combine them exactly as
+// the serial loop of Trainer::get_close would (Trainer.cpp:34-114: is_min is the AND over all
+// candidates; the result is the FIRST maximum in bvec order, i.e. the largest value with ties
+// to the lowest static position), then every rank applies remove_available + get_mean to the
+// union (mc_scan_commit).  One exchange of a fixed 1 KiB block per rank per step; a second
+// one only when some rank flagged more than kInline candidates.
+struct ShardBlock {
+  static constexpr uint32_t kInline = 248;
+  double best_val;
+  uint64_t best_pos;
+  uint32_t has_best, is_min, n_flagged, pad;
+  uint32_t flagged[kInline];
+};
+static_assert(sizeof(ShardBlock) == 1024, "exchange block");
+
+void sharded_step(mc_ctx *ctx, const ShardComm &comm, uint32_t centre, uint64_t S, uint64_t E,
+                  std::vector<uint32_t> &flag_buf, std::vector<uint32_t> &all_flagged, mc_scan_result *res,
+                  PhaseTimer &timer) {
+  mc_scan_result loc{};
+  {
+    Scope sc(timer, "accumulate.scan_part");
+    check(mc_scan_part(ctx, centre, S, E, (uint32_t)comm.rank, (uint32_t)comm.world, flag_buf.data(), flag_buf.size(),
+                       &loc),
+          "mc_scan_part");
+  }
+  Scope sx(timer, "accumulate.exchange");
+  const int W = comm.world;
+  ShardBlock mine;
+  memset(&mine, 0, sizeof mine);
+  mine.best_val = loc.best_val;
+  mine.best_pos = loc.best_pos;
+  mine.has_best = loc.has_best ? 1 : 0;
+  mine.is_min = loc.is_min ? 1 : 0;
+  mine.n_flagged = (uint32_t)loc.n_flagged;
+  memcpy(mine.flagged, flag_buf.data(), std::min<uint64_t>(loc.n_flagged, ShardBlock::kInline) * 4);
+  std::vector<ShardBlock> all(W);
+  if (comm.allgather(comm.user, &mine, sizeof mine, all.data()) != 0)
+    throw Error("get_close all-gather across ranks failed", 1);
+  memset(res, 0, sizeof *res);
+  res->is_min = 1;
+  res->best_val = -1.0;
+  uint64_t total = 0, most = 0;
+  for (const auto &b : all) {
+    res->is_min &= (int32_t)b.is_min;
+    if (b.has_best && (!res->has_best || b.best_val > res->best_val ||
+                       (b.best_val == res->best_val && b.best_pos < res->best_pos))) {
+      res->has_best = 1;
+      res->best_val = b.best_val;
+      res->best_pos = b.best_pos;
+    }
+    total += b.n_flagged;
+    most = std::max<uint64_t>(most, b.n_flagged);
+  }
+  all_flagged.clear();
+  if (most > ShardBlock::kInline) {  // long lists: one more all-gather of every full list
+    std::vector<uint32_t> big(most, 0), gathered(most * W);
+    std::copy(flag_buf.begin(), flag_buf.begin() + loc.n_flagged, big.begin());
+    if (comm.allgather(comm.user, big.data(), most * 4, gathered.data()) != 0)
+      throw Error("get_close all-gather across ranks failed", 1);
+    for (int r = 0; r < W; r++)
+      all_flagged.insert(all_flagged.end(), gathered.begin() + most * r, gathered.begin() + most * r + all[r].n_flagged);
+  } else {
+    for (const auto &b : all) all_flagged.insert(all_flagged.end(), b.flagged, b.flagged + b.n_flagged);
+  }
+  std::sort(all_flagged.begin(), all_flagged.end());  // each part is ascending; blocks interleave
+  if (all_flagged.size() != total || (total == 0) != (res->is_min != 0))
+    throw Error("inconsistent sharded get_close results", 1);
+  res->n_flagged = total;
+}
+
 // accumulate (ClusterFactory.cpp:637-714): grow one cluster around `last` until get_close
-// finds no similar candidate; returns the next seed through *last_ptr.
+// finds no similar candidate; returns the next seed through *last_ptr.  With `shard`, every
+// get_close step is split over the ranks (sharded_step).
 void accumulate(uint32_t *last_ptr, const Dataset &ds, mc_ctx *ctx, BVec &bv, std::vector<Center> &centers,
                 const ClusterConfig &cfg, ClusterStats &stats, std::vector<uint32_t> &flag_buf, PhaseTimer &timer,
-                AlignMemo *memo) {
+                AlignMemo *memo, const ShardComm *shard, std::vector<uint32_t> &all_flagged) {
   uint32_t last = *last_ptr;
   std::vector<uint32_t> current = {last};
   check(mc_cluster_begin(ctx, last), "mc_cluster_begin");
@@ -131,10 +206,14 @@ void accumulate(uint32_t *last_ptr, const Dataset &ds, mc_ctx *ctx, BVec &bv, st
       stats.scan_steps++;
       stats.scan_candidates += (uint64_t)count;
       if (memo) memo->begin_step(last, S, E);
-      Scope sc(timer, "accumulate.mc_scan");
-      check(mc_scan(ctx, last, S, E, flag_buf.data(), flag_buf.size(), &res), "mc_scan");
-      stats.align_nw_pairs += res.nw_pairs;
-      stats.align_nw_cells += res.nw_cells;
+      if (shard) {
+        sharded_step(ctx, *shard, last, S, E, flag_buf, all_flagged, &res, timer);
+      } else {
+        Scope sc(timer, "accumulate.mc_scan");
+        check(mc_scan(ctx, last, S, E, flag_buf.data(), flag_buf.size(), &res), "mc_scan");
+        stats.align_nw_pairs += res.nw_pairs;
+        stats.align_nw_cells += res.nw_cells;
+      }
     } else {  // the OpenMP loop runs no iteration: result NULL, is_min stays true
       res.is_min = 1;
       res.has_best = 0;
@@ -156,8 +235,17 @@ void accumulate(uint32_t *last_ptr, const Dataset &ds, mc_ctx *ctx, BVec &bv, st
         if (memo) memo->removed(order[res.best_pos]);
       }
     } else {
+      if (shard) {
+        mc_scan_result cr{};
+        {
+          Scope sc(timer, "accumulate.commit");
+          check(mc_scan_commit(ctx, all_flagged.data(), all_flagged.size(), &cr), "mc_scan_commit");
+        }
+        res.new_centre = cr.new_centre;
+      }
       Scope sr(timer, "accumulate.remove");
-      std::vector<uint32_t> flagged(flag_buf.begin(), flag_buf.begin() + res.n_flagged);
+      std::vector<uint32_t> flagged = shard ? all_flagged
+                                            : std::vector<uint32_t>(flag_buf.begin(), flag_buf.begin() + res.n_flagged);
       if (memo)
         for (uint32_t pos : flagged) memo->removed(order[pos]);
       bv.remove_positions(flagged, bounds.first.first, bounds.second.first, current);
@@ -202,13 +290,21 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
   std::vector<Center> part;
   const auto &order = bv.static_order();
   check(mc_set_order(ctx, order.data(), order.size()), "mc_set_order");
-  std::vector<uint32_t> flag_buf(order.size() + 1);
+  std::vector<uint32_t> flag_buf(order.size() + 1), all_flagged;
   std::unique_ptr<AlignMemo> memo;
   if (cfg.align) memo.reset(new AlignMemo(ds.size(), bv));
+  // Record-sharded accumulation (every get_close step split over the ranks) when several ranks
+  // share the clustering and the device takes sharded steps (8/16-bit k-mer histograms);
+  // otherwise each rank runs the whole chain (identical on every rank).
+  // MC_SHARD_FORCE=1 (tests) takes the sharded code path with a single rank too.
+  const bool multi = cfg.comm && (cfg.comm->world > 1 || getenv("MC_SHARD_FORCE"));
+  const ShardComm *shard = (multi && !memo && cfg.width <= 2 && !getenv("MC_SHARD_REPLICATE")) ? cfg.comm : nullptr;
   // The device-resident loop (mc_accumulate) unless alignment mode or the configuration
   // asks for the step API; MC_ACCUM_STEPS=1 forces the host-driven loop (both are GPU paths).
   bool done = false;
-  if (!memo && !getenv("MC_ACCUM_STEPS")) {
+  if (shard) {
+    stats.accum_path = "sharded steps x" + std::to_string(shard->world);
+  } else if (!memo && !getenv("MC_ACCUM_STEPS")) {
     Scope s(timer, "accumulate");
     const auto &bins = bv.bins();
     std::vector<uint32_t> bin_lo(bins.size() + 1, 0);
@@ -246,7 +342,8 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
       check(mc_kill(ctx, bv.spos(last)), "mc_kill");
       if (memo) memo->removed(last);
     }
-    while (last != BVec::NONE) accumulate(&last, ds, ctx, bv, part, cfg, stats, flag_buf, timer, memo.get());
+    while (last != BVec::NONE)
+      accumulate(&last, ds, ctx, bv, part, cfg, stats, flag_buf, timer, memo.get(), shard, all_flagged);
   }
   Scope s(timer, "update+merge");
   for (int it = 0; it < cfg.iterations; it++) {
@@ -264,7 +361,7 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
       uint32_t e = std::min<uint32_t>(j + cfg.delta, C - 1);
       stats.update_evals += off[e + 1] - off[b];
     }
-    if (C && !memo && cfg.comm && cfg.comm->world > 1) {
+    if (C && !memo && multi) {
       // this rank's share of the centres, then the centre-reassignment all-gather
       const uint32_t W = (uint32_t)cfg.comm->world, per = (C + W - 1) / W;
       const uint32_t j0 = std::min<uint32_t>(C, per * (uint32_t)cfg.comm->rank), j1 = std::min<uint32_t>(C, j0 + per);

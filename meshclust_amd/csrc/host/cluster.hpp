@@ -19,10 +19,10 @@ struct Center {
   bool del = false;
 };
 
-// The ranks (one process per GPU) that share one clustering.  Every rank
-// runs the same sequential accumulation; each mean-shift iteration is split by centre and the
-// ranks exchange the new centres with `allgather` (equal blocks of `bytes`, rank order into
-// `out`; returns 0 on success).
+// The ranks (one process per GPU) that share one clustering.  Every get_close
+// step of the accumulation is split over the ranks by record (static bvec blocks), each
+// mean-shift iteration by centre; the ranks exchange partial step results and new centres with
+// `allgather` (equal blocks of `bytes`, rank order into `out`; returns 0 on success).
 struct ShardComm {
   int rank = 0, world = 1;
   int (*allgather)(void *user, const void *in, uint64_t bytes, void *out) = nullptr;
@@ -36,6 +36,7 @@ struct ClusterConfig {
   int delta = 5;
   bool verbose = true;
   bool align = false;  // classifier feature is Feature::align (Runner.cpp:32-34, 332)
+  int width = 1;       // histogram bytes per bin (Runner.cpp:75-89)
 };
 
 struct ClusterStats {

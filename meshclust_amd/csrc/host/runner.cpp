@@ -25,7 +25,8 @@ namespace mc {
 
 static void usage(const char *prog) {
   printf("Usage: %s *.fasta [--id 0.90] [--kmer 3] [--delta 5] [--output output.clstr] [--iterations 20] "
-         "[--align] [--sample 3000] [--pivot 40] [--threads TMAX] [--device GPU] [--stats-json FILE]\n",
+         "[--align] [--sample 3000] [--pivot 40] [--threads TMAX] [--device GPU] [--devices GPU,GPU,..] "
+         "[--stats-json FILE]\n",
          prog);
   printf("MI355X-native MeShClust (meshclust_amd, C-ABI v%d)\n", MC_ABI_VERSION);
 }
@@ -81,6 +82,16 @@ Options parse_options(int argc, char **argv, bool require_files) {
       i++;
     } else if (arg == "--device" && i + 1 < argc) {
       o.device = atoi(argv[++i]);
+    } else if (arg == "--devices" && i + 1 < argc) {
+      o.devices.clear();
+      for (const char *p = argv[++i]; *p;) {
+        char *end = nullptr;
+        long d = strtol(p, &end, 10);
+        if (end == p || d < 0) throw OptionError("--devices takes a comma-separated list of GPU indices", 1, false);
+        o.devices.push_back((int)d);
+        p = *end == ',' ? end + 1 : end;
+        if (*end && *end != ',') throw OptionError("--devices takes a comma-separated list of GPU indices", 1, false);
+      }
     } else if (arg == "--stats-json" && i + 1 < argc) {
       o.stats_json = argv[++i];
     } else if (arg == "--quiet") {
@@ -203,6 +214,7 @@ RunResult run_pipeline(const Dataset &ds, mc_ctx *ctx, Options opt, bool upload,
   cc.delta = opt.delta;
   cc.verbose = verbose;
   cc.align = opt.align;
+  cc.width = rr.width;
   cc.comm = comm;
   rr.part = mean_shift_cluster(ds, ctx, bv, cc, rr.timer, rr.stats);
   rr.stats.nw_pairs = tr.nw_pairs;
@@ -243,6 +255,47 @@ static void write_stats(const std::string &path, const RunResult &rr, double par
   fclose(f);
 }
 
+// --devices: one host thread per GPU, each with its own context and RCCL rank, sharing one
+// clustering (cluster.cpp: sharded get_close steps, centre all-gather per mean-shift
+// iteration).  Every rank ends with the same partition; rank 0's is written.
+static int allgather_rccl(void *user, const void *in, uint64_t bytes, void *out) {
+  return mc_comm_allgather((mc_comm *)user, in, bytes, out);
+}
+
+static RunResult run_multi_gpu(const Dataset &ds, const Options &opt) {
+  const int W = (int)opt.devices.size();
+  uint8_t id[MC_COMM_ID_BYTES];
+  check(mc_comm_unique_id(id), "mc_comm_unique_id");
+  std::vector<RunResult> res(W);
+  std::vector<std::exception_ptr> err(W);
+  std::vector<std::thread> th;
+  for (int r = 0; r < W; r++)
+    th.emplace_back([&, r]() {
+      mc_ctx *ctx = nullptr;
+      mc_comm *comm = nullptr;
+      try {
+        check(mc_ctx_create(opt.devices[r], &ctx), "mc_ctx_create");
+        check(mc_comm_create(opt.devices[r], r, W, id, &comm), "mc_comm_create");
+        ShardComm sc;
+        sc.rank = r;
+        sc.world = W;
+        sc.allgather = allgather_rccl;
+        sc.user = comm;
+        Options o = opt;
+        o.quiet = opt.quiet || r != 0;
+        res[r] = run_pipeline(ds, ctx, o, true, &sc);
+      } catch (...) {
+        err[r] = std::current_exception();
+      }
+      if (comm) mc_comm_destroy(comm, err[r] ? 1 : 0);
+      if (ctx) mc_ctx_destroy(ctx);
+    });
+  for (auto &t : th) t.join();
+  for (int r = 0; r < W; r++)
+    if (err[r]) std::rethrow_exception(err[r]);
+  return std::move(res[0]);
+}
+
 int meshclust_main(int argc, char **argv) {
   Options opt;
   try {
@@ -268,8 +321,13 @@ int meshclust_main(int argc, char **argv) {
     Dataset ds;
     parse_fasta_files(opt.files, ds, threads);
     double parse_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    check(mc_ctx_create(opt.device, &ctx), "mc_ctx_create");
-    RunResult rr = run_pipeline(ds, ctx, opt);
+    RunResult rr;
+    if (opt.devices.size() > 1) {
+      rr = run_multi_gpu(ds, opt);
+    } else {
+      check(mc_ctx_create(opt.devices.empty() ? opt.device : opt.devices[0], &ctx), "mc_ctx_create");
+      rr = run_pipeline(ds, ctx, opt);
+    }
     auto t1 = std::chrono::steady_clock::now();
     if (!opt.quiet) printf("Printing output\n");
     write_clstr(opt.output, ds, rr.part, threads);

@@ -25,6 +25,7 @@ struct Options {
   std::vector<std::string> files;
   // additions of this implementation
   int device = 0;
+  std::vector<int> devices;  // --devices 0,1,..: one clustering shared by these GPUs (RCCL)
   bool quiet = false;
   std::string stats_json;  // per-phase timings + work counts
 };

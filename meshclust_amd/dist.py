@@ -1,13 +1,18 @@
 """One clustering shared by several GPUs: one process per GPU over
 torch.distributed.
 
-MeShClust's accumulation is a chain of dependent steps (the next centre is the member closest
-to the current mean), so every rank runs it -- on its own GPU, deterministically, with the
-same result.  The mean-shift update that follows is independent per centre: each rank computes
-the new centres of its share (``mc_mean_shift_range``) and the ranks all-gather them, the
-centre-reassignment exchange, once per iteration.  The C++ driver calls back into Python for
-that exchange (``mcl_run_sharded``); with the ``nccl`` backend (RCCL on ROCm) the blocks travel
-as device tensors, with ``gloo`` as host tensors.
+The C++ driver (csrc/host/cluster.cpp) splits every get_close step of the accumulation over the
+ranks by record -- rank r scans the alive candidates of the window in its static bvec blocks
+(mc_scan_part) -- and the ranks all-gather one 1 KiB block per step ({first maximum of combo 0,
+is_min, flagged positions}) before every rank applies the same remove_available + get_mean
+(mc_scan_commit).  Each mean-shift iteration is split by centre and the ranks all-gather the
+new centres (the centre-reassignment exchange).  The exchange is a C callback
+``allgather(user, in, bytes, out)``:
+
+* ``RcclShardComm`` -- RCCL over xGMI, called from C++ (libmcgpu's mc_comm_allgather); torch
+  only distributes the communicator id (the product path on GPUs);
+* ``TorchShardComm`` -- a Python callback over a torch.distributed group (gloo on CPUs: the
+  CPU tests, where no RCCL exists).
 
 Results are identical to a single-rank run (tests/test_distributed.py).
 """
@@ -16,8 +21,40 @@ import ctypes as C
 ALLGATHER = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p)
 
 
+class RcclShardComm:
+    """An RCCL communicator of libmcgpu (mc_comm) for this rank's GPU; rank 0's id is broadcast
+    over the default torch.distributed group."""
+
+    def __init__(self, device, group=None):
+        import torch.distributed as dist
+        from . import gpu_lib, MCError
+        self.lib = gpu_lib()
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        uid = C.create_string_buffer(128)
+        if self.rank == 0 and self.lib.mc_comm_unique_id(uid) != 0:
+            raise MCError("mc_comm_unique_id: " + self.lib.mc_last_error().decode())
+        box = [uid.raw]
+        dist.broadcast_object_list(box, src=0, group=group)
+        self.user = C.c_void_p()
+        if self.lib.mc_comm_create(device, self.rank, self.world, box[0], C.byref(self.user)) != 0:
+            raise MCError("mc_comm_create: " + self.lib.mc_last_error().decode())
+        self.callback = C.cast(self.lib.mc_comm_allgather, C.c_void_p)  # called from C++ directly
+
+    @property
+    def calls(self):
+        c, b = C.c_uint64(), C.c_uint64()
+        self.lib.mc_comm_stats(self.user, C.byref(c), C.byref(b))
+        return c.value
+
+    def close(self, abort=False):
+        if self.user:
+            self.lib.mc_comm_destroy(self.user, 1 if abort else 0)
+            self.user = C.c_void_p()
+
+
 class TorchShardComm:
-    """All-gather of equal byte blocks over a torch.distributed process group."""
+    """All-gather of equal byte blocks over a torch.distributed process group (Python callback)."""
 
     def __init__(self, group=None):
         import torch
@@ -29,6 +66,7 @@ class TorchShardComm:
         self.device = torch.device("cuda", torch.cuda.current_device()) if nccl else torch.device("cpu")
         self.calls = 0
         self.bytes = 0
+        self.user = None
         self.callback = ALLGATHER(self._allgather)  # keep a reference: C holds the pointer
 
     def _allgather(self, _user, src, nbytes, dst):
@@ -48,3 +86,6 @@ class TorchShardComm:
             return 0
         except Exception:  # reported to the driver as a failed exchange (it raises)
             return 1
+
+    def close(self, abort=False):
+        pass

@@ -322,6 +322,54 @@ int mc_scan(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, uint32_t *flagge
   return MC_OK;
 }
 
+int mc_scan_part(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, uint32_t part, uint32_t nparts, uint32_t *flagged,
+                 uint64_t cap, mc_scan_result *res) {
+  if (c->align) return fail(MC_ERR_UNSUPPORTED, "sharded get_close steps take k-mer histograms");
+  if (S > E || E >= c->order.size() || nparts == 0 || part >= nparts) return fail(MC_ERR_ARG, "bad sharded window");
+  memset(res, 0, sizeof *res);
+  double best_val = -1;
+  bool has = false;
+  uint64_t best_pos = 0, nf = 0;
+  for (uint64_t pos = S; pos <= E; pos++) {
+    if (!c->alive[pos] || (pos / MC_SHARD_BLOCK) % nparts != part) continue;
+    double s, c0;
+    const int d = classify(c, c->order[pos], centre, &s, &c0);
+    if (c0 > best_val) {
+      best_val = c0;
+      best_pos = pos;
+      has = true;
+    }
+    if (d) {
+      if (nf >= cap) return fail(MC_ERR_ARG, "flag buffer too small");
+      flagged[nf++] = (uint32_t)pos;
+    }
+  }
+  res->is_min = nf == 0;
+  res->has_best = has;
+  res->best_pos = best_pos;
+  res->best_val = best_val;
+  res->n_flagged = nf;
+  res->new_centre = 0xffffffffu;
+  res->n_members = (uint32_t)c->members.size();
+  return MC_OK;
+}
+
+int mc_scan_commit(mc_ctx *c, const uint32_t *flagged, uint64_t n, mc_scan_result *res) {
+  if (c->align) return fail(MC_ERR_UNSUPPORTED, "sharded get_close steps take k-mer histograms");
+  memset(res, 0, sizeof *res);
+  for (uint64_t i = 0; i < n; i++) {
+    if (flagged[i] >= c->order.size() || !c->alive[flagged[i]] || (i && flagged[i] <= flagged[i - 1]))
+      return fail(MC_ERR_ARG, "mc_scan_commit: positions must be ascending, alive and in range");
+    c->alive[flagged[i]] = 0;
+    c->members.push_back(c->order[flagged[i]]);
+  }
+  res->is_min = n == 0;
+  res->n_flagged = n;
+  res->new_centre = n ? mean_closest(c, c->members) : 0xffffffffu;
+  res->n_members = (uint32_t)c->members.size();
+  return MC_OK;
+}
+
 int mc_mean_shift_select(mc_ctx *c, const uint32_t *cid, uint32_t C, const uint64_t *off, const uint32_t *members,
                          int delta, const uint8_t *keep, uint32_t *newc) {
   uint64_t k = 0;
@@ -363,6 +411,15 @@ int mc_accumulate(mc_ctx *, const uint32_t *, const uint64_t *, uint32_t, double
                   uint64_t *, uint64_t *) {
   return fail(MC_ERR_UNSUPPORTED, "the CPU oracle engine drives accumulation step by step");
 }
+
+// RCCL is a GPU-side transport: the CPU engine's ranks exchange through the caller's callback.
+int mc_comm_unique_id(uint8_t *) { return fail(MC_ERR_UNSUPPORTED, "no RCCL in the CPU oracle engine"); }
+int mc_comm_create(int, int, int, const uint8_t *, mc_comm **) {
+  return fail(MC_ERR_UNSUPPORTED, "no RCCL in the CPU oracle engine");
+}
+int mc_comm_allgather(mc_comm *, const void *, uint64_t, void *) { return MC_ERR_UNSUPPORTED; }
+int mc_comm_stats(const mc_comm *, uint64_t *, uint64_t *) { return MC_ERR_UNSUPPORTED; }
+int mc_comm_destroy(mc_comm *, int) { return MC_OK; }
 
 int mc_timers(mc_ctx *, double *ms, int n, int) {
   for (int i = 0; i < n; i++) ms[i] = 0;

@@ -1,6 +1,8 @@
 """One rank of a sharded clustering (launched by torch.distributed.run; see
 tests/test_distributed.py).  Engine: the CPU oracle engine (test-only) or, with --gpu, the
-product's libmcgpu on this rank's GPU."""
+product's libmcgpu on cuda:0 (every rank: the test boxes have one GPU).  Exchange: a gloo
+all-gather through a Python callback, or with --rccl libmcgpu's RCCL communicator called from
+C++ (one rank per GPU, so world size 1 on a one-GPU box)."""
 import argparse
 import ctypes as C
 import json
@@ -16,20 +18,22 @@ def main():
     ap.add_argument("fasta")
     ap.add_argument("out")
     ap.add_argument("--gpu", action="store_true")
+    ap.add_argument("--rccl", action="store_true")
     ap.add_argument("flags", nargs="*")
     a = ap.parse_args()
     import torch.distributed as dist
     dist.init_process_group("gloo", init_method="env://")
-    from meshclust_amd.dist import TorchShardComm
-    comm = TorchShardComm()
+    from meshclust_amd.dist import RcclShardComm, TorchShardComm
     if a.gpu:
         import meshclust_amd as M
         eng = M.Engine(0)
+        comm = RcclShardComm(0) if a.rccl else TorchShardComm()
         ds = M.Dataset([a.fasta], threads=4)
         st = ds.run(eng, a.flags + ["--threads", "4"], upload=True, clstr=a.out if comm.rank == 0 else None,
                     comm=comm)
         eng.close()
     else:
+        comm = TorchShardComm()
         lib = C.CDLL(os.path.join(ROOT, "oracle", "_build", "libmeshclust_cpu.so"))
         lib.mcl_parse.restype = C.c_void_p
         lib.mcl_parse.argtypes = [C.POINTER(C.c_char_p), C.c_int, C.c_int, C.c_char_p, C.c_int]
@@ -45,11 +49,13 @@ def main():
         buf = C.create_string_buffer(1 << 16)
         rc = lib.mcl_run_sharded(ds, ctx, len(argv), (C.c_char_p * len(argv))(*argv), 1,
                                  a.out.encode() if comm.rank == 0 else None, buf, len(buf), comm.rank, comm.world,
-                                 C.cast(comm.callback, C.c_void_p), None)
+                                 C.cast(comm.callback, C.c_void_p), comm.user)
         assert rc == 0, buf.value
         st = json.loads(buf.value.decode())
     with open(a.out + ".rank%d.json" % comm.rank, "w") as f:
-        json.dump({"calls": comm.calls, "bytes": comm.bytes, "clusters": st.get("clusters")}, f)
+        json.dump({"calls": comm.calls, "clusters": st.get("clusters"), "accum_path": st.get("accum_path"),
+                   "scan_steps": st.get("scan_steps")}, f)
+    comm.close()
     dist.destroy_process_group()
 
 
