@@ -114,16 +114,18 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    if world > 1:
+    if world > 1 or a.shard:
         import torch.distributed as dist  # noqa: F811
-        dist.init_process_group("gloo", init_method="env://")
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29517")
+        dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=world)
 
     import meshclust_amd as M
     if rank == 0 and not os.path.exists(M.GPU_LIB):
         M.build()
     if dist:
         dist.barrier()
-    shard = dist is not None and a.shard
+    shard = dist is not None and a.shard  # (MC_SHARD_FORCE=1 takes the sharded steps at N = 1 too)
     fasta = ensure_fasta(a.n, a.len, a.templates, a.mut, a.seed + (0 if shard else rank))
     threads = min(16, host_threads())
     eng = M.Engine(local)

@@ -825,27 +825,40 @@ int mc_accumulate(mc_ctx *c, const uint32_t *bin_lo, const uint64_t *bounds, uin
             (unsigned long long)out[1], out[5] / 1e5, out[12] / 1e5, out[13] / 1e5, out[14] / 1e5, out[6] / 1e5,
             out[7] / 1e5, out[8] / 1e5, out[9] / 1e5, out[10] / 1e5, out[11] / 1e5);
     if (atoi(getenv("MC_ACCUM_PROFILE")) >= 2 && c->s_h.p) {
-      // per step (first 4096): record published -> seen by the last active worker -> its scan
-      // done -> its partial stored -> controller has every partial -> collect done
-      std::vector<uint64_t> tr(4096 * 8);
+      // per step (first 4096; accum.hip trace_mark): record published -> first / last active
+      // worker saw it -> first / last scan done -> first / last partial stored -> controller
+      // has every partial -> collect done
+      const int TW = 16;
+      std::vector<uint64_t> tr(4096 * TW);
       MCG_CHECK(hipMemcpy(tr.data(), c->s_h.p, tr.size() * 8, hipMemcpyDeviceToHost));
-      double a[5] = {0, 0, 0, 0, 0};
-      uint64_t cnt = 0, nact = 0;
+      double a[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, m[5] = {0, 0, 0, 0, 0};
+      uint64_t cnt = 0, nact = 0, mcnt = 0;
+      for (uint64_t st = 1; st < 4096; st++) {  // MC_ACCUM_PROFILE=2: the middle active worker
+        const uint64_t *t = &tr[st * TW];
+        if (!t[0] || !t[10] || !t[14]) continue;
+        for (int i = 0; i < 5; i++) m[i] += (double)(int64_t)(t[10 + i] - t[0]);
+        mcnt++;
+      }
+      if (mcnt)
+        fprintf(stderr, "[accum trace] middle worker, avg us after publish: seen %.2f kill-log %.2f wave0-scanned %.2f "
+                "all-scanned %.2f partial %.2f\n", m[0] / mcnt / 100, m[1] / mcnt / 100, m[2] / mcnt / 100,
+                m[3] / mcnt / 100, m[4] / mcnt / 100);
       for (uint64_t st = 1; st < 4096; st++) {
-        const uint64_t *t = &tr[st * 8];
-        if (!t[0] || !t[2] || !t[5] || !t[6]) continue;
-        a[0] += (double)(int64_t)(t[2] - t[0]);
-        a[1] += (double)(int64_t)(t[3] - t[2]);
-        a[2] += (double)(int64_t)(t[4] - t[3]);
-        a[3] += (double)(int64_t)(t[5] - t[4]);
-        a[4] += (double)(int64_t)(t[6] - t[5]);
-        nact += t[7];
+        const uint64_t *t = &tr[st * TW];
+        if (!t[0] || !t[7] || !t[8]) continue;
+        const uint64_t p = t[0], s0 = ~t[1], s1 = t[2], c0 = ~t[3], c1 = t[4], q0 = ~t[5], q1 = t[6];
+        const double d[9] = {(double)(int64_t)(s0 - p), (double)(int64_t)(s1 - p), (double)(int64_t)(c0 - p),
+                             (double)(int64_t)(c1 - p), (double)(int64_t)(q0 - p), (double)(int64_t)(q1 - p),
+                             (double)(int64_t)(t[7] - p), (double)(int64_t)(t[8] - p), 0.0};
+        for (int i = 0; i < 8; i++) a[i] += d[i];
+        nact += t[9];
         cnt++;
       }
       if (cnt)
-        fprintf(stderr, "[accum trace] %llu steps, avg us: publish->seen %.2f scan %.2f ->partial %.2f ->all seen %.2f "
-                "collect %.2f; active WGs %.1f\n", (unsigned long long)cnt, a[0] / cnt / 100, a[1] / cnt / 100,
-                a[2] / cnt / 100, a[3] / cnt / 100, a[4] / cnt / 100, (double)nact / cnt);
+        fprintf(stderr, "[accum trace] %llu steps, avg us after publish: seen %.2f..%.2f scanned %.2f..%.2f "
+                "partial %.2f..%.2f all-seen %.2f collect-done %.2f; active WGs %.1f\n", (unsigned long long)cnt,
+                a[0] / cnt / 100, a[1] / cnt / 100, a[2] / cnt / 100, a[3] / cnt / 100, a[4] / cnt / 100,
+                a[5] / cnt / 100, a[6] / cnt / 100, a[7] / cnt / 100, (double)nact / cnt);
     }
   }
   return MC_OK;

@@ -52,6 +52,7 @@ constexpr uint32_t NONE = 0xffffffffu;
 constexpr uint64_t NONE64 = ~0ull;
 constexpr uint32_t RING = 64;          // step records kept for workgroups that read them late
 constexpr uint32_t TRACE_STEPS = 4096;
+constexpr int TRACE_W = 16;            // trace words per step (MC_ACCUM_PROFILE=2), see trace_mark
 constexpr int KINL = 4;                // kill-log entries carried inline in a step record
 constexpr int REC_HDR = 14;            // centre, S, E, kn, KINL kills, mag / sumsq / len (2 each)
 constexpr int PART_G = 8;              // granules per partial
@@ -72,7 +73,7 @@ struct WinTab {
 // What the controller needs of a static position when it joins a cluster: magnitudes and
 // window data, one 64-byte line (its row is in the row-major static copy `hr`)
 struct MInfo {
-  uint64_t mag, sumsq, len, pad;
+  uint64_t mag, sumsq, len, bin;  // bin: the bvec bin holding this static position
   WinTab wt;
 };
 
@@ -108,10 +109,23 @@ struct AccArgs {
   uint64_t *out;        // [0] clusters [1] steps [2] candidates [3] error [4] members, timers
   uint64_t budget;      // longest wait for one hand-off, s_memrealtime ticks (100 MHz)
   int prof;             // controller phase timers (MC_ACCUM_PROFILE)
-  uint64_t *trace;      // MC_ACCUM_PROFILE=2: per-step timestamps, TRACE_STEPS x 8
+  uint64_t *trace;      // MC_ACCUM_PROFILE>=2: per-step timestamps, TRACE_STEPS x TRACE_W
+  int trace_all;        // MC_ACCUM_PROFILE=3: every active worker marks min/max (atomics)
 };
 
 __device__ __forceinline__ uint64_t now() { return __builtin_amdgcn_s_memrealtime(); }
+
+// Step trace (MC_ACCUM_PROFILE=2/3), words per step: 0 record published, 7 controller has
+// every partial, 8 collect done, 9 active workers; =3: 1/2 first/last worker saw it, 3/4
+// first/last scan done, 5/6 first/last partial stored (minima kept as maxima of ~t); =2: the
+// middle active worker alone (plain stores) 10 saw it, 11 kill log applied, 12 wave 0 scanned,
+// 13 every wave scanned + reduced, 14 partial stored.
+__device__ __forceinline__ void trace_mark(const AccArgs &A, uint32_t step, int slot, uint64_t t) {
+  if (!A.trace || !A.trace_all || step >= TRACE_STEPS) return;
+  uint64_t *w = A.trace + (uint64_t)step * TRACE_W;
+  atomicMax((unsigned long long *)&w[slot], (unsigned long long)~t);
+  atomicMax((unsigned long long *)&w[slot + 1], (unsigned long long)t);
+}
 __device__ __forceinline__ bool timed_out(const AccArgs &A, uint64_t t0) { return now() - t0 > A.budget; }
 
 // Hand-off primitives: relaxed agent-scope atomics lower to global loads / stores with sc1
@@ -281,9 +295,9 @@ struct DevBvec {
     return a;
   }
   // kill one static position (bvec::pop / erase / remove_available); any thread, atomics
-  __device__ void kill_one(uint64_t p) {
+  __device__ void kill_one(uint64_t p) { kill_in(p, bin_of(p)); }
+  __device__ void kill_in(uint64_t p, uint64_t b) {  // ... when its bin b is known
     atomicAnd(&bits[p >> 5], ~(1u << (p & 31)));
-    const uint64_t b = bin_of(p);
     atomicSub(&cn[b], 1u);
     for (uint64_t i = b + 1; i <= nb; i += i & (~i + 1)) atomicSub(&fw[i], 1u);
   }
@@ -333,7 +347,15 @@ __global__ __launch_bounds__(256) void wintab_kernel(uint64_t n, const uint64_t 
     m.mag = mag_s[id];
     m.sumsq = sumsq_s[id];
     m.len = L;
-    m.pad = 0;
+    {  // bin: bin_lo[b] <= id < bin_lo[b + 1]
+      uint64_t a = 0, z = nb;
+      while (z - a > 1) {
+        const uint64_t mid = (a + z) / 2;
+        if (bin_lo[mid] <= id) a = mid;
+        else z = mid;
+      }
+      m.bin = a;
+    }
     m.wt = w;
     out[id] = m;
     for (int c = 0; c < nch; c++) hr[id * nch + c] = hs[(uint64_t)c * npad + id];
@@ -379,17 +401,24 @@ __device__ __forceinline__ void worker(const AccArgs &A, const DevClassifier &C,
   // are the controller's pops and erases, which arrive with the step records
   for (uint64_t i = threadIdx.x; i < A.fcap; i += NT) lal[i] = 1;
   const int res = A.res;
-  uint64_t rmag[2] = {0, 0}, rsq[2] = {0, 0}, rlen[2] = {0, 0};  // resident magnitudes (res <= 2 kept here)
-  PTerms rterm[2] = {{0, 0, 0.0}, {0, 0, 0.0}};
+  // resident chunks' per-candidate data (res <= 2 kept in registers; fixed indices only, so
+  // nothing is spilled to scratch)
+  PInfo rinf0{0, 0, 0}, rinf1{0, 0, 0};
+  PTerms rterm0{0, 0, 0.0}, rterm1{0, 0, 0.0};
   for (int i = 0; i < res; i++) {
     const uint64_t pos = ((uint64_t)w + (uint64_t)i * GW) * NT + threadIdx.x;
     for (int k = 0; k < nch; k++)
       lrow[((uint64_t)i * nch + k) * NT + threadIdx.x] = pos < A.N ? A.hs[(uint64_t)k * A.npad + pos] : make_uint4(0, 0, 0, 0);
     if (i < 2 && pos < A.N) {
-      rmag[i] = A.mag_s[pos];
-      rsq[i] = A.sumsq_s[pos];
-      rlen[i] = A.len_s[pos];
-      rterm[i] = pterms(rmag[i], rsq[i], A.B);
+      const PInfo pi{A.mag_s[pos], A.sumsq_s[pos], A.len_s[pos]};
+      const PTerms pt = pterms(pi.mag, pi.sumsq, A.B);
+      if (i == 0) {
+        rinf0 = pi;
+        rterm0 = pt;
+      } else {
+        rinf1 = pi;
+        rterm1 = pt;
+      }
     }
   }
   if (threadIdx.x == 0) s_abort = 0;
@@ -468,7 +497,7 @@ __device__ __forceinline__ void worker(const AccArgs &A, const DevClassifier &C,
     }
     seen = s_go;
     uint64_t t_seen = 0;
-    if (A.trace && threadIdx.x == 0) t_seen = now();
+    if (A.trace && threadIdx.x == 0) t_seen = now();  // (recorded only by active workers)
     const uint32_t *hdr = srec + 4 * nch;
     if (hdr[0] == NONE) return;  // accumulation finished
     const uint64_t P_S = hdr[1], P_E = hdr[2];
@@ -488,6 +517,8 @@ __device__ __forceinline__ void worker(const AccArgs &A, const DevClassifier &C,
       }
       kcur = kend;
     }
+    uint64_t t_klog = 0;
+    if (A.trace && threadIdx.x == 0) t_klog = now();
     // ---- the chunks of the window this worker owns: Trainer::get_close ----------------
     const uint64_t c0 = P_S / NT, c1 = P_E / NT;
     const uint32_t nact = (uint32_t)(c1 - c0 + 1 < (uint64_t)GW ? c1 - c0 + 1 : (uint64_t)GW);
@@ -527,10 +558,10 @@ __device__ __forceinline__ void worker(const AccArgs &A, const DevClassifier &C,
         }
         int d;
         if (li < 2 && C.layout) {
-          d = classify_std(C, acc.finish(rmag[li], pc.mag), PInfo{rmag[li], rsq[li], rlen[li]}, rterm[li], pc, tq, A.B,
-                           &cv);
+          const PInfo pi = li == 0 ? rinf0 : rinf1;
+          d = classify_std(C, acc.finish(pi.mag, pc.mag), pi, li == 0 ? rterm0 : rterm1, pc, tq, A.B, &cv);
         } else {
-          const PInfo pi = li < 2 ? PInfo{rmag[li], rsq[li], rlen[li]} : PInfo{A.mag_s[pos], A.sumsq_s[pos], A.len_s[pos]};
+          const PInfo pi = li == 0 ? rinf0 : li == 1 ? rinf1 : PInfo{A.mag_s[pos], A.sumsq_s[pos], A.len_s[pos]};
           d = classify_cand<T>(acc, pi, pc, A.B, C, &cv);
         }
         if (d) {
@@ -584,7 +615,14 @@ __device__ __forceinline__ void worker(const AccArgs &A, const DevClassifier &C,
     }
     drain();  // this wave's flagged-list stores are complete before the partial announces them
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (A.trace && !A.trace_all && threadIdx.x == 0 && mine == nact / 2 && seen < TRACE_STEPS) {
+      uint64_t *tr = A.trace + (uint64_t)seen * TRACE_W;
+      tr[10] = t_seen;
+      tr[11] = t_klog;
+      tr[12] = t_scanned;
+      tr[13] = now();
+    }
+    if (threadIdx.x < PART_G) {  // lane j of wave 0 stores granule j
       double v = s_bv[0];
       uint64_t p = s_bp[0];
       for (int i = 1; i < NW; i++)
@@ -592,20 +630,23 @@ __device__ __forceinline__ void worker(const AccArgs &A, const DevClassifier &C,
           v = s_bv[i];
           p = s_bp[i];
         }
-      uint64_t *q = A.partials + (uint64_t)w * PART_G;
       const uint64_t vb = (uint64_t)__double_as_longlong(v);
-      st64(q + 0, gran(seen, (uint32_t)(vb >> 32)));
-      st64(q + 1, gran(seen, (uint32_t)vb));
-      st64(q + 2, gran(seen, p == NONE64 ? NONE : (uint32_t)p));
-      st64(q + 3, gran(seen, s_nfl));
-      st64(q + 4, gran(seen, s_nscan));
-      for (int j = 0; j < INL; j++) st64(q + 5 + j, gran(seen, (uint32_t)j < s_nfl ? s_inl[j] : NONE));
-      if (A.trace && mine == nact - 1 && seen < TRACE_STEPS) {
-        uint64_t *tr = A.trace + (uint64_t)seen * 8;
-        tr[2] = t_seen;
-        tr[3] = t_scanned;
-        tr[4] = now();
-        tr[7] = nact;
+      const int j = threadIdx.x;
+      const uint32_t nfl = s_nfl;
+      const uint32_t data = j == 0   ? (uint32_t)(vb >> 32)
+                            : j == 1 ? (uint32_t)vb
+                            : j == 2 ? (p == NONE64 ? NONE : (uint32_t)p)
+                            : j == 3 ? nfl
+                            : j == 4 ? s_nscan
+                                     : ((uint32_t)(j - 5) < nfl ? s_inl[j - 5] : NONE);
+      st64(A.partials + (uint64_t)w * PART_G + j, gran(seen, data));
+      if (A.trace && !A.trace_all && j == 0 && mine == nact / 2 && seen < TRACE_STEPS)
+        A.trace[(uint64_t)seen * TRACE_W + 14] = now();
+      if (A.trace && A.trace_all && j == 0) {
+        const uint64_t t = now();
+        trace_mark(A, seen, 1, t_seen);
+        trace_mark(A, seen, 3, t_scanned);
+        trace_mark(A, seen, 5, t);
       }
     }
   }
@@ -754,8 +795,8 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
     st32(A.mem_pos + cl_start + qm, p);
     st64(A.mkeys + cl_start + qm, key);
     const uint4 *hrow = A.hr + (uint64_t)p * nch;
+    const MInfo mi = A.minfo[p];
     if (qm < A.mrow) {
-      const MInfo mi = A.minfo[p];
       mc.pos[qm] = p;
       mc.key[qm] = key;
       mc.info[qm * 3 + 0] = mi.mag;
@@ -773,7 +814,7 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
           if (pv[e]) atomicAdd((unsigned long long *)&msum[k * per + e], (unsigned long long)pv[e]);
       }
     }
-    bv.kill_one(p);
+    bv.kill_in(p, mi.bin);
   };
 
   // bvec after insert_finalize: every static position alive
@@ -875,7 +916,7 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
       const uint64_t t = now();
       t_ws[2] += t - t_mark;
       t_mark = t;
-      if (A.trace && step < TRACE_STEPS) A.trace[(uint64_t)step * 8 + 0] = t;
+      if (A.trace && step < TRACE_STEPS) A.trace[(uint64_t)step * TRACE_W + 0] = t;
     }
     if (!have) break;  // the record told the workers to stop
 
@@ -952,7 +993,10 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
     }
     if (threadIdx.x == 0) s_sumF = 0;
     __syncthreads();
-    if (A.trace && threadIdx.x == 0 && step < TRACE_STEPS) A.trace[(uint64_t)step * 8 + 5] = now();
+    if (A.trace && threadIdx.x == 0 && step < TRACE_STEPS) {
+      A.trace[(uint64_t)step * TRACE_W + 7] = now();
+      A.trace[(uint64_t)step * TRACE_W + 9] = nact;
+    }
     if (s_abort) {
       if (threadIdx.x == 0) atomicMax((unsigned long long *)&A.out[3], 99ull);
       return;
@@ -1108,7 +1152,7 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
     if (A.prof && threadIdx.x == 0) {
       const uint64_t t = now();
       t_coll += t - t_mark;
-      if (A.trace && step < TRACE_STEPS) A.trace[(uint64_t)step * 8 + 6] = t;
+      if (A.trace && step < TRACE_STEPS) A.trace[(uint64_t)step * TRACE_W + 8] = t;
     }
   }
   if (threadIdx.x == 0) {
@@ -1293,9 +1337,10 @@ int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, 
   A.prof = getenv("MC_ACCUM_PROFILE") ? 1 : 0;
   A.trace = nullptr;
   if (getenv("MC_ACCUM_PROFILE") && atoi(getenv("MC_ACCUM_PROFILE")) >= 2) {
-    if (ensure(c->s_h, TRACE_STEPS * 64)) return MC_ERR_OOM;
-    MCG_CHECK(hipMemsetAsync(c->s_h.p, 0, TRACE_STEPS * 64, c->stream));
+    if (ensure(c->s_h, TRACE_STEPS * TRACE_W * 8)) return MC_ERR_OOM;
+    MCG_CHECK(hipMemsetAsync(c->s_h.p, 0, TRACE_STEPS * TRACE_W * 8, c->stream));
     A.trace = (uint64_t *)c->s_h.p;
+    A.trace_all = atoi(getenv("MC_ACCUM_PROFILE")) >= 3;
   }
   if (getenv("MC_ACCUM_PROFILE"))
     fprintf(stderr, "[accum] variant: width %d nch %d resident chunks/worker %d global-bitmap %d member-cache %u lds %zu G %u\n",
