@@ -145,10 +145,7 @@ __device__ __forceinline__ uint32_t ld32(const uint32_t *p) {
 __device__ __forceinline__ void drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 __device__ __forceinline__ uint64_t gran(uint32_t tag, uint32_t data) { return ((uint64_t)tag << 32) | data; }
 
-__device__ __forceinline__ uint32_t wave_sum32(uint32_t v) {
-  for (int o = 32; o >= 1; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o, 64);
-  return v;
-}
+__device__ __forceinline__ uint32_t wave_sum32(uint32_t v) { return wave_sum32_all(v); }
 
 __device__ __forceinline__ bool better(double v, uint64_t p, double bv, uint64_t bp) {
   return v > bv || (v == bv && p < bp);
@@ -215,7 +212,7 @@ struct DevBvec {
       const uint64_t bal = __ballot(x != 0);
       if (bal) {
         const int L = __builtin_ctzll(bal);
-        const uint32_t y = (uint32_t)__shfl((int)x, L, 64);
+        const uint32_t y = (uint32_t)__builtin_amdgcn_readlane((int)x, L);
         return ((base + (uint64_t)L) << 5) + (uint64_t)__builtin_ctz(y);
       }
     }
@@ -231,7 +228,7 @@ struct DevBvec {
       const uint64_t bal = __ballot(x != 0);
       if (bal) {
         const int L = __builtin_ctzll(bal);  // lowest lane = highest word
-        const uint32_t y = (uint32_t)__shfl((int)x, L, 64);
+        const uint32_t y = (uint32_t)__builtin_amdgcn_readlane((int)x, L);
         return ((uint64_t)(top - L) << 5) + (uint64_t)(31 - __builtin_clz(y));
       }
     }
@@ -272,12 +269,12 @@ struct DevBvec {
         const uint32_t u = (uint32_t)__shfl_up((int)inc, o, 64);
         if (lane >= o) inc += u;
       }
-      const uint32_t tot = (uint32_t)__shfl((int)inc, 63, 64);
+      const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
       if (c < tot) {
         const uint64_t hit = __ballot(inc > c);
         const int L = __builtin_ctzll(hit);
-        uint32_t y = (uint32_t)__shfl((int)x, L, 64);
-        const uint32_t before = (uint32_t)__shfl((int)(inc - pc), L, 64);
+        uint32_t y = (uint32_t)__builtin_amdgcn_readlane((int)x, L);
+        const uint32_t before = (uint32_t)__builtin_amdgcn_readlane((int)(inc - pc), L);
         for (uint64_t k = c - before; k > 0; k--) y &= y - 1;
         return ((base + (uint64_t)L) << 5) + (uint64_t)__builtin_ctz(y);
       }
@@ -467,7 +464,7 @@ __device__ __forceinline__ void worker(const AccArgs &A, const DevClassifier &C,
             __builtin_amdgcn_s_sleep(1);
           }
         }
-        v = (uint32_t)__shfl((int)v, 0, 64);
+        v = (uint32_t)__builtin_amdgcn_readlane((int)v, 0);
         if (v == seen) {
           state = 2;
           break;
@@ -551,8 +548,20 @@ __device__ __forceinline__ void worker(const AccArgs &A, const DevClassifier &C,
       if ((int64_t)li < res) {  // resident rows (LDS)
         const uint4 *rr = lrow + li * (uint64_t)nch * NT + threadIdx.x;
         if constexpr (NCH > 0) {
+          // every LDS read of a half row in flight before the first use (one wait per half,
+          // not one LDS round trip per chunk)
+          constexpr int HB = NC >= 8 ? 8 : NC;
 #pragma unroll
-          for (int k = 0; k < NC; k++) acc.add(rr[(uint64_t)k * NT], clds[k]);
+          for (int k0 = 0; k0 < NC; k0 += HB) {
+            uint4 rv[HB], cvv[HB];
+#pragma unroll
+            for (int k = 0; k < HB; k++) {
+              rv[k] = rr[(uint64_t)(k0 + k) * NT];
+              cvv[k] = clds[k0 + k];
+            }
+#pragma unroll
+            for (int k = 0; k < HB; k++) acc.add(rv[k], cvv[k]);
+          }
         } else {
           for (int k = 0; k < nch; k++) acc.add(rr[(uint64_t)k * NT], clds[k]);
         }
@@ -560,6 +569,16 @@ __device__ __forceinline__ void worker(const AccArgs &A, const DevClassifier &C,
         if (li < 2 && C.layout) {
           const PInfo pi = li == 0 ? rinf0 : rinf1;
           d = classify_std(C, acc.finish(pi.mag, pc.mag), pi, li == 0 ? rterm0 : rterm1, pc, tq, A.B, &cv);
+#ifdef MC_EXP_DOUBLE_CLASSIFY  // timing experiment: the classifier's cost, run twice
+          {
+            double cv2;
+            PInfo p2 = pi;
+            p2.len += (uint64_t)(A.budget >> 62);  // 0 at run time, unknown to the compiler
+            const int d2 = classify_std(C, acc.finish(p2.mag, pc.mag), p2, li == 0 ? rterm0 : rterm1, pc, tq, A.B, &cv2);
+            d &= d2 | (cv2 == cv ? 1 : 0);
+            cv = cv2 > cv ? cv2 : cv;
+          }
+#endif
         } else {
           const PInfo pi = li == 0 ? rinf0 : li == 1 ? rinf1 : PInfo{A.mag_s[pos], A.sumsq_s[pos], A.len_s[pos]};
           d = classify_cand<T>(acc, pi, pc, A.B, C, &cv);
@@ -599,14 +618,7 @@ __device__ __forceinline__ void worker(const AccArgs &A, const DevClassifier &C,
     uint64_t t_scanned = 0;
     if (A.trace && threadIdx.x == 0) t_scanned = now();
     // first maximum of this worker; scanned count
-    for (int o = 32; o >= 1; o >>= 1) {
-      const double ov = __shfl_xor(best_v, o, 64);
-      const uint64_t op = shfl_xor64(best_p, o);
-      if (better(ov, op, best_v, best_p)) {
-        best_v = ov;
-        best_p = op;
-      }
-    }
+    wave_best_all(best_v, best_p, better);
     nscan = wave_sum32(nscan);
     if (lane == 0) {
       s_bv[wv] = best_v;
@@ -976,14 +988,7 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
       t_mark = t;
     }
     // block reduction: the first maximum, the flagged and scanned totals
-    for (int o = 32; o >= 1; o >>= 1) {
-      const double ov = __shfl_xor(bv_, o, 64);
-      const uint64_t op = shfl_xor64(bp_, o);
-      if (better(ov, op, bv_, bp_)) {
-        bv_ = ov;
-        bp_ = op;
-      }
-    }
+    wave_best_all(bv_, bp_, better);
     const uint32_t wscan = wave_sum32(scan_w), wflag = wave_sum32(cnt_w);
     if (lane == 0) {
       s_bv[wv] = bv_;
@@ -1063,7 +1068,7 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
         reinterpret_cast<T *>(Fl)[b] = (T)F;
         part += F;
       }
-      for (int o = 32; o >= 1; o >>= 1) part += shfl_xor64(part, o);
+      part = wave_sum64_all(part);
       if (lane == 0 && part) atomicAdd((unsigned long long *)&s_sumF, (unsigned long long)part);
       __syncthreads();
       if (A.prof && threadIdx.x == 0) {
@@ -1081,9 +1086,19 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
         uint64_t mp, key;
         if (q < A.mrow) {
           const uint4 *row = mc.row + q * mc.rp;
-          if constexpr (NCH > 0) {
+          if constexpr (NCH > 0) {  // half a row of LDS reads in flight per wait
+            constexpr int HB = NC >= 8 ? 8 : NC;
 #pragma unroll
-            for (int k = 0; k < NC; k++) acc.add(row[k], F4[k]);
+            for (int k0 = 0; k0 < NC; k0 += HB) {
+              uint4 rv[HB], fv[HB];
+#pragma unroll
+              for (int k = 0; k < HB; k++) {
+                rv[k] = row[k0 + k];
+                fv[k] = F4[k0 + k];
+              }
+#pragma unroll
+              for (int k = 0; k < HB; k++) acc.add(rv[k], fv[k]);
+            }
           } else {
             for (int k = 0; k < nch; k++) acc.add(row[k], F4[k]);
           }
@@ -1104,14 +1119,16 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
           bq = q;
         }
       }
-      for (int o = 32; o >= 1; o >>= 1) {
-        const double od = __shfl_xor(bd, o, 64);
-        const uint64_t ok = shfl_xor64(bk, o), oq = shfl_xor64(bq, o);
-        if (od < bd || (od == bd && ok < bk)) {
-          bd = od;
-          bk = ok;
-          bq = oq;
-        }
+      {  // first minimum by (distance, key); keys are unique, so the lane holding it gives q
+        double rd = bd;
+        uint64_t rk = bk;
+        wave_best_all(rd, rk, [](double a, uint64_t ka, double b, uint64_t kb) { return a < b || (a == b && ka < kb); });
+        const uint64_t hit = __ballot(bd == rd && bk == rk);
+        const int L = hit ? __builtin_ctzll(hit) : 0;
+        bq = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(bq >> 32), L) << 32) |
+             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bq, L);
+        bd = rd;
+        bk = rk;
       }
       if (lane == 0) {
         s_bv[wv] = bd;

@@ -55,6 +55,66 @@ struct Acc<uint8_t> {
   }
 };
 
+// ---- wave reductions on DPP (VALU lane moves, no LDS permute) -----------------------------
+// quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror, then row_bcast:15 (rows 1, 3)
+// and row_bcast:31 (rows 2, 3): the reduction of all 64 lanes ends in lane 63.  Lanes of rows a
+// broadcast does not write keep `old`.
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ uint32_t dpp_mv(uint32_t old, uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, CTRL, ROWS, 0xf, false);
+}
+#define MCG_DPP_STEPS(X) X(0xB1, 0xf) X(0x4E, 0xf) X(0x141, 0xf) X(0x140, 0xf) X(0x142, 0xa) X(0x143, 0xc)
+
+// sum of v over the wave, valid in lane 63 (wave_sum32_all: in every lane, via readlane)
+__device__ __forceinline__ uint32_t wave_sum32_l63(uint32_t v) {
+#define MCG_SUM_STEP(C, R) v += dpp_mv<C, R>(0u, v);
+  MCG_DPP_STEPS(MCG_SUM_STEP)
+#undef MCG_SUM_STEP
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_sum32_all(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)wave_sum32_l63(v), 63);
+}
+__device__ __forceinline__ uint64_t wave_sum64_all(uint64_t v) {
+#define MCG_SUM64_STEP(C, R)                                                       \
+  {                                                                                \
+    const uint64_t o = ((uint64_t)dpp_mv<C, R>(0u, (uint32_t)(v >> 32)) << 32) |   \
+                       dpp_mv<C, R>(0u, (uint32_t)v);                              \
+    v += o;                                                                        \
+  }
+  MCG_DPP_STEPS(MCG_SUM64_STEP)
+#undef MCG_SUM64_STEP
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 63);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 63);
+  return ((uint64_t)hi << 32) | lo;
+}
+// the best (value, key) pair of the wave under a strict total order `better(a, ka, b, kb)`,
+// returned in every lane; V is double or uint64_t, keys uint64_t
+template <typename V, typename Better>
+__device__ __forceinline__ void wave_best_all(V &v, uint64_t &k, Better better) {
+#define MCG_BEST_STEP(C, R)                                                                          \
+  {                                                                                                  \
+    const uint64_t vb = __builtin_bit_cast(uint64_t, v);                                             \
+    const uint64_t ov = ((uint64_t)dpp_mv<C, R>((uint32_t)(vb >> 32), (uint32_t)(vb >> 32)) << 32) | \
+                        dpp_mv<C, R>((uint32_t)vb, (uint32_t)vb);                                    \
+    const uint64_t ok = ((uint64_t)dpp_mv<C, R>((uint32_t)(k >> 32), (uint32_t)(k >> 32)) << 32) |   \
+                        dpp_mv<C, R>((uint32_t)k, (uint32_t)k);                                      \
+    const V ovv = __builtin_bit_cast(V, ov);                                                         \
+    if (better(ovv, ok, v, k)) {                                                                     \
+      v = ovv;                                                                                       \
+      k = ok;                                                                                        \
+    }                                                                                                \
+  }
+  MCG_DPP_STEPS(MCG_BEST_STEP)
+#undef MCG_BEST_STEP
+  const uint64_t vb = __builtin_bit_cast(uint64_t, v);
+  const uint64_t r = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(vb >> 32), 63) << 32) |
+                     (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)vb, 63);
+  v = __builtin_bit_cast(V, r);
+  k = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(k >> 32), 63) << 32) |
+      (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)k, 63);
+}
+
 __device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int o) {
   uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
   lo = __shfl_xor(lo, o, 64);
@@ -371,11 +431,14 @@ __device__ uint64_t mean_closest_fast(const RowRef &R, const uint32_t *rows, con
     const uint64_t r = rows[q];
     Acc<T> acc;
     if (nch == 16) {  // k = 4 at 8 bits (or k = 3 at 16): all loads in flight at once
-      uint4 v[16];
+      uint4 v[16], f[16];
 #pragma unroll
-      for (int c = 0; c < 16; c++) v[c] = R.chunk(r, c);
+      for (int c = 0; c < 16; c++) {
+        v[c] = R.chunk(r, c);
+        f[c] = Fl[c];
+      }
 #pragma unroll
-      for (int c = 0; c < 16; c++) acc.add(v[c], Fl[c]);
+      for (int c = 0; c < 16; c++) acc.add(v[c], f[c]);
     } else {
 #pragma unroll 8
       for (int c = 0; c < nch; c++) acc.add(R.chunk(r, c), Fl[c]);
