@@ -131,18 +131,13 @@ def main():
     eng = M.Engine(local)
     args = ["--id", a.id, "--threads", str(threads)]
     comm = None
-    if shard:
-        import torch
-        from meshclust_amd.dist import RcclShardComm, TorchShardComm
-        if torch.cuda.is_available():
-            comm = RcclShardComm(local)  # libmcgpu's RCCL communicator, called from C++
-        else:
-            comm = TorchShardComm()
-
-    import torch
-    if torch.cuda.is_available():
-        torch.cuda.set_device(local)  # sync() below must wait on this rank's GPU, not cuda:0
-    sync = torch.cuda.synchronize if torch.cuda.is_available() else (lambda: None)
+    if shard:  # libmcgpu's RCCL communicator, called from C++ (torch.distributed only hands out its id)
+        from meshclust_amd.dist import RcclShardComm
+        comm = RcclShardComm(local)
+    # The GPU is driven by libmcgpu alone: torch's own HIP runtime (a second HIP/HSA runtime in
+    # the process, from torch's bundled ROCm) is never initialised here -- two runtimes on one
+    # GPU made the process fault in the system HSA runtime's exit handler under rocprofv3.
+    sync = eng.sync  # hipDeviceSynchronize on this rank's GPU
     out_dir = tempfile.mkdtemp(prefix="mc_bench_out")
     clstr = os.path.join(out_dir, "bench_rank%d.clstr" % rank)
 
@@ -283,6 +278,9 @@ def main():
     if comm is not None:
         comm.close()
     eng.close()
+    if os.environ.get("MC_DUMP_MAPS"):  # diagnostics: the process map, to resolve exit-time PCs
+        with open("/proc/self/maps") as f, open(os.environ["MC_DUMP_MAPS"], "w") as g:
+            g.write(f.read())
     import shutil
     shutil.rmtree(out_dir, ignore_errors=True)
     if dist:

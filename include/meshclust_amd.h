@@ -301,6 +301,9 @@ int mc_comm_stats(const mc_comm *comm, uint64_t *calls, uint64_t *bytes);
 /* abort != 0: ncclCommAbort (a peer failed), else ncclCommDestroy. */
 int mc_comm_destroy(mc_comm *comm, int abort);
 
+/* Wait for all work on the context's GPU (every stream; benchmark boundaries). */
+int mc_sync(mc_ctx *ctx);
+
 /* Device time (ms) accumulated per kernel family since the last reset (diagnostics). */
 int mc_timers(mc_ctx *ctx, double *ms_out, int n, int reset);
 

@@ -90,7 +90,7 @@ def gpu_lib():
                      "mc_nw_identity_raw", "mc_set_order", "mc_kill", "mc_cluster_begin", "mc_scan",
                      "mc_mean_shift", "mc_timers", "mc_classify_values", "mc_mean_shift_select", "mc_accumulate",
                      "mc_scan_part", "mc_scan_commit", "mc_comm_unique_id", "mc_comm_create", "mc_comm_allgather",
-                     "mc_comm_stats", "mc_comm_destroy"):
+                     "mc_comm_stats", "mc_comm_destroy", "mc_sync"):
             getattr(lib, name).restype = C.c_int
         lib.mc_comm_create.argtypes = [C.c_int, C.c_int, C.c_int, C.c_char_p, C.POINTER(C.c_void_p)]
         lib.mc_comm_allgather.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]
@@ -282,6 +282,10 @@ class Engine:
         _check(self.lib.mc_nw_identity_raw(self.ctx, _p(a_cat), _p(a_off), _p(b_cat), _p(b_off), C.c_uint64(m),
                                            _p(ident), _p(ln), _p(ids), _p(sc)), "mc_nw_identity_raw")
         return ident, ln, ids, sc
+
+    def sync(self):
+        """Wait for all work on this context's GPU (mc_sync)."""
+        _check(self.lib.mc_sync(self.ctx), "mc_sync")
 
     def timers(self, reset=False):
         out = np.zeros(2 * len(FAMILIES))

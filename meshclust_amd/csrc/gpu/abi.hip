@@ -936,6 +936,13 @@ int mc_mean_shift_select(mc_ctx *c, const uint32_t *centre_ids, uint32_t C, cons
   return mean_shift_common(c, centre_ids, C, member_off, members, delta, keep, new_centre, 0, C);
 }
 
+int mc_sync(mc_ctx *c) {
+  if (!c) return MC_ERR_ARG;
+  MCG_CHECK(hipSetDevice(c->device));
+  MCG_CHECK(hipDeviceSynchronize());
+  return MC_OK;
+}
+
 int mc_timers(mc_ctx *c, double *ms_out, int n, int reset) {
   if (!c) return MC_ERR_ARG;
   (void)hipStreamSynchronize(c->stream);

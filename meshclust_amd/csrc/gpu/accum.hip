@@ -386,7 +386,7 @@ __device__ __forceinline__ void worker(const AccArgs &A, const DevClassifier &C,
   __shared__ int s_abort;
   constexpr int NC = NCH > 0 ? NCH : 1;
   const uint32_t GW = gridDim.x - 1, w = blockIdx.x - 1;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wv = wave_id();
   const int nch = NCH > 0 ? NCH : A.nch;
   const int rec_words = (int)A.rec_g;
   uint32_t *srec = reinterpret_cast<uint32_t *>(dyn);
@@ -681,7 +681,7 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
   __shared__ uint64_t s_sumF;
   constexpr int NC = NCH > 0 ? NCH : 1;
   const uint32_t GW = gridDim.x - 1;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wv = wave_id();
   const int nch = NCH > 0 ? NCH : A.nch;
   const int rec_words = (int)A.rec_g;
   uint8_t *Fl = reinterpret_cast<uint8_t *>(dyn);  // integer mean row

@@ -51,7 +51,7 @@ __global__ __launch_bounds__(NT) void distance_keys_kernel(HistView H, const uin
                                                            uint16_t *__restrict__ keys, uint32_t ptile) {
   extern __shared__ __attribute__((aligned(16))) uint4 plds[];
   const int nch = (int)((H.B * (int)sizeof(T) + 15) / 16);
-  const int lane = threadIdx.x & 63, group = lane >> 4, lig = lane & 15, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, group = lane >> 4, lig = lane & 15, wave = wave_id();
   const int rows_per_block = 16;  // 4 waves x 4 groups
   for (uint32_t p0 = 0; p0 < npiv; p0 += ptile) {
     const uint32_t pn = min(ptile, npiv - p0);
@@ -206,7 +206,7 @@ __global__ __launch_bounds__(NT) void scan_kernel(HistView H, DevClassifier C, c
       best_p = op;
     }
   }
-  const int w = threadIdx.x >> 6;
+  const int w = wave_id();
   if ((threadIdx.x & 63) == 0) {
     rv[w] = best_v;
     rp[w] = best_p;
@@ -282,7 +282,7 @@ __device__ void mean_closest(const HistView &H, const uint32_t *ids, const uint6
       bi = oi;
     }
   }
-  const int w = threadIdx.x >> 6;
+  const int w = wave_id();
   if ((threadIdx.x & 63) == 0) {
     rd[w] = bd;
     rk[w] = bk;
@@ -412,7 +412,7 @@ __global__ __launch_bounds__(NT) void mean_shift_kernel(HistView H, DevClassifie
     // ordered compaction within the workgroup: wave prefix via ballot, waves in order
     __shared__ uint32_t wcount[NT / 64];
     const uint64_t bal = __ballot(d);
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, w = wave_id();
     if (lane == 0) wcount[w] = (uint32_t)__popcll(bal);
     __syncthreads();
     uint32_t before = cnt;

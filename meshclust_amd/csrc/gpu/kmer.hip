@@ -255,7 +255,7 @@ __global__ __launch_bounds__(KT) void kmer_kernel(KArgs A, bool write) {
   extern __shared__ __attribute__((aligned(16))) uint32_t ltab[];
   __shared__ uint64_t s_max[KW];
   const int B = 1 << (2 * A.k);
-  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wv = wave_id(), lane = threadIdx.x & 63;
   const bool glob = A.gtab != nullptr;
   uint32_t *base = glob ? A.gtab + (uint64_t)blockIdx.x * KW * (uint64_t)B : ltab;  // this workgroup's tables
   uint32_t *mytab = base + (A.shared ? 0 : (size_t)wv * B);

@@ -20,6 +20,12 @@
 
 namespace mcg {
 
+// This wave's index in its workgroup, as a wave-uniform (SGPR) value: threadIdx.x >> 6 is
+// uniform per wave, but the compiler's divergence analysis cannot see that, and everything
+// derived from it (loop bounds, wave roles) would otherwise be computed per lane with
+// exec-mask branches.
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); }
+
 // Kernel families for the device timers (mc_timers): ms and launch count per family.
 enum Family { F_KMER = 0, F_KEYS, F_PAIRS, F_SCAN, F_FINAL, F_MSHIFT, F_NW, F_NFAM };
 

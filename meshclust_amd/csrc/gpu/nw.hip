@@ -310,6 +310,12 @@ int launch_bucket(mc_ctx *c, NWPairs q) {
 // with a barrier in between).  Inside a wave the bottom row moves down by one lane per step
 // with DPP wave_shr:1 (a VALU move, no LDS round trip).
 constexpr int KLAG = 16, RING_C = 64;
+struct GenStep {  // tags of the latency form's step variants
+  static constexpr bool value = true;
+};
+struct SteadyStep {
+  static constexpr bool value = false;
+};
 
 
 template <int R, typename P, int W>
@@ -326,7 +332,7 @@ __global__ __launch_bounds__(64 * W) void nw_mw_kernel(NWPairs q) {
   const int la = (int)(q.aoff[q.ai[p] + 1] - q.aoff[q.ai[p]]);
   const uint8_t *b = q.Bq + q.boff[q.bi[p]];
   const int lb = (int)(q.boff[q.bi[p] + 1] - q.boff[q.bi[p]]);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, gl = threadIdx.x;
+  const int lane = threadIdx.x & 63, w = wave_id(), gl = threadIdx.x;
   const int len1 = la + 1, len2 = lb + 1;
   const int shorter = (len2 < len1 ? len2 : len1) - 1;
   const int lenDiff = len2 > len1 ? len2 - len1 : len1 - len2;
@@ -406,10 +412,15 @@ __global__ __launch_bounds__(64 * W) void nw_mw_kernel(NWPairs q) {
       }
     };
     fetch(1 - lagw);
-    for (int t = 0; t < steps; t++) {
+    const bool row0 = w == 0 && blk == 0;  // lane 0's upper neighbour is GlobAlignE's row 0
+    // One step of this wave.  GEN: the general form (ramp-up / ramp-down: lanes outside
+    // 1 <= j <= lb idle).  Steady state (every lane inside, lb >= 64): no per-lane branches --
+    // lane 0's hand-in is a select and its prefetch a broadcast LDS read of a uniform slot.
+    auto step = [&](int t, auto gen_tag) {
+      constexpr bool GEN = decltype(gen_tag)::value;
       const int j = t - lane - lagw + 1;  // column of this lane at this step
       const int idx = t - lagw;           // lane 0 reads seq2[idx]
-      if (idx >= 0 && (idx & 63) == 0) {
+      if ((!GEN || idx >= 0) && (idx & 63) == 0) {
         bcur = bnext;
         const int nx = idx + 64 + lane;
         bnext = nx < lb ? b[nx] : 0;
@@ -418,26 +429,63 @@ __global__ __launch_bounds__(64 * W) void nw_mw_kernel(NWPairs q) {
       int uM = dpp_shr1(oM), uX = dpp_shr1(oX), uY = dpp_shr1(oY);
       P uMP = dshr<P>(oMP), uXP = dshr<P>(oXP), uYP = dshr<P>(oYP);
       int bc = dpp_shr1(ob);
-      if (lane == 0) {
-        bc = (j >= 1 && j <= lb) ? b0 : 0;
-        if (j >= 1 && j <= lb) {
-          if (w == 0 && blk == 0) {  // row 0: M = X = -inf, Y = -o - j*e, lengths j
-            uM = NINF;
-            uX = NINF;
-            uY = -GO - j * GE;
-            uMP = uXP = uYP = 0;
-          } else {  // bottom row of wave w-1 (or of the previous row block) at column j
-            uM = nM;
-            uX = nX;
-            uY = nY;
-            uMP = nMP;
-            uXP = nXP;
-            uYP = nYP;
+      if constexpr (GEN) {
+        if (lane == 0) {
+          bc = (j >= 1 && j <= lb) ? b0 : 0;
+          if (j >= 1 && j <= lb) {
+            if (row0) {  // row 0: M = X = -inf, Y = -o - j*e, lengths j
+              uM = NINF;
+              uX = NINF;
+              uY = -GO - j * GE;
+              uMP = uXP = uYP = 0;
+            } else {  // bottom row of wave w-1 (or of the previous row block) at column j
+              uM = nM;
+              uX = nX;
+              uY = nY;
+              uMP = nMP;
+              uXP = nXP;
+              uYP = nYP;
+            }
+          }
+        }
+        fetch(j + 1);
+      } else {
+        const bool l0 = lane == 0;
+        bc = l0 ? b0 : bc;
+        const int hM = row0 ? NINF : nM, hX = row0 ? NINF : nX, hY = row0 ? -GO - j * GE : nY;
+        const P hMP = row0 ? (P)0 : nMP, hXP = row0 ? (P)0 : nXP, hYP = row0 ? (P)0 : nYP;
+        uM = l0 ? hM : uM;
+        uX = l0 ? hX : uX;
+        uY = l0 ? hY : uY;
+        uMP = l0 ? hMP : uMP;
+        uXP = l0 ? hXP : uXP;
+        uYP = l0 ? hYP : uYP;
+        const int jn = idx + 2;  // lane 0's next column (uniform)
+        if (w > 0) {
+          const int sl = jn % RING_C;
+          nM = rM[sl][w];
+          nX = rX[sl][w];
+          nY = rY[sl][w];
+          nMP = rMP[sl][w];
+          nXP = rXP[sl][w];
+          nYP = rYP[sl][w];
+        } else if (blk > 0 && jn <= lb) {
+          const int *sb = bnd + 6 * jn;
+          nM = sb[0];
+          nX = sb[1];
+          nY = sb[2];
+          nMP = (P)(uint32_t)sb[3];
+          nXP = (P)(uint32_t)sb[4];
+          nYP = (P)(uint32_t)sb[5];
+          if constexpr (sizeof(P) == 8) {
+            const int *s2 = bnd + 6 * (lb + 1) + 6 * jn;
+            nMP |= (P)(uint32_t)s2[3] << 32;
+            nXP |= (P)(uint32_t)s2[4] << 32;
+            nYP |= (P)(uint32_t)s2[5] << 32;
           }
         }
       }
-      fetch(j + 1);
-      if (j >= 1 && j <= lb) {
+      if (!GEN || (j >= 1 && j <= lb)) {
         int aM = uM, aX = uX;
         P aMP = uMP, aXP = uXP;
         int gM = dM, gX = dX, gY = dY;
@@ -518,7 +566,13 @@ __global__ __launch_bounds__(64 * W) void nw_mw_kernel(NWPairs q) {
         ob = bc;
       }
       if (W > 1 && (t % KLAG) == KLAG - 1) __syncthreads();
-    }
+    };
+    // steady state: lane 63's column >= 1 and lane 0's <= lb, i.e. lagw + 63 <= t < lagw + lb
+    const int ts0 = lb >= 64 ? lagw + 63 : steps, ts1 = lb >= 64 ? lagw + lb : steps;
+    int t = 0;
+    for (; t < ts0; t++) step(t, GenStep{});
+    for (; t < ts1; t++) step(t, SteadyStep{});
+    for (; t < steps; t++) step(t, GenStep{});
     const int fl = la - blk * ROWS - 1;
     if (fl >= 0 && fl < ROWS && gl == fl / R) {
       const int r = fl % R;
