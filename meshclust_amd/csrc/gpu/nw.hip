@@ -571,6 +571,10 @@ __global__ __launch_bounds__(64 * W) void nw_mw_kernel(NWPairs q) {
     const int ts0 = lb >= 64 ? lagw + 63 : steps, ts1 = lb >= 64 ? lagw + lb : steps;
     int t = 0;
     for (; t < ts0; t++) step(t, GenStep{});
+    for (; t + 1 < ts1; t += 2) {  // two steps per trip: the state registers alternate, no copies
+      step(t, SteadyStep{});
+      step(t + 1, SteadyStep{});
+    }
     for (; t < ts1; t++) step(t, SteadyStep{});
     for (; t < steps; t++) step(t, GenStep{});
     const int fl = la - blk * ROWS - 1;
