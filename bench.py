@@ -212,7 +212,7 @@ def main():
         # one launch per clustering = the device-resident accumulation (accum.hip); otherwise
         # one fused scan launch per get_close step (scan.hip)
         device_loop = fam_n["scan"] <= a.steps
-        kname = "accum_kernel<unsigned char>" if device_loop else "fused_scan_kernel<unsigned char>"
+        kname = "accum_kernel<unsigned char" if device_loop else "fused_scan_kernel<unsigned char"
         roof = {"kernel": ("accum_kernel (whole accumulation phase, %d dependent get_close steps per launch)"
                            % s0["scan_steps"]) if device_loop else "fused_scan_kernel (Trainer::get_close step)",
                 "bound": "hbm", "achieved": round(ach, 1),
@@ -222,7 +222,7 @@ def main():
                 "us_per_step": round(fam_ms["scan"] * 1e3 / sum(s["scan_steps"] for s in stats), 2)}
         pmc = os.path.join(ROOT, "profiles", "pmc_latest.json")
         if os.path.exists(pmc):  # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (scripts/pmc_summary.py)
-            e = json.load(open(pmc)).get(kname)
+            e = next((v for k2, v in sorted(json.load(open(pmc)).items()) if k2.startswith(kname)), None)
             if e and "hbm_bytes_per_dispatch" in e:
                 roof["traffic"] = round(e["hbm_bytes_per_dispatch"])
                 roof["traffic_unit"] = "bytes/launch (FETCH_SIZE x2 + WRITE_SIZE, profiles/pmc_latest.json)"
