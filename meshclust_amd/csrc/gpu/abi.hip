@@ -776,13 +776,13 @@ int mc_accumulate(mc_ctx *c, const uint32_t *bin_lo, const uint64_t *bounds, uin
   TRY(upload(c->s_e, bounds, nbins, c->stream));
   TRY(ensure(c->s_f, n * 4 + 16));
   TRY(ensure(c->s_g, (n + 1) * 8 + 16));
-  TRY(ensure(c->acc_out, 128));
-  MCG_CHECK(hipMemsetAsync(c->acc_out.p, 0, 128, c->stream));
+  TRY(ensure(c->acc_out, 256));
+  MCG_CHECK(hipMemsetAsync(c->acc_out.p, 0, 256, c->stream));
   TRY(launch_accum(c, (const uint32_t *)c->s_d.p, (const uint64_t *)c->s_e.p, nbins, sim, (uint32_t *)c->members.p,
                    (uint64_t *)c->member_keys.p, (uint32_t *)c->s_f.p, (uint64_t *)c->s_g.p,
                    (uint64_t *)c->acc_out.p));
-  uint64_t out[16];
-  MCG_CHECK(hipMemcpyAsync(out, c->acc_out.p, 128, hipMemcpyDeviceToHost, c->stream));
+  uint64_t out[32];
+  MCG_CHECK(hipMemcpyAsync(out, c->acc_out.p, 256, hipMemcpyDeviceToHost, c->stream));
   MCG_CHECK(hipStreamSynchronize(c->stream));
   flush_timers(c);
   if (out[3]) {
@@ -821,9 +821,12 @@ int mc_accumulate(mc_ctx *c, const uint32_t *bin_lo, const uint64_t *bounds, uin
   }
   if (getenv("MC_ACCUM_PROFILE")) {
     fprintf(stderr, "[accum] steps %llu window %.3f (centre data %.3f window %.3f record %.3f) wait %.3f collect %.3f "
-            "(stragglers+reduce %.3f column sums %.3f mean %.3f closest %.3f) ms\n",
+            "(stragglers+reduce %.3f column sums %.3f [takes %.3f] mean %.3f closest %.3f) ms\n",
             (unsigned long long)out[1], out[5] / 1e5, out[12] / 1e5, out[13] / 1e5, out[14] / 1e5, out[6] / 1e5,
-            out[7] / 1e5, out[8] / 1e5, out[9] / 1e5, out[10] / 1e5, out[11] / 1e5);
+            out[7] / 1e5, out[8] / 1e5, out[9] / 1e5, out[15] / 1e5, out[10] / 1e5, out[11] / 1e5);
+    if (out[17])  // the controller's shader-clock ticks over its 100 MHz real-time ticks
+      fprintf(stderr, "[accum] controller shader clock %.0f MHz over %.3f ms\n", (double)out[16] / ((double)out[17] / 100.0),
+              out[17] / 1e5);
     if (atoi(getenv("MC_ACCUM_PROFILE")) >= 2 && c->s_h.p) {
       // per step (first 4096; accum.hip trace_mark): record published -> first / last active
       // worker saw it -> first / last scan done -> first / last partial stored -> controller
@@ -831,18 +834,22 @@ int mc_accumulate(mc_ctx *c, const uint32_t *bin_lo, const uint64_t *bounds, uin
       const int TW = 16;
       std::vector<uint64_t> tr(4096 * TW);
       MCG_CHECK(hipMemcpy(tr.data(), c->s_h.p, tr.size() * 8, hipMemcpyDeviceToHost));
-      double a[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, m[5] = {0, 0, 0, 0, 0};
-      uint64_t cnt = 0, nact = 0, mcnt = 0;
+      double a[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, m[6] = {0, 0, 0, 0, 0, 0};
+      uint64_t cnt = 0, nact = 0, mcnt = 0, scnt = 0;
       for (uint64_t st = 1; st < 4096; st++) {  // MC_ACCUM_PROFILE=2: the middle active worker
         const uint64_t *t = &tr[st * TW];
         if (!t[0] || !t[10] || !t[14]) continue;
         for (int i = 0; i < 5; i++) m[i] += (double)(int64_t)(t[10 + i] - t[0]);
+        if (t[15]) {  // (thread 0's own candidate was scanned)
+          m[5] += (double)(int64_t)(t[15] - t[0]);
+          scnt++;
+        }
         mcnt++;
       }
       if (mcnt)
-        fprintf(stderr, "[accum trace] middle worker, avg us after publish: seen %.2f kill-log %.2f wave0-scanned %.2f "
-                "all-scanned %.2f partial %.2f\n", m[0] / mcnt / 100, m[1] / mcnt / 100, m[2] / mcnt / 100,
-                m[3] / mcnt / 100, m[4] / mcnt / 100);
+        fprintf(stderr, "[accum trace] middle worker, avg us after publish: seen %.2f kill-log %.2f wave0-sums %.2f "
+                "wave0-scanned %.2f all-scanned %.2f partial %.2f\n", m[0] / mcnt / 100, m[1] / mcnt / 100,
+                scnt ? m[5] / scnt / 100 : 0.0, m[2] / mcnt / 100, m[3] / mcnt / 100, m[4] / mcnt / 100);
       for (uint64_t st = 1; st < 4096; st++) {
         const uint64_t *t = &tr[st * TW];
         if (!t[0] || !t[7] || !t[8]) continue;

@@ -292,8 +292,8 @@ struct DevBvec {
     return a;
   }
   // kill one static position (bvec::pop / erase / remove_available); any thread, atomics
-  __device__ void kill_one(uint64_t p) { kill_in(p, bin_of(p)); }
-  __device__ void kill_in(uint64_t p, uint64_t b) {  // ... when its bin b is known
+  __device__ __forceinline__ void kill_one(uint64_t p) { kill_in(p, bin_of(p)); }
+  __device__ __forceinline__ void kill_in(uint64_t p, uint64_t b) {  // ... when its bin b is known
     atomicAnd(&bits[p >> 5], ~(1u << (p & 31)));
     atomicSub(&cn[b], 1u);
     for (uint64_t i = b + 1; i <= nb; i += i & (~i + 1)) atomicSub(&fw[i], 1u);
@@ -514,7 +514,7 @@ __device__ __forceinline__ void worker(const AccArgs &A, const DevClassifier &C,
       }
       kcur = kend;
     }
-    uint64_t t_klog = 0;
+    uint64_t t_klog = 0, t_sad = 0;
     if (A.trace && threadIdx.x == 0) t_klog = now();
     // ---- the chunks of the window this worker owns: Trainer::get_close ----------------
     const uint64_t c0 = P_S / NT, c1 = P_E / NT;
@@ -565,6 +565,12 @@ __device__ __forceinline__ void worker(const AccArgs &A, const DevClassifier &C,
         } else {
           for (int k = 0; k < nch; k++) acc.add(rr[(uint64_t)k * NT], clds[k]);
         }
+        if constexpr (sizeof(T) == 1)
+          if (A.trace && threadIdx.x == 0) {  // (profile: the byte sums are done)
+            acc.fold();
+            asm volatile("" ::"v"(acc.sad), "v"(acc.dot));
+            t_sad = now();
+          }
         int d;
         if (li < 2 && C.layout) {
           const PInfo pi = li == 0 ? rinf0 : rinf1;
@@ -632,6 +638,7 @@ __device__ __forceinline__ void worker(const AccArgs &A, const DevClassifier &C,
       tr[10] = t_seen;
       tr[11] = t_klog;
       tr[12] = t_scanned;
+      tr[15] = t_sad;
       tr[13] = now();
     }
     if (threadIdx.x < PART_G) {  // lane j of wave 0 stores granule j
@@ -724,8 +731,9 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
   uint32_t kn = 0;      // kill-log length
   uint32_t kn_pub = 0;  // ... when the last record was published
   uint64_t t_wait = 0, t_coll = 0, t_mark = 0;
+  const uint64_t clk0 = A.prof ? __builtin_amdgcn_s_memtime() : 0, rt0 = A.prof ? now() : 0;
   uint64_t t_sub[4] = {0, 0, 0, 0};  // collect: reduce (stragglers), column sums, mean, closest
-  uint64_t t_ws[4] = {0, 0, 0, 0};   // window: centre window data, window, record, -
+  uint64_t t_ws[4] = {0, 0, 0, 0};   // window: centre window data, window, record; [3] collect's takes
 
   auto finish_cluster = [&]() {
     if (threadIdx.x == 0) {
@@ -1030,6 +1038,7 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
       for (uint64_t i = (threadIdx.x + NT - 64) % NT; i < nflag && i < PLIST; i += NT) take(M + i, s_plist[i]);
       if (M + nflag > A.mrow) drain();  // members past the cache are read back from mem_pos / mkeys
       __syncthreads();
+      if (A.prof && threadIdx.x == 0) t_ws[3] += now() - tq;  // (the takes, inside "column sums")
       // column sums of the cached new members: thread (word w of a row, member slice sl) adds
       // up its 32-bit word over the slice's members, then one LDS atomic per bin and thread
       const uint64_t q0 = M, q1 = M + nflag < A.mrow ? M + nflag : (uint64_t)A.mrow;
@@ -1183,6 +1192,10 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
     A.out[7] = t_coll;
     for (int i = 0; i < 4; i++) A.out[8 + i] = t_sub[i];
     for (int i = 0; i < 4; i++) A.out[12 + i] = t_ws[i];
+    if (A.prof) {
+      A.out[16] = __builtin_amdgcn_s_memtime() - clk0;
+      A.out[17] = now() - rt0;
+    }
   }
 }
 

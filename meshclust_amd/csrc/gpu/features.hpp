@@ -28,18 +28,28 @@ struct Acc;
 
 template <>
 struct Acc<uint8_t> {
-  uint32_t sad = 0, dot = 0;
+  // four independent accumulator chains per sum (one per 32-bit word of a chunk): a row's 64
+  // byte instructions of each kind are four dependent chains of 16, not one of 64
+  uint32_t s4[4] = {0, 0, 0, 0}, d4[4] = {0, 0, 0, 0};
+  uint32_t sad = 0, dot = 0;  // valid after fold() (finish / reduce16 fold themselves)
   __device__ __forceinline__ void add(const uint4 &a, const uint4 &b) {
-    sad = __builtin_amdgcn_sad_u8(a.x, b.x, sad);
-    sad = __builtin_amdgcn_sad_u8(a.y, b.y, sad);
-    sad = __builtin_amdgcn_sad_u8(a.z, b.z, sad);
-    sad = __builtin_amdgcn_sad_u8(a.w, b.w, sad);
-    dot = __builtin_amdgcn_udot4(a.x, b.x, dot, false);
-    dot = __builtin_amdgcn_udot4(a.y, b.y, dot, false);
-    dot = __builtin_amdgcn_udot4(a.z, b.z, dot, false);
-    dot = __builtin_amdgcn_udot4(a.w, b.w, dot, false);
+    s4[0] = __builtin_amdgcn_sad_u8(a.x, b.x, s4[0]);
+    s4[1] = __builtin_amdgcn_sad_u8(a.y, b.y, s4[1]);
+    s4[2] = __builtin_amdgcn_sad_u8(a.z, b.z, s4[2]);
+    s4[3] = __builtin_amdgcn_sad_u8(a.w, b.w, s4[3]);
+    d4[0] = __builtin_amdgcn_udot4(a.x, b.x, d4[0], false);
+    d4[1] = __builtin_amdgcn_udot4(a.y, b.y, d4[1], false);
+    d4[2] = __builtin_amdgcn_udot4(a.z, b.z, d4[2], false);
+    d4[3] = __builtin_amdgcn_udot4(a.w, b.w, d4[3], false);
+  }
+  __device__ __forceinline__ void fold() {
+    sad += (s4[0] + s4[1]) + (s4[2] + s4[3]);
+    dot += (d4[0] + d4[1]) + (d4[2] + d4[3]);
+    s4[0] = s4[1] = s4[2] = s4[3] = 0;
+    d4[0] = d4[1] = d4[2] = d4[3] = 0;
   }
   __device__ __forceinline__ void reduce16() {
+    fold();
 #pragma unroll
     for (int o = 8; o >= 1; o >>= 1) {
       sad += __shfl_xor(sad, o, 64);
@@ -47,10 +57,12 @@ struct Acc<uint8_t> {
     }
   }
   __device__ __forceinline__ PS finish(uint64_t magp, uint64_t magq) const {
+    const uint32_t sa = sad + (s4[0] + s4[1]) + (s4[2] + s4[3]);
+    const uint32_t dt = dot + (d4[0] + d4[1]) + (d4[2] + d4[3]);
     PS s;
-    s.sabs = sad;
-    s.smin = (magp + magq - sad) >> 1;
-    s.sdot = dot;
+    s.sabs = sa;
+    s.smin = (magp + magq - sa) >> 1;
+    s.sdot = dt;
     return s;
   }
 };

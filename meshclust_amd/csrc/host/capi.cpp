@@ -36,7 +36,10 @@ void mcl_view(void *dsv, const uint8_t **codes, const uint64_t **seq_off, const 
   *seg = ds->seg.data();
   *seg_off = ds->seg_off.data();
 }
-const char *mcl_header(void *ds, uint64_t i) { return ((mc::Dataset *)ds)->headers.at(i).c_str(); }
+const char *mcl_header(void *dsv, uint64_t i) {
+  const auto *ds = (mc::Dataset *)dsv;
+  return i < ds->size() ? ds->headers.c_str(i) : nullptr;
+}
 void mcl_free(void *ds) { delete (mc::Dataset *)ds; }
 
 // Error text as a JSON string literal body (quotes, backslashes and control bytes escaped).

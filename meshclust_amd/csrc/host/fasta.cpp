@@ -383,7 +383,14 @@ void parse_fasta_files(const std::vector<std::string> &files, Dataset &ds, int t
       lsum += ck[t].bytes;
     }
     const uint64_t nr = rec0[T], nwords = word0[T];
-    ds.headers.resize(nr);
+    std::vector<uint64_t> hb0(T + 1, ds.headers.blob.size());  // header bytes (+ NUL) per chunk
+    for (int t = 0; t < T; t++) {
+      uint64_t b = 0;
+      for (const auto &rec : ck[t].recs) b += rec.hdr_len + 1;
+      hb0[t + 1] = hb0[t] + b;
+    }
+    ds.headers.blob.resize(hb0[T]);
+    ds.headers.off.resize(nr + 1);
     ds.lengths.resize(nr);
     ds.seq_off.resize(nr + 1);
     ds.pk_off.resize(nr + 1);
@@ -400,11 +407,14 @@ void parse_fasta_files(const std::vector<std::string> &files, Dataset &ds, int t
 #pragma omp parallel for schedule(dynamic, 1) num_threads(threads)
     for (int t = 0; t < T; t++) {
       const Chunk &c = ck[t];
-      uint64_t sg = seg0[t];
+      uint64_t sg = seg0[t], hb = hb0[t];
       for (size_t r = 0; r < c.recs.size(); r++) {
         const auto &rec = c.recs[r];
         const uint64_t id = rec0[t] + r;
-        ds.headers[id].assign(buf + rec.hdr, rec.hdr_len);
+        memcpy(&ds.headers.blob[hb], buf + rec.hdr, rec.hdr_len);
+        hb += rec.hdr_len;
+        ds.headers.blob[hb++] = '\0';
+        ds.headers.off[id + 1] = hb;
         ds.lengths[id] = rec.len;
         ds.seq_off[id + 1] = byte0[t] + rec.off + rec.len;
         ds.pk_off[id + 1] = word0[t] + (r + 1 < c.recs.size() ? c.recs[r + 1].w_off : c.pk.size());
