@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Time bin/meshclust end to end (parse -> .clstr written) on the BASELINE.json configs that
-are not bench.py's line: config C (--align, batched NW) and config E (the
-viral shape, mixed 8-12 kb genomes, k = 6).  One JSON line per run, also written to
+are not bench.py's line: config C (--align, batched NW), config D on one GPU
+(1M reads) and config E (the viral shape, mixed 8-12 kb genomes, k = 6).  One JSON line per run, also written to
 gpurun_out/configs_<name>.json.
 
 usage: configs.py NAME [NAME ...]      names: see CONFIGS below
@@ -32,6 +32,8 @@ CONFIGS = {
             "config E: 7 families x 13 genomes, 8-12 kb, 5-15% within-family mutation, --id 0.80"),
     "E9100": (("families", 70, 130, 8000, 12000, 0.05, 0.15, 61), ["--id", "0.80"], 900,
               "config E scaled: 70 families x 130 genomes, 8-12 kb, --id 0.80"),
+    "D1M": (("reads", 1000000, 1000, 10000, 0.03, 51), ["--id", "0.90"], 900,
+            "config D on one GPU: 1M x 1 kb, 10,000 templates, mut 0.03, --id 0.90"),
 }
 
 
@@ -67,12 +69,20 @@ def run(name, outdir):
                      "sequences_per_s": round(s["n"] / wall, 1),
                      "nw_pairs": s.get("nw_pairs", 0) + s.get("align_nw_pairs", 0), "nw_cells": cells,
                      "nw_cells_per_s_wall": round(cells / wall, 1), "phases_ms": s.get("phases_ms")})
+        if s.get("scan_candidates") and s.get("phases_ms", {}).get("accumulate"):
+            # accumulation scan: algorithmic bytes (B*w + 17 per evaluation) over the phase's wall
+            evb = (4 ** s["k"]) * s["width"] + 17
+            line.update({"scan_evals": s["scan_candidates"], "scan_steps": s.get("scan_steps"),
+                         "accum_scan_gbs": round(s["scan_candidates"] * evb / (s["phases_ms"]["accumulate"] / 1e3) / 1e9, 1)})
         g = os.path.join(ROOT, "tests", "golden", "cfg_%s.clstr.gz" % name)
         if os.path.exists(g):  # reference output on the same input: canonical partition
             import clstr
             line["partition_equals_reference"] = clstr.canonical(out) == clstr.canonical(g)
         os.makedirs(outdir, exist_ok=True)
-        os.replace(out, os.path.join(outdir, "configs_%s.clstr" % name))
+        if s["n"] <= 200000:  # (large outputs are not copied back)
+            os.replace(out, os.path.join(outdir, "configs_%s.clstr" % name))
+        else:
+            os.remove(out)
     else:
         line["stderr"] = r.stderr[-600:]
     print(json.dumps(line), flush=True)
