@@ -831,25 +831,36 @@ int mc_accumulate(mc_ctx *c, const uint32_t *bin_lo, const uint64_t *bounds, uin
       // per step (first 4096; accum.hip trace_mark): record published -> first / last active
       // worker saw it -> first / last scan done -> first / last partial stored -> controller
       // has every partial -> collect done
-      const int TW = 16;
+      const int TW = 20;  // accum.hip TRACE_W
       std::vector<uint64_t> tr(4096 * TW);
       MCG_CHECK(hipMemcpy(tr.data(), c->s_h.p, tr.size() * 8, hipMemcpyDeviceToHost));
-      double a[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, m[6] = {0, 0, 0, 0, 0, 0};
-      uint64_t cnt = 0, nact = 0, mcnt = 0, scnt = 0;
+      double a[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, m[7] = {0, 0, 0, 0, 0, 0, 0};
+      uint64_t cnt = 0, nact = 0, mcnt = 0, scnt = 0, bcnt = 0;
+      double mb[3] = {0, 0, 0};
       for (uint64_t st = 1; st < 4096; st++) {  // MC_ACCUM_PROFILE=2: the middle active worker
         const uint64_t *t = &tr[st * TW];
         if (!t[0] || !t[10] || !t[14]) continue;
         for (int i = 0; i < 5; i++) m[i] += (double)(int64_t)(t[10 + i] - t[0]);
         if (t[15]) {  // (thread 0's own candidate was scanned)
           m[5] += (double)(int64_t)(t[15] - t[0]);
+          m[6] += (double)(int64_t)(t[16] - t[0]);
           scnt++;
+        }
+        if (t[17] && t[18] && t[19]) {
+          mb[0] += (double)(int64_t)(t[17] - t[0]);
+          mb[1] += (double)(int64_t)(t[18] - t[0]);
+          mb[2] += (double)(int64_t)(t[19] - t[0]);
+          bcnt++;
         }
         mcnt++;
       }
       if (mcnt)
-        fprintf(stderr, "[accum trace] middle worker, avg us after publish: seen %.2f kill-log %.2f wave0-sums %.2f "
-                "wave0-scanned %.2f all-scanned %.2f partial %.2f\n", m[0] / mcnt / 100, m[1] / mcnt / 100,
-                scnt ? m[5] / scnt / 100 : 0.0, m[2] / mcnt / 100, m[3] / mcnt / 100, m[4] / mcnt / 100);
+        fprintf(stderr, "[accum trace] middle worker, avg us after publish: seen %.2f kill-log %.2f wave0-top %.2f "
+                "wave0-sums %.2f wave0-scanned %.2f all-scanned %.2f partial %.2f\n", m[0] / mcnt / 100, m[1] / mcnt / 100,
+                scnt ? m[6] / scnt / 100 : 0.0, scnt ? m[5] / scnt / 100 : 0.0, m[2] / mcnt / 100, m[3] / mcnt / 100, m[4] / mcnt / 100);
+      if (bcnt)
+        fprintf(stderr, "[accum trace] middle worker barrier: last wave arrives %.2f, wave 0 leaves %.2f, last wave leaves %.2f\n",
+                mb[0] / bcnt / 100, mb[1] / bcnt / 100, mb[2] / bcnt / 100);
       for (uint64_t st = 1; st < 4096; st++) {
         const uint64_t *t = &tr[st * TW];
         if (!t[0] || !t[7] || !t[8]) continue;

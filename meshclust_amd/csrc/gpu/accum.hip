@@ -52,7 +52,7 @@ constexpr uint32_t NONE = 0xffffffffu;
 constexpr uint64_t NONE64 = ~0ull;
 constexpr uint32_t RING = 64;          // step records kept for workgroups that read them late
 constexpr uint32_t TRACE_STEPS = 4096;
-constexpr int TRACE_W = 16;            // trace words per step (MC_ACCUM_PROFILE=2), see trace_mark
+constexpr int TRACE_W = 20;            // trace words per step (MC_ACCUM_PROFILE=2), see trace_mark
 constexpr int KINL = 4;                // kill-log entries carried inline in a step record
 constexpr int REC_HDR = 14;            // centre, S, E, kn, KINL kills, mag / sumsq / len (2 each)
 constexpr int PART_G = 8;              // granules per partial
@@ -146,6 +146,23 @@ __device__ __forceinline__ void drain() { asm volatile("s_waitcnt vmcnt(0)" ::: 
 __device__ __forceinline__ uint64_t gran(uint32_t tag, uint32_t data) { return ((uint64_t)tag << 32) | data; }
 
 __device__ __forceinline__ uint32_t wave_sum32(uint32_t v) { return wave_sum32_all(v); }
+
+// n / d and n % d for a run-time divisor d (the worker count) and n < 2^22 (chunk indices):
+// float reciprocal, then one correction either way (|error| < 0.5 before truncation), instead
+// of the compiler's 64-bit division sequence.
+struct Div32 {
+  uint32_t d;
+  float inv;
+  __device__ __forceinline__ explicit Div32(uint32_t d_) : d(d_), inv(1.0f / (float)d_) {}
+  __device__ __forceinline__ uint32_t div(uint32_t n) const {
+    uint32_t q = (uint32_t)((float)n * inv);
+    const int32_t r = (int32_t)(n - q * d);
+    if (r < 0) q--;
+    else if ((uint32_t)r >= d) q++;
+    return q;
+  }
+  __device__ __forceinline__ uint32_t mod(uint32_t n) const { return n - div(n) * d; }
+};
 
 __device__ __forceinline__ bool better(double v, uint64_t p, double bv, uint64_t bp) {
   return v > bv || (v == bv && p < bp);
@@ -386,6 +403,7 @@ __device__ __forceinline__ void worker(const AccArgs &A, const DevClassifier &C,
   __shared__ int s_abort;
   constexpr int NC = NCH > 0 ? NCH : 1;
   const uint32_t GW = gridDim.x - 1, w = blockIdx.x - 1;
+  const Div32 dgw(GW);
   const int lane = threadIdx.x & 63, wv = wave_id();
   const int nch = NCH > 0 ? NCH : A.nch;
   const int rec_words = (int)A.rec_g;
@@ -510,22 +528,28 @@ __device__ __forceinline__ void worker(const AccArgs &A, const DevClassifier &C,
       for (uint32_t e = kcur; e < kend; e++) {
         const uint32_t p = e >= kinl0 ? hdr[4 + KINL - (kend - e)] : ld32(A.klog + e);
         const uint64_t ch = p / NT;
-        if (ch % GW == w && (p % NT) == (uint32_t)threadIdx.x) lal[(ch / GW) * NT + threadIdx.x] = 0;
+        if ((p % NT) == (uint32_t)threadIdx.x) {
+          const uint32_t cq = dgw.div((uint32_t)ch);
+          if ((uint32_t)ch - cq * GW == w) lal[(uint64_t)cq * NT + threadIdx.x] = 0;
+        }
       }
       kcur = kend;
     }
-    uint64_t t_klog = 0, t_sad = 0;
+    uint64_t t_klog = 0, t_sad = 0, t_top = 0;
     if (A.trace && threadIdx.x == 0) t_klog = now();
     // ---- the chunks of the window this worker owns: Trainer::get_close ----------------
     const uint64_t c0 = P_S / NT, c1 = P_E / NT;
     const uint32_t nact = (uint32_t)(c1 - c0 + 1 < (uint64_t)GW ? c1 - c0 + 1 : (uint64_t)GW);
-    const uint32_t mine = (w + GW - (uint32_t)(c0 % GW)) % GW;
+    const uint32_t mine = dgw.mod(w + GW - dgw.mod((uint32_t)c0));
     if (mine >= nact) continue;
     if (threadIdx.x == 0) {
       s_nfl = 0;
       s_nscan = 0;
     }
+    uint64_t t_w7 = 0, t_bar = 0;
+    if (A.trace && threadIdx.x == NT - 64) t_w7 = now();  // (profile: the last wave reaches the barrier)
     __syncthreads();
+    if (A.trace && (threadIdx.x == 0 || threadIdx.x == NT - 64)) t_bar = now();
     double best_v = -1.0;
     uint64_t best_p = NONE64;
     uint32_t nscan = 0;
@@ -538,11 +562,12 @@ __device__ __forceinline__ void worker(const AccArgs &A, const DevClassifier &C,
       else st32(A.fpos + base + idx, (uint32_t)pos);
     };
     for (uint64_t ch = c0 + mine; ch <= c1; ch += GW) {
-      const uint64_t li = ch / GW;  // local chunk index
+      const uint64_t li = dgw.div((uint32_t)ch);  // local chunk index
       const uint64_t pos = ch * NT + threadIdx.x;
       uint8_t *la = lal + li * NT + threadIdx.x;
       if (!(pos >= P_S && pos <= P_E && *la)) continue;
       nscan++;
+      if (A.trace && threadIdx.x == 0) t_top = now();
       Acc<T> acc;
       double cv;
       if ((int64_t)li < res) {  // resident rows (LDS)
@@ -579,8 +604,11 @@ __device__ __forceinline__ void worker(const AccArgs &A, const DevClassifier &C,
           {
             double cv2;
             PInfo p2 = pi;
-            p2.len += (uint64_t)(A.budget >> 62);  // 0 at run time, unknown to the compiler
-            const int d2 = classify_std(C, acc.finish(p2.mag, pc.mag), p2, li == 0 ? rterm0 : rterm1, pc, tq, A.B, &cv2);
+            const uint64_t z = (uint64_t)(A.budget >> 62);  // 0 at run time, unknown to the compiler
+            p2.len += z;
+            p2.mag += z;
+            p2.sumsq += z;
+            const int d2 = classify_std(C, acc.finish(p2.mag, pc.mag), p2, pterms(p2.mag, p2.sumsq, A.B), pc, tq, A.B, &cv2);
             d &= d2 | (cv2 == cv ? 1 : 0);
             cv = cv2 > cv ? cv2 : cv;
           }
@@ -639,7 +667,13 @@ __device__ __forceinline__ void worker(const AccArgs &A, const DevClassifier &C,
       tr[11] = t_klog;
       tr[12] = t_scanned;
       tr[15] = t_sad;
+      tr[16] = t_top;
+      tr[18] = t_bar;
       tr[13] = now();
+    }
+    if (A.trace && !A.trace_all && threadIdx.x == NT - 64 && mine == nact / 2 && seen < TRACE_STEPS) {
+      A.trace[(uint64_t)seen * TRACE_W + 17] = t_w7;
+      A.trace[(uint64_t)seen * TRACE_W + 19] = t_bar;
     }
     if (threadIdx.x < PART_G) {  // lane j of wave 0 stores granule j
       double v = s_bv[0];
@@ -950,7 +984,7 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
     uint64_t bp_ = NONE64;
     uint32_t cnt_w = 0, scan_w = 0;
     if (threadIdx.x < nact) {  // (nact <= G - 1 < NT)
-      const uint32_t wk = (uint32_t)((c0 + threadIdx.x) % GW);
+      const uint32_t wk = Div32(GW).mod((uint32_t)c0 + threadIdx.x);
       const uint64_t *q = A.partials + (uint64_t)wk * PART_G;
       const uint64_t t0 = now();
       uint64_t g8[PART_G];
