@@ -11,6 +11,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
+#include <vector>
 
 #include "mcgpu.hpp"
 
@@ -803,14 +805,32 @@ int mc_accumulate(mc_ctx *c, const uint32_t *bin_lo, const uint64_t *bounds, uin
   MCG_CHECK(hipMemcpyAsync(pos.data(), c->members.p, n * 4, hipMemcpyDeviceToHost, c->stream));
   MCG_CHECK(hipMemcpyAsync(keys.data(), c->member_keys.p, n * 8, hipMemcpyDeviceToHost, c->stream));
   MCG_CHECK(hipStreamSynchronize(c->stream));
-  // `current` order: the seed, then each step's flagged candidates in bvec order
-  std::vector<std::pair<uint64_t, uint32_t>> tmp;
-  for (uint64_t k = 0; k < ncl; k++) {
-    const uint64_t a = member_off[k], b = member_off[k + 1];
-    tmp.clear();
-    for (uint64_t i = a; i < b; i++) tmp.emplace_back(keys[i], pos[i]);
-    std::sort(tmp.begin(), tmp.end());
-    for (uint64_t i = a; i < b; i++) member_ids[i] = c->h_order[tmp[i - a].second];
+  // `current` order: the seed, then each step's flagged candidates in bvec order -- each
+  // cluster's members sorted by key, clusters split over a few host threads by member count
+  auto order_clusters = [&](uint64_t k0, uint64_t k1) {
+    std::vector<std::pair<uint64_t, uint32_t>> tmp;
+    for (uint64_t k = k0; k < k1; k++) {
+      const uint64_t a = member_off[k], b = member_off[k + 1];
+      tmp.clear();
+      for (uint64_t i = a; i < b; i++) tmp.emplace_back(keys[i], pos[i]);
+      std::sort(tmp.begin(), tmp.end());
+      for (uint64_t i = a; i < b; i++) member_ids[i] = c->h_order[tmp[i - a].second];
+    }
+  };
+  {
+    const unsigned T = n >= 65536 ? std::min(8u, std::max(1u, std::thread::hardware_concurrency())) : 1u;
+    std::vector<uint64_t> cut(T + 1, ncl);
+    cut[0] = 0;
+    for (unsigned t = 1; t < T; t++) {  // first cluster whose members start at or after t/T of n
+      const uint64_t want = n * t / T;
+      cut[t] = (uint64_t)(std::lower_bound(member_off, member_off + ncl + 1, want) - member_off);
+      if (cut[t] > ncl) cut[t] = ncl;
+      if (cut[t] < cut[t - 1]) cut[t] = cut[t - 1];
+    }
+    std::vector<std::thread> th;
+    for (unsigned t = 1; t < T; t++) th.emplace_back(order_clusters, cut[t], cut[t + 1]);
+    order_clusters(cut[0], cut[1]);
+    for (auto &x : th) x.join();
   }
   for (uint64_t k = 0; k < ncl; k++) centre_ids[k] = c->h_order[centre_ids[k]];  // static positions -> ids
   *nclusters = ncl;
