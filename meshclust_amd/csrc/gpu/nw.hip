@@ -656,7 +656,11 @@ int launch_nw(mc_ctx *c, const uint8_t *d_A, const uint64_t *d_aoff, const uint3
   // bucket pairs by rows per lane and payload width; boundary scratch for multi-block pairs.
   // Few pairs (fewer than the chip's SIMDs) are latency-bound: one multi-wave workgroup per pair;
   // many pairs: one wavefront per pair.
-  const bool mw = m < 1024;
+  static const uint64_t mw_max = [] {  // MC_NW_MW_MAX: largest batch for the latency form
+    const char *e = getenv("MC_NW_MW_MAX");
+    return e ? (uint64_t)atoll(e) : (uint64_t)1024;
+  }();
+  const bool mw = m < mw_max;
   enum { NB = 24 };  // latency form: (R, payload) x waves 4 / 8 / 16
   int bucket_waves[NB] = {0};
   std::vector<uint32_t> bucket[NB];

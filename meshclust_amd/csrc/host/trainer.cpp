@@ -155,8 +155,20 @@ std::vector<PairId> Trainer::split() {
     for (size_t i = 0; i < P; i++) sorted.emplace_back(std::move(w[i]));
   }
   auto pt_at = [&](size_t i, size_t pos) { return (uint32_t)sorted[i].at((int64_t)pos); };
-  // binary search with alignment (:703-721): the 150 dependent chains advance together, one
-  // batched NW launch per step.
+  // binary search with alignment (:703-721): the 150 dependent chains advance together.  Each
+  // round aligns, for every active chain, the next `look` levels of its decision tree at once
+  // (the current pivot, both positions the next comparison can move to, ...: 2^look - 1 pairs
+  // per chain), then walks the tree with the identities: the same decisions as one level per
+  // round -- the same pivots -- in ceil(levels / look) dependent rounds instead of one per
+  // level.  The alignments of the branches not taken are extra work (counted in nw_cells).
+  // Two levels per round measured fastest at config B (9 rounds of 450 pairs in the latency
+  // form: 8.3 ms of NW, training 21.8 ms vs 25.1 ms with one level; three levels are 1,050-pair
+  // rounds whose extra pairs cost more than the rounds they save); MC_NW_LOOKAHEAD = 1..4.
+  const int look = [] {
+    const char *e = getenv("MC_NW_LOOKAHEAD");
+    const int v = e ? atoi(e) : 2;
+    return v < 1 ? 1 : v > 4 ? 4 : v;
+  }();
   std::vector<size_t> offset(P, N / 4), pivot(P, 2 * (N / 4));
   std::vector<char> active(P, 1);
   // Sampler positions of the current pivot estimate (the loops of :732-755 below).
@@ -168,29 +180,72 @@ std::vector<PairId> Trainer::split() {
     for (int t = 0; t < (int)to_add_each && std::round(as) < (double)npts; t++, as += after_inc)
       out.push_back((size_t)(int)std::round(as));
   };
+  // the decision tree of chain state (p, o) to depth d, breadth first: node n's children are
+  // 2n+1 (identity below the cutoff: p - o) and 2n+2 (above: p + o), each with offset o / 2;
+  // a node whose offset is 0 is not aligned (the chain stops there, as `gather` drops it)
+  auto tree = [&](size_t p, size_t o, int d, std::vector<size_t> &pos, std::vector<char> &live) {
+    const size_t nn = ((size_t)1 << d) - 1;
+    pos.assign(nn, 0);
+    live.assign(nn, 0);
+    std::vector<size_t> off(nn, 0);
+    pos[0] = p;
+    off[0] = o;
+    live[0] = o > 0;
+    for (size_t n = 0; 2 * n + 2 < nn; n++) {
+      if (!live[n]) continue;
+      const size_t oc = off[n] / 2;
+      pos[2 * n + 1] = pos[n] - off[n];
+      pos[2 * n + 2] = pos[n] + off[n];
+      off[2 * n + 1] = off[2 * n + 2] = oc;
+      live[2 * n + 1] = live[2 * n + 2] = oc > 0;
+    }
+  };
   {
     Scope s(timer_, "train.nw_search");
     std::vector<PairId> batch;
-    std::vector<size_t> who;
+    std::vector<size_t> who, first;  // chain of each batch entry's tree; first entry of each chain
+    std::vector<std::vector<size_t>> tpos(P);
+    std::vector<std::vector<char>> tlive(P);
     auto gather = [&]() {
       who.clear();
       for (size_t i = 0; i < P; i++) {
         if (active[i] && offset[i] == 0) active[i] = 0;
         if (active[i]) who.push_back(i);
       }
-      batch.resize(who.size());
+    };
+    auto build_batch = [&](bool parallel) {
+      first.assign(who.size() + 1, 0);
+      for (size_t t = 0; t < who.size(); t++) {
+        tree(pivot[who[t]], offset[who[t]], look, tpos[who[t]], tlive[who[t]]);
+        size_t m = 0;
+        for (char l : tlive[who[t]]) m += l != 0;
+        first[t + 1] = first[t] + m;
+      }
+      batch.resize(first[who.size()]);
+      auto fill = [&](size_t t) {
+        const size_t i = who[t];
+        size_t q = first[t];
+        for (size_t n = 0; n < tpos[i].size(); n++)
+          if (tlive[i][n]) batch[q++] = PairId(indices[i], pt_at(i, tpos[i][n]));
+      };
+      if (parallel) {
+#pragma omp parallel for schedule(dynamic) num_threads(cfg_.threads)
+        for (size_t t = 0; t < who.size(); t++) fill(t);
+      } else {
+        for (size_t t = 0; t < who.size(); t++) fill(t);
+      }
     };
     gather();
     {
       Scope s2(timer_, "train.nw_search.resolve");
-#pragma omp parallel for schedule(dynamic) num_threads(cfg_.threads)
-      for (size_t t = 0; t < who.size(); t++) batch[t] = PairId(indices[who[t]], pt_at(who[t], pivot[who[t]]));
+      build_batch(true);
     }
     while (!batch.empty()) {
-      // The GPU aligns this round's pairs while the host resolves, in every chain, both
-      // positions the next round can probe (pivot -/+ offset), or in a chain's last round the
-      // sampler's positions around the final pivot: the lazy sorts' partitions are then ready
-      // when the identities come back.  Each LazyIntroSort is touched by one host thread only.
+      // The GPU aligns this round's trees while the host resolves, in every chain, the positions
+      // of every tree the next round can start from (or, for a chain that ends within this
+      // round, the sampler's positions around each pivot it can end on): the lazy sorts'
+      // partitions are then ready when the identities come back.  Each LazyIntroSort is touched
+      // by one host thread only.
       std::vector<double> al;
       // An error of the GPU thread (mc::Error from check()) must not escape the std::thread
       // (std::terminate would end the host process): it is carried out and rethrown here.
@@ -208,12 +263,31 @@ std::vector<PairId> Trainer::split() {
 #pragma omp parallel for schedule(dynamic) num_threads(std::max(1, cfg_.threads - 1))
         for (size_t t = 0; t < who.size(); t++) {
           const size_t i = who[t];
-          std::vector<size_t> pos;
-          if (offset[i] / 2 > 0) {
-            pos.push_back(pivot[i] - offset[i]);
-            pos.push_back(pivot[i] + offset[i]);
-          } else {  // last round: the final pivot is pivot-1, pivot or pivot+1
-            sample_positions(i, pivot[i], pos);
+          // the states the walk can end in: below the live nodes of the last level (or where
+          // a node's offset reaches 0), each the root of the next round's tree
+          std::vector<size_t> pos, tp;
+          std::vector<char> tl;
+          const std::vector<size_t> &np = tpos[i];
+          const std::vector<char> &nl = tlive[i];
+          const size_t nn = np.size(), inner = nn / 2;  // nodes of the last level: inner .. nn-1
+          for (size_t n = 0; n < nn; n++) {
+            if (!nl[n]) continue;
+            const bool last_level = n >= inner || !nl[2 * n + 1];
+            if (!last_level) continue;
+            // offset of node n: o >> depth(n)
+            size_t depth = 0;
+            for (size_t x = n; x > 0; x = (x - 1) / 2) depth++;
+            const size_t on = offset[i] >> depth, oc = on / 2;
+            for (int side = 0; side < 2; side++) {
+              const size_t pc = side ? np[n] + on : np[n] - on;
+              if (oc > 0) {
+                tree(pc, oc, look, tp, tl);
+                for (size_t m = 0; m < tp.size(); m++)
+                  if (tl[m]) pos.push_back(tp[m]);
+              } else {
+                sample_positions(i, pc, pos);
+              }
+            }
           }
           for (size_t q : pos)
             if (q < sorted[i].size()) pt_at(i, q);
@@ -228,18 +302,32 @@ std::vector<PairId> Trainer::split() {
       if (gpu_err) std::rethrow_exception(gpu_err);
       if (spec_err) std::rethrow_exception(spec_err);
       for (size_t t = 0; t < who.size(); t++) {
-        size_t i = who[t];
-        double algn = al[t];
-        if (algn < cfg_.cutoff) pivot[i] -= offset[i];
-        else if (algn > cfg_.cutoff) pivot[i] += offset[i];
-        else { active[i] = 0; continue; }
-        offset[i] /= 2;
+        const size_t i = who[t];
+        // the aligned nodes of this chain's tree, in batch order
+        size_t q = first[t], n = 0;
+        std::vector<double> val(tpos[i].size(), 0.0);
+        for (size_t m = 0; m < tpos[i].size(); m++)
+          if (tlive[i][m]) val[m] = al[q++];
+        for (int d = 0; d < look && active[i]; d++) {
+          const double algn = val[n];
+          if (algn < cfg_.cutoff) {
+            pivot[i] -= offset[i];
+            n = 2 * n + 1;
+          } else if (algn > cfg_.cutoff) {
+            pivot[i] += offset[i];
+            n = 2 * n + 2;
+          } else {
+            active[i] = 0;
+            break;
+          }
+          offset[i] /= 2;
+          if (offset[i] == 0) break;  // (gather drops the chain)
+        }
       }
       gather();
-      // The new pivots are pivot -/+ offset, both resolved by the speculation above: these are
-      // plain lookups, and waking a thread team for them cost more than the lookups themselves.
+      // The new trees were resolved by the speculation above: plain lookups.
       Scope s2(timer_, "train.nw_search.resolve");
-      for (size_t t = 0; t < who.size(); t++) batch[t] = PairId(indices[who[t]], pt_at(who[t], pivot[who[t]]));
+      build_batch(false);
     }
   }
   int aerr = 0;
