@@ -94,7 +94,9 @@ struct AccArgs {
   // hand-off
   uint64_t *ring;  // RING records of rec_g granules
   uint32_t rec_g;
-  uint32_t *klog;      // static positions killed by the controller (pop / erase), append-only
+  uint64_t *klog;      // static positions killed by the controller (pop / erase), append-only,
+                       // entry e a granule tagged e + 1 (a reader checks the tag: no drain
+                       // is needed before the step record that counts it)
   uint32_t *go;        // latest published step (for a workgroup that fell RING steps behind)
   uint64_t *partials;  // G * PART_G granules
   uint32_t *fpos;      // worker w's flagged positions beyond the INL inline ones, at w * fcap
@@ -501,7 +503,7 @@ __device__ __forceinline__ void worker(const AccArgs &A, const DevClassifier &C,
         // else: that slot is being rewritten for a later step: read `go` again
       }
       if (lane == 0) {
-        s_abort = state == 2;
+        if (state == 2) s_abort = 1;
         s_go = got;
       }
     }
@@ -525,8 +527,23 @@ __device__ __forceinline__ void worker(const AccArgs &A, const DevClassifier &C,
     // flags of the positions it owns (offset = its thread index), so no barrier is needed
     {
       const uint32_t kinl0 = kend > (uint32_t)KINL ? kend - KINL : 0;
+      const uint64_t t0k = kinl0 > kcur ? now() : 0;
       for (uint32_t e = kcur; e < kend; e++) {
-        const uint32_t p = e >= kinl0 ? hdr[4 + KINL - (kend - e)] : ld32(A.klog + e);
+        uint32_t p;
+        if (e >= kinl0) {
+          p = hdr[4 + KINL - (kend - e)];
+        } else {  // older than the record's inline entries: the tagged log entry
+          uint64_t g = ld64(A.klog + e);
+          for (uint32_t it = 1; (uint32_t)(g >> 32) != e + 1; it++) {
+            if ((it & 255) == 0 && timed_out(A, t0k)) {
+              s_abort = 1;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            g = ld64(A.klog + e);
+          }
+          p = (uint32_t)g;
+        }
         const uint64_t ch = p / NT;
         if ((p % NT) == (uint32_t)threadIdx.x) {
           const uint32_t cq = dgw.div((uint32_t)ch);
@@ -763,7 +780,6 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
   uint32_t step = 0;
   uint64_t err = 0;
   uint32_t kn = 0;      // kill-log length
-  uint32_t kn_pub = 0;  // ... when the last record was published
   uint64_t t_wait = 0, t_coll = 0, t_mark = 0;
   const uint64_t clk0 = A.prof ? __builtin_amdgcn_s_memtime() : 0, rt0 = A.prof ? now() : 0;
   uint64_t t_sub[4] = {0, 0, 0, 0};  // collect: reduce (stragglers), column sums, mean, closest
@@ -802,7 +818,7 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
     __syncthreads();
   };
   auto log_kill = [&](uint64_t p) {  // thread 0: a pop / erase, for the workers
-    st32(A.klog + kn, (uint32_t)p);
+    st64(A.klog + kn, gran(kn + 1, (uint32_t)p));
     s_klast[kn % KINL] = (uint32_t)p;
   };
   auto pop = [&]() -> uint64_t {  // bvec::pop (bvec.cpp:26-37): static position or ~0
@@ -959,13 +975,13 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
     // step; the kill-log entries are drained first (a late reader finds them there)
     if (wv == 0) {
       uint64_t *r = A.ring + (uint64_t)(step % RING) * A.rec_g;
-      if (kn != kn_pub) drain();  // kill-log entries written since the last record
+      // (kill-log entries are tagged granules: a worker that needs one checks its tag, so the
+      // record is not held back until they land)
       for (int j = lane; j < rec_words; j += 64) st64(r + j, gran(step, rec_word(j, have, S, E)));
       // `go` is only a hint for a worker that fell RING steps behind: it re-validates the
       // record's tags after reading it
       if (lane == 0) st32(A.go, step);
     }
-    kn_pub = kn;
     if (A.prof && threadIdx.x == 0) {
       const uint64_t t = now();
       t_ws[2] += t - t_mark;
@@ -1345,7 +1361,7 @@ int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, 
   const size_t part_bytes = ((size_t)GW * PART_G * 8 + 255) / 256 * 256;
   const size_t bits_bytes = pl.gbits ? ((c->norder + 31) / 32 * 4 + 255) / 256 * 256 : 0;
   const size_t fpos_bytes = ((size_t)GW * fcap * 4 + 255) / 256 * 256;
-  const size_t klog_bytes = (c->norder * 4 + 16 + 255) / 256 * 256;
+  const size_t klog_bytes = (c->norder * 8 + 16 + 255) / 256 * 256;
   if (ensure(c->s_a, ring_bytes) || ensure(c->s_b, part_bytes + bits_bytes) ||
       ensure(c->s_c, fpos_bytes + klog_bytes))
     return MC_ERR_OOM;
@@ -1388,7 +1404,7 @@ int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, 
   A.partials = (uint64_t *)c->s_b.p;
   char *sc = (char *)c->s_c.p;
   A.fpos = (uint32_t *)sc;
-  A.klog = (uint32_t *)(sc + fpos_bytes);
+  A.klog = (uint64_t *)(sc + fpos_bytes);
   A.fcap = fcap;
   A.res = pl.res;
   A.mrow = pl.mrow;

@@ -34,3 +34,18 @@ def test_e2e_byte_identical(harness, name, tmp_path):
     with gzip.open(fixtures.golden("e2e_%s.clstr.gz" % name), "rb") as f:
         want = f.read()
     assert out.read_bytes() == want
+
+
+@pytest.mark.parametrize("look", ["1", "3"])
+@pytest.mark.parametrize("name", ["a1k", "m2k_id80", "fam2k_id85"])
+def test_e2e_nw_lookahead_depth(harness, name, look, tmp_path):
+    """Trainer::split's binary search aligns MC_NW_LOOKAHEAD levels of every chain's decision
+    tree per dependent round (default 2): one level (the reference's order) and three give the
+    same pivots, so the same .clstr (Trainer.cpp:703-721)."""
+    fa, flags = fixtures.e2e_input(name, tmp_path)
+    out = tmp_path / (name + ".clstr")
+    r = subprocess.run([harness, fa] + flags + ["--output", str(out), "--quiet"], capture_output=True, text=True,
+                       timeout=900, env=dict(os.environ, MC_NW_LOOKAHEAD=look))
+    assert r.returncode == 0, r.stderr[-2000:]
+    with gzip.open(fixtures.golden("e2e_%s.clstr.gz" % name), "rb") as f:
+        assert out.read_bytes() == f.read()
