@@ -4,6 +4,7 @@
 #include "lazysort.hpp"
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <exception>
@@ -129,7 +130,7 @@ std::vector<PairId> Trainer::split() {
   if (cfg_.verbose) printf("Point pairs: %zu\n", indices.size());
   const size_t to_add_each = cfg_.max_pts_from_one / 2;
   const size_t P = indices.size();
-  // every pivot's distance to every point: one GPU launch.  Each pivot's std::sort runs on
+  // every pivot's distance to every point on the GPU (in chunks, below).  Each pivot's std::sort runs on
   // (key << 32 | id) words with a comparator that looks only at the key: the comparison
   // outcomes -- and so the permutation -- are those of sorting ids by keys[id].
   // std::sort(pts, by distance to pivot i) is evaluated lazily (lazysort.hpp): only the
@@ -138,29 +139,8 @@ std::vector<PairId> Trainer::split() {
   std::vector<uint16_t> keys(P * N);
   std::vector<LazyIntroSort> sorted;
   sorted.reserve(P);
-  {
-    Scope s(timer_, "train.sort_keys");
-    {
-      Scope s3(timer_, "train.sort_keys.pivots_dev");
-      check(mc_distance_keys(ctx_, indices.data(), (uint32_t)P, all_ids.data(), N, keys.data()), "mc_distance_keys");
-    }
-    Scope s4(timer_, "train.sort_keys.build");
-    std::vector<std::vector<uint64_t>> w(P);
-#pragma omp parallel for schedule(dynamic) num_threads(cfg_.threads)
-    for (size_t i = 0; i < P; i++) {
-      const uint16_t *kk = &keys[i * N];
-      w[i].resize(N);
-      for (size_t t = 0; t < N; t++) w[i][t] = ((uint64_t)kk[points[t]] << 32) | points[t];
-    }
-    for (size_t i = 0; i < P; i++) sorted.emplace_back(std::move(w[i]));
-  }
+  for (size_t i = 0; i < P; i++) sorted.emplace_back(std::vector<uint64_t>{});  // filled below
   auto pt_at = [&](size_t i, size_t pos) { return (uint32_t)sorted[i].at((int64_t)pos); };
-  // binary search with alignment (:703-721): the 150 dependent chains advance together.  Each
-  // round aligns, for every active chain, the next `look` levels of its decision tree at once
-  // (the current pivot, both positions the next comparison can move to, ...: 2^look - 1 pairs
-  // per chain), then walks the tree with the identities: the same decisions as one level per
-  // round -- the same pivots -- in ceil(levels / look) dependent rounds instead of one per
-  // level.  The alignments of the branches not taken are extra work (counted in nw_cells).
   // Two levels per round measured fastest at config B (9 rounds of 450 pairs in the latency
   // form: 8.3 ms of NW, training 21.8 ms vs 25.1 ms with one level; three levels are 1,050-pair
   // rounds whose extra pairs cost more than the rounds they save); MC_NW_LOOKAHEAD = 1..4.
@@ -169,17 +149,6 @@ std::vector<PairId> Trainer::split() {
     const int v = e ? atoi(e) : 2;
     return v < 1 ? 1 : v > 4 ? 4 : v;
   }();
-  std::vector<size_t> offset(P, N / 4), pivot(P, 2 * (N / 4));
-  std::vector<char> active(P, 1);
-  // Sampler positions of the current pivot estimate (the loops of :732-755 below).
-  auto sample_positions = [&](size_t i, size_t pv, std::vector<size_t> &out) {
-    const size_t npts = sorted[i].size();
-    double before_inc = (double)pv / to_add_each, after_inc = ((double)(npts - pv)) / to_add_each;
-    double bs = 0, as = (double)pv;
-    for (int t = 0; t < (int)to_add_each; t++, bs += before_inc) out.push_back((size_t)(int)std::round(bs));
-    for (int t = 0; t < (int)to_add_each && std::round(as) < (double)npts; t++, as += after_inc)
-      out.push_back((size_t)(int)std::round(as));
-  };
   // the decision tree of chain state (p, o) to depth d, breadth first: node n's children are
   // 2n+1 (identity below the cutoff: p - o) and 2n+2 (above: p + o), each with offset o / 2;
   // a node whose offset is 0 is not aligned (the chain stops there, as `gather` drops it)
@@ -199,6 +168,67 @@ std::vector<PairId> Trainer::split() {
       off[2 * n + 1] = off[2 * n + 2] = oc;
       live[2 * n + 1] = live[2 * n + 2] = oc > 0;
     }
+  };
+  {
+    // Pipelined over chunks of pivots: a host thread drives the GPU (keys of chunk c + 1 and
+    // their copy home) while the OpenMP team builds chunk c's (key << 32 | id) words and lazy
+    // sorts and resolves the positions of the first round's decision tree (every chain starts
+    // at the same state, so the same positions).
+    Scope s(timer_, "train.sort_keys");
+    Scope s3(timer_, "train.sort_keys.pivots");
+    std::vector<size_t> pos0;
+    std::vector<char> live0;
+    tree(2 * (N / 4), N / 4, look, pos0, live0);
+    const size_t Q = std::max<size_t>(1, (P + 3) / 4);  // pivots per chunk
+    const size_t nchunk = (P + Q - 1) / Q;
+    std::atomic<size_t> ready{0};
+    std::exception_ptr key_err;
+    std::thread gpu([&]() {
+      try {
+        for (size_t c = 0; c < nchunk; c++) {
+          const size_t c0 = c * Q, n = std::min(Q, P - c0);
+          check(mc_distance_keys(ctx_, indices.data() + c0, (uint32_t)n, all_ids.data(), N, keys.data() + c0 * N),
+                "mc_distance_keys");
+          ready.store(c + 1, std::memory_order_release);
+        }
+      } catch (...) {
+        key_err = std::current_exception();
+        ready.store(nchunk + 1, std::memory_order_release);  // (wakes the consumer)
+      }
+    });
+    for (size_t c = 0; c < nchunk; c++) {
+      while (ready.load(std::memory_order_acquire) <= c) std::this_thread::yield();
+      if (ready.load(std::memory_order_acquire) > nchunk) break;  // the GPU thread failed
+      const size_t c0 = c * Q, c1 = std::min(P, c0 + Q);
+#pragma omp parallel for schedule(dynamic) num_threads(cfg_.threads)
+      for (size_t i = c0; i < c1; i++) {
+        const uint16_t *kk = &keys[i * N];
+        std::vector<uint64_t> w(N);
+        for (size_t t = 0; t < N; t++) w[t] = ((uint64_t)kk[points[t]] << 32) | points[t];
+        sorted[i] = LazyIntroSort(std::move(w));
+        for (size_t n = 0; n < pos0.size(); n++)
+          if (live0[n] && pos0[n] < N) pt_at(i, pos0[n]);
+      }
+    }
+    gpu.join();
+    if (key_err) std::rethrow_exception(key_err);
+  }
+  // binary search with alignment (:703-721): the 150 dependent chains advance together.  Each
+  // round aligns, for every active chain, the next `look` levels of its decision tree at once
+  // (the current pivot, both positions the next comparison can move to, ...: 2^look - 1 pairs
+  // per chain), then walks the tree with the identities: the same decisions as one level per
+  // round -- the same pivots -- in ceil(levels / look) dependent rounds instead of one per
+  // level.  The alignments of the branches not taken are extra work (counted in nw_cells).
+  std::vector<size_t> offset(P, N / 4), pivot(P, 2 * (N / 4));
+  std::vector<char> active(P, 1);
+  // Sampler positions of the current pivot estimate (the loops of :732-755 below).
+  auto sample_positions = [&](size_t i, size_t pv, std::vector<size_t> &out) {
+    const size_t npts = sorted[i].size();
+    double before_inc = (double)pv / to_add_each, after_inc = ((double)(npts - pv)) / to_add_each;
+    double bs = 0, as = (double)pv;
+    for (int t = 0; t < (int)to_add_each; t++, bs += before_inc) out.push_back((size_t)(int)std::round(bs));
+    for (int t = 0; t < (int)to_add_each && std::round(as) < (double)npts; t++, as += after_inc)
+      out.push_back((size_t)(int)std::round(as));
   };
   {
     Scope s(timer_, "train.nw_search");
