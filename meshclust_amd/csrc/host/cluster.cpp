@@ -1,7 +1,11 @@
 // cluster.cpp -- see cluster.hpp.
 #include "cluster.hpp"
 
+#include <fcntl.h>
+#include <unistd.h>
+
 #include <algorithm>
+#include <cerrno>
 #include <cfloat>
 #include <cstdio>
 #include <cstdlib>
@@ -458,8 +462,8 @@ inline void put_uint(std::string &o, unsigned long long v) {
 // "i\t{len}nt, {header}... " per member with '*' after the centre.  Clusters are formatted
 // into per-thread buffers in parallel and written in order.
 void write_clstr(const std::string &path, const Dataset &ds, const std::vector<Center> &part, int threads) {
-  FILE *f = fopen(path.c_str(), "w");
-  if (!f) throw Error("cannot open output " + path, 1);
+  const int fd = open(path.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+  if (fd < 0) throw Error("cannot open output " + path, 1);
   const size_t C = part.size();
   std::vector<int> label(C, -1);
   int counter = 0;
@@ -467,33 +471,55 @@ void write_clstr(const std::string &path, const Dataset &ds, const std::vector<C
     if (!part[c].points.empty()) label[c] = counter++;
   const int T = std::max(1, std::min<int>(threads, (int)(C / 64) + 1));
   std::vector<std::string> out(T);
-#pragma omp parallel for schedule(static, 1) num_threads(T)
-  for (int t = 0; t < T; t++) {
-    std::string &o = out[t];
-    const size_t c0 = C * t / T, c1 = C * (t + 1) / T;
-    for (size_t c = c0; c < c1; c++) {
-      const auto &cen = part[c];
-      if (cen.points.empty()) continue;
-      o += ">Cluster ";
-      put_uint(o, (unsigned long long)label[c]);
-      o += '\n';
-      unsigned long long pt = 0;
-      for (uint32_t p : cen.points) {
-        put_uint(o, pt++);
-        o += '\t';
-        put_uint(o, (unsigned long long)ds.lengths[p]);
-        o += "nt, ";
-        o += ds.headers[p];
-        o += "... ";
-        if (p == cen.centre) o += '*';
+  std::vector<uint64_t> at(T + 1, 0);
+  bool ok = true;
+#pragma omp parallel num_threads(T)
+  {
+#pragma omp for schedule(static, 1)
+    for (int t = 0; t < T; t++) {
+      std::string &o = out[t];
+      const size_t c0 = C * t / T, c1 = C * (t + 1) / T;
+      size_t est = 0;
+      for (size_t c = c0; c < c1; c++) est += 24 + part[c].points.size() * 48;
+      o.reserve(est);
+      for (size_t c = c0; c < c1; c++) {
+        const auto &cen = part[c];
+        if (cen.points.empty()) continue;
+        o += ">Cluster ";
+        put_uint(o, (unsigned long long)label[c]);
         o += '\n';
+        unsigned long long pt = 0;
+        for (uint32_t p : cen.points) {
+          put_uint(o, pt++);
+          o += '\t';
+          put_uint(o, (unsigned long long)ds.lengths[p]);
+          o += "nt, ";
+          o += ds.headers[p];
+          o += "... ";
+          if (p == cen.centre) o += '*';
+          o += '\n';
+        }
+      }
+    }
+#pragma omp single
+    for (int t = 0; t < T; t++) at[t + 1] = at[t] + out[t].size();
+    // every part written at its offset by its own thread (parallel copies into the page cache)
+#pragma omp for schedule(static, 1) reduction(&& : ok)
+    for (int t = 0; t < T; t++) {
+      const char *d = out[t].data();
+      size_t off = 0;
+      while (off < out[t].size()) {
+        const ssize_t r = pwrite(fd, d + off, out[t].size() - off, (off_t)(at[t] + off));
+        if (r < 0 && errno == EINTR) continue;
+        if (r <= 0) {
+          ok = false;
+          break;
+        }
+        off += (size_t)r;
       }
     }
   }
-  bool ok = true;
-  for (const auto &o : out)
-    if (!o.empty()) ok &= fwrite(o.data(), 1, o.size(), f) == o.size();
-  ok &= fclose(f) == 0;
+  ok &= close(fd) == 0;
   if (!ok) throw Error("cannot write output " + path, 1);
 }
 
