@@ -376,6 +376,7 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
         throw Error("centre all-gather across ranks failed", 1);
       std::copy(all.begin(), all.begin() + C, newc.begin());
     } else if (C && !memo) {
+      Scope sm(timer, "update.mean_shift");
       check(mc_mean_shift(ctx, cids.data(), C, off.data(), members.data(), cfg.delta, newc.data()), "mc_mean_shift");
     } else if (C) {
       // Trainer::filter(center clone, good): feat->compute(*member, *clone) (Trainer.cpp:334-349)
@@ -420,6 +421,7 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
     std::vector<uint8_t> sim(pa.size(), 0);
     std::vector<double> c0(pa.size(), 0.0);
     if (!pa.empty() && !memo) {
+      Scope sm(timer, "update.merge_pairs");
       check(mc_classify_pairs(ctx, pa.data(), pb.data(), pa.size(), sim.data(), c0.data(), nullptr), "mc_classify_pairs");
     } else if (!pa.empty()) {  // both centres are clones: only memoised pairs can be similar
       std::vector<double> val;
@@ -441,6 +443,7 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
         c0[idx[r]] = c2[r];
       }
     }
+    Scope sc(timer, "update.cascade");
     merge_cascade(part, poff, sim, c0);
   }
   return part;
