@@ -107,9 +107,34 @@ static double decision_threshold() {
 }
 
 template <typename T>
-static int upload(Buf &b, const T *h, size_t count, hipStream_t s) {
-  if (int rc = ensure(b, count * sizeof(T) + 16)) return rc;
-  if (count) MCG_CHECK(hipMemcpyAsync(b.p, h, count * sizeof(T), hipMemcpyHostToDevice, s));
+static int upload(mc_ctx *c, Buf &b, const T *h, size_t count, hipStream_t s) {
+  const size_t bytes = count * sizeof(T);
+  if (int rc = ensure(b, bytes + 16)) return rc;
+  if (!count) return MC_OK;
+  // Small inputs (the per-call id lists, offsets, member lists) go through a pinned staging
+  // ring owned by the context: a copy from pinned memory is a plain DMA, a pageable one is
+  // staged by the runtime.  A region is reused only after a stream synchronize that follows
+  // its copy (the ring wraps behind one).
+  static const bool staged = !getenv("MC_PAGEABLE_UPLOADS");
+  constexpr size_t STAGE = 8u << 20, SMALL = 1u << 20;
+  if (staged && bytes <= SMALL) {
+    if (!c->h_stage && hipHostMalloc((void **)&c->h_stage, STAGE, hipHostMallocDefault) != hipSuccess) {
+      (void)hipGetLastError();
+      c->h_stage = nullptr;
+    }
+    if (c->h_stage) {
+      size_t off = (c->stage_off + 255) & ~(size_t)255;
+      if (off + bytes > STAGE) {
+        MCG_CHECK(hipStreamSynchronize(s));
+        off = 0;
+      }
+      memcpy(c->h_stage + off, h, bytes);
+      MCG_CHECK(hipMemcpyAsync(b.p, c->h_stage + off, bytes, hipMemcpyHostToDevice, s));
+      c->stage_off = off + bytes;
+      return MC_OK;
+    }
+  }
+  MCG_CHECK(hipMemcpyAsync(b.p, h, bytes, hipMemcpyHostToDevice, s));
   return MC_OK;
 }
 
@@ -173,6 +198,7 @@ int mc_ctx_destroy(mc_ctx *c) {
                  &c->msum, &c->ident_s, &c->al_a, &c->al_b, &c->al_out, &c->acc_out})
     release(*b);
   if (c->h_scan) (void)hipHostFree(c->h_scan);
+  if (c->h_stage) (void)hipHostFree(c->h_stage);
   if (c->h_res) (void)hipHostFree(c->h_res);
   for (auto e : c->ev_pool) (void)hipEventDestroy(e);
   (void)hipEventDestroy(c->ev0);
@@ -203,10 +229,10 @@ static int load_common(mc_ctx *c, const uint64_t *seq_off, uint64_t n, const int
   TRY(ensure(c->codes, seq_off[n] + 16));
   TRY(ensure(c->packed, pk_off[n] * 4 + 16));
   TRY(ensure(c->impure, n + 16));
-  TRY(upload(c->pk_off, pk_off.data(), n + 1, c->stream));
-  TRY(upload(c->seq_off, seq_off, n + 1, c->stream));
-  TRY(upload(c->seg, seg, 2 * seg_off[n], c->stream));
-  TRY(upload(c->seg_off, seg_off, n + 1, c->stream));
+  TRY(upload(c, c->pk_off, pk_off.data(), n + 1, c->stream));
+  TRY(upload(c, c->seq_off, seq_off, n + 1, c->stream));
+  TRY(upload(c, c->seg, seg, 2 * seg_off[n], c->stream));
+  TRY(upload(c, c->seg_off, seg_off, n + 1, c->stream));
   return MC_OK;
 }
 
@@ -339,8 +365,8 @@ int mc_distance_keys(mc_ctx *c, const uint32_t *pivots, uint32_t npiv, const uin
   MCG_CHECK(hipSetDevice(c->device));
   TRY(check_ids(c, pivots, npiv));
   TRY(check_ids(c, ids, m));
-  TRY(upload(c->s_a, pivots, npiv, c->stream));
-  TRY(upload(c->s_b, ids, m, c->stream));
+  TRY(upload(c, c->s_a, pivots, npiv, c->stream));
+  TRY(upload(c, c->s_b, ids, m, c->stream));
   TRY(ensure(c->s_c, (size_t)npiv * m * 2 + 16));
   TRY(launch_distance_keys(c, (uint32_t *)c->s_a.p, npiv, (uint32_t *)c->s_b.p, m, (uint16_t *)c->s_c.p));
   TRY(download(keys, c->s_c.p, (size_t)npiv * m, c->stream));
@@ -361,8 +387,8 @@ int mc_pair_features(mc_ctx *c, const uint32_t *a, const uint32_t *b, uint64_t m
   MCG_CHECK(hipSetDevice(c->device));
   TRY(check_ids(c, a, m));
   TRY(check_ids(c, b, m));
-  TRY(upload(c->s_a, a, m, c->stream));
-  TRY(upload(c->s_b, b, m, c->stream));
+  TRY(upload(c, c->s_a, a, m, c->stream));
+  TRY(upload(c, c->s_b, b, m, c->stream));
   TRY(ensure(c->s_c, m * nflag * 8 + 16));
   TRY(launch_pairs(c, (uint32_t *)c->s_a.p, (uint32_t *)c->s_b.p, m, flags, nflag, (double *)c->s_c.p, nullptr,
                    nullptr, nullptr, false));
@@ -419,8 +445,8 @@ int mc_classify_pairs(mc_ctx *c, const uint32_t *a, const uint32_t *b, uint64_t 
   MCG_CHECK(hipSetDevice(c->device));
   TRY(check_ids(c, a, m));
   TRY(check_ids(c, b, m));
-  TRY(upload(c->s_a, a, m, c->stream));
-  TRY(upload(c->s_b, b, m, c->stream));
+  TRY(upload(c, c->s_a, a, m, c->stream));
+  TRY(upload(c, c->s_b, b, m, c->stream));
   TRY(ensure(c->s_c, m * 17 + 64));
   uint8_t *d_sim = (uint8_t *)c->s_c.p;
   double *d_c0 = (double *)((char *)c->s_c.p + (m + 15) / 16 * 16);
@@ -446,8 +472,8 @@ int mc_nw_identity(mc_ctx *c, const uint32_t *a, const uint32_t *b, uint64_t m, 
     la[i] = c->h_seq_off[a[i] + 1] - c->h_seq_off[a[i]];
     lb[i] = c->h_seq_off[b[i] + 1] - c->h_seq_off[b[i]];
   }
-  TRY(upload(c->s_d, a, m, c->stream));
-  TRY(upload(c->s_e, b, m, c->stream));
+  TRY(upload(c, c->s_d, a, m, c->stream));
+  TRY(upload(c, c->s_e, b, m, c->stream));
   TRY(ensure(c->s_f, m * 16 + 64));
   double *d_id = (double *)c->s_f.p;
   int32_t *d_len = (int32_t *)(d_id + m), *d_ids = d_len + m;
@@ -519,7 +545,7 @@ int mc_set_order(mc_ctx *c, const uint32_t *order, uint64_t n) {
   for (uint64_t p = 0; p < n; p++) c->h_spos[order[p]] = p;
   c->h_order.assign(order, order + n);
   c->h_alive.assign(n, 1);
-  TRY(upload(c->order, order, n, c->stream));
+  TRY(upload(c, c->order, order, n, c->stream));
   TRY(ensure(c->alive, n + 16));
   MCG_CHECK(hipMemsetAsync(c->alive.p, 1, n, c->stream));
   TRY(ensure(c->members, (n + 1) * 4));
@@ -639,9 +665,9 @@ static int align_window(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, uint
   *cells = cl;
   TRY(ensure(c->ident_s, c->norder * 8 + 16));
   if (ai.empty()) return MC_OK;
-  TRY(upload(c->al_a, ai.data(), ai.size(), c->stream));
-  TRY(upload(c->al_b, bi.data(), bi.size(), c->stream));
-  TRY(upload(c->al_out, out.data(), out.size(), c->stream));
+  TRY(upload(c, c->al_a, ai.data(), ai.size(), c->stream));
+  TRY(upload(c, c->al_b, bi.data(), bi.size(), c->stream));
+  TRY(upload(c, c->al_out, out.data(), out.size(), c->stream));
   return launch_nw(c, (uint8_t *)c->codes.p, (uint64_t *)c->seq_off.p, (uint32_t *)c->al_a.p, (uint8_t *)c->codes.p,
                    (uint64_t *)c->seq_off.p, (uint32_t *)c->al_b.p, ai.size(), la, lb, (double *)c->ident_s.p, nullptr,
                    nullptr, nullptr, (uint32_t *)c->al_out.p);
@@ -774,8 +800,8 @@ int mc_accumulate(mc_ctx *c, const uint32_t *bin_lo, const uint64_t *bounds, uin
   }
   MCG_CHECK(hipSetDevice(c->device));
   const uint64_t n = c->norder;
-  TRY(upload(c->s_d, bin_lo, (size_t)nbins + 1, c->stream));
-  TRY(upload(c->s_e, bounds, nbins, c->stream));
+  TRY(upload(c, c->s_d, bin_lo, (size_t)nbins + 1, c->stream));
+  TRY(upload(c, c->s_e, bounds, nbins, c->stream));
   TRY(ensure(c->s_f, n * 4 + 16));
   TRY(ensure(c->s_g, (n + 1) * 8 + 16));
   TRY(ensure(c->acc_out, 256));
@@ -908,7 +934,7 @@ int mc_classify_values(mc_ctx *c, const double *raw, uint64_t m, uint8_t *simila
   if (!raw) return MC_ERR_ARG;
   MCG_CHECK(hipSetDevice(c->device));
   const int ns = c->cls.c.n_single;
-  TRY(upload(c->s_a, raw, m * ns, c->stream));
+  TRY(upload(c, c->s_a, raw, m * ns, c->stream));
   TRY(ensure(c->s_c, m * 17 + 64));
   uint8_t *d_sim = (uint8_t *)c->s_c.p;
   double *d_c0 = (double *)((char *)c->s_c.p + (m + 15) / 16 * 16);
@@ -932,9 +958,9 @@ static int mean_shift_common(mc_ctx *c, const uint32_t *centre_ids, uint32_t C, 
   TRY(check_ids(c, centre_ids, C));
   const uint64_t nm = member_off[C];
   TRY(check_ids(c, members, nm));
-  TRY(upload(c->s_a, centre_ids, C, c->stream));
-  TRY(upload(c->s_b, member_off, C + 1, c->stream));
-  TRY(upload(c->s_c, members, nm, c->stream));
+  TRY(upload(c, c->s_a, centre_ids, C, c->stream));
+  TRY(upload(c, c->s_b, member_off, C + 1, c->stream));
+  TRY(upload(c, c->s_c, members, nm, c->stream));
   const uint8_t *d_keep = nullptr;
   if (keep) {
     uint64_t nk = 0;
@@ -943,7 +969,7 @@ static int mean_shift_common(mc_ctx *c, const uint32_t *centre_ids, uint32_t C, 
       const uint32_t e = std::min<uint32_t>(j + delta, C - 1);
       nk += member_off[e + 1] - member_off[b];
     }
-    TRY(upload(c->al_out, keep, nk, c->stream));
+    TRY(upload(c, c->al_out, keep, nk, c->stream));
     d_keep = (const uint8_t *)c->al_out.p;
   }
   TRY(ensure(c->flags_out, (size_t)C * 4 + 16));

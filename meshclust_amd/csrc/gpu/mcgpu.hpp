@@ -83,6 +83,8 @@ struct HostScan {
 struct mc_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  uint8_t *h_stage = nullptr;  // pinned staging ring for small uploads (abi.hip upload)
+  size_t stage_off = 0;
   // sequences
   uint64_t n = 0;
   std::vector<uint64_t> h_seq_off;
