@@ -246,6 +246,21 @@ def test_e2e_cli_byte_identical(eng, name, tmp_path):
         assert out.read_bytes() == f.read()
 
 
+@pytest.mark.parametrize("env", [{"MC_NW_LOOKAHEAD": "1"}, {"MC_NW_LOOKAHEAD": "3"}, {"MC_PAGEABLE_UPLOADS": "1"}],
+                         ids=["lookahead1", "lookahead3", "pageable"])
+@pytest.mark.parametrize("name", ["b3k300", "fam2k_id85"])
+def test_e2e_cli_variants_byte_identical(eng, name, env, tmp_path):
+    """The training search's lookahead depth (Trainer.cpp:703-721: one level per round, the
+    reference's order, or three) and the upload path do not change the output."""
+    fa, flags = fixtures.e2e_input(name, tmp_path)
+    out = tmp_path / (name + ".clstr")
+    r = subprocess.run([M.BIN, fa] + flags + ["--output", str(out), "--quiet"], capture_output=True, text=True,
+                       timeout=600, env=dict(os.environ, **env))
+    assert r.returncode == 0, r.stderr[-3000:]
+    with gzip.open(fixtures.golden("e2e_%s.clstr.gz" % name), "rb") as f:
+        assert out.read_bytes() == f.read()
+
+
 # ---------------------------------------------------------------- alignment mode
 def align_classifier(cutoff):
     """The classifier Trainer::train installs for k == 0 (Trainer.cpp:570-577)."""
