@@ -41,3 +41,18 @@ def test_distance_d_identity_random():
             from fractions import Fraction
             got = float(Fraction(1) - Fraction(frac) * Fraction(frac)) * 10000.0
         assert got == want, (t, M, B)
+
+
+def test_div32_float_reciprocal_division():
+    """accum.hip's Div32: n / d for the worker count d (<= 256) and chunk indices n < 2^22 as
+    trunc(float(n) * (1/d)) with one correction either way equals integer division, also when
+    the float reciprocal is off by one ulp."""
+    n = np.arange(0, 1 << 22, dtype=np.uint32)
+    nf = n.astype(np.float32)
+    for d in (1, 7, 8, 63, 127, 248, 255, 256):
+        inv0 = np.float32(1.0) / np.float32(d)
+        for inv in (inv0, np.nextafter(inv0, np.float32(0)), np.nextafter(inv0, np.float32(2))):
+            q = (nf * inv).astype(np.uint32)
+            r = n.astype(np.int64) - q.astype(np.int64) * d
+            q = np.where(r < 0, q - 1, np.where(r >= d, q + 1, q))
+            assert np.array_equal(q, n // d), d
