@@ -814,7 +814,9 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
     for (int b = threadIdx.x; b < A.B; b += NT) msum[b] = reinterpret_cast<const T *>(A.hr + pos * nch)[b];
     M = 1;
     last_q = 0;
-    drain();
+    // (no drain: the seed's member-list entries are never read back in the kernel -- member 0
+    // is always in the LDS cache -- and the kill log is tagged, so the stores need not have
+    // landed before the next step is published)
     __syncthreads();
   };
   auto log_kill = [&](uint64_t p) {  // thread 0: a pop / erase, for the workers
