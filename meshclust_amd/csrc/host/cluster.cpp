@@ -124,7 +124,7 @@ struct ShardBlock {
   static constexpr uint32_t kInline = 248;
   double best_val;
   uint64_t best_pos;
-  uint32_t has_best, is_min, n_flagged, pad;
+  uint32_t has_best, is_min, n_flagged, failed;
   uint32_t flagged[kInline];
 };
 static_assert(sizeof(ShardBlock) == 1024, "exchange block");
@@ -133,16 +133,25 @@ void sharded_step(mc_ctx *ctx, const ShardComm &comm, uint32_t centre, uint64_t 
                   std::vector<uint32_t> &flag_buf, std::vector<uint32_t> &all_flagged, mc_scan_result *res,
                   PhaseTimer &timer) {
   mc_scan_result loc{};
+  // A rank whose scan fails still takes part in the exchange, with its block marked failed, so
+  // every rank throws after the same all-gather instead of its peers waiting in it forever.
+  std::string scan_err;
   {
     Scope sc(timer, "accumulate.scan_part");
-    check(mc_scan_part(ctx, centre, S, E, (uint32_t)comm.rank, (uint32_t)comm.world, flag_buf.data(), flag_buf.size(),
-                       &loc),
-          "mc_scan_part");
+    try {
+      check(mc_scan_part(ctx, centre, S, E, (uint32_t)comm.rank, (uint32_t)comm.world, flag_buf.data(),
+                         flag_buf.size(), &loc),
+            "mc_scan_part");
+    } catch (const std::exception &e) {
+      scan_err = e.what();
+      loc = mc_scan_result{};
+    }
   }
   Scope sx(timer, "accumulate.exchange");
   const int W = comm.world;
   ShardBlock mine;
   memset(&mine, 0, sizeof mine);
+  mine.failed = scan_err.empty() ? 0 : 1;
   mine.best_val = loc.best_val;
   mine.best_pos = loc.best_pos;
   mine.has_best = loc.has_best ? 1 : 0;
@@ -152,6 +161,9 @@ void sharded_step(mc_ctx *ctx, const ShardComm &comm, uint32_t centre, uint64_t 
   std::vector<ShardBlock> all(W);
   if (comm.allgather(comm.user, &mine, sizeof mine, all.data()) != 0)
     throw Error("get_close all-gather across ranks failed", 1);
+  for (int r = 0; r < W; r++)
+    if (all[r].failed)
+      throw Error(scan_err.empty() ? "get_close failed on rank " + std::to_string(r) : scan_err, 1);
   memset(res, 0, sizeof *res);
   res->is_min = 1;
   res->best_val = -1.0;
@@ -370,10 +382,19 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
       const uint32_t W = (uint32_t)cfg.comm->world, per = (C + W - 1) / W;
       const uint32_t j0 = std::min<uint32_t>(C, per * (uint32_t)cfg.comm->rank), j1 = std::min<uint32_t>(C, j0 + per);
       std::vector<uint32_t> mine(per, 0), all((size_t)per * W, 0);
-      check(mc_mean_shift_range(ctx, cids.data(), C, off.data(), members.data(), cfg.delta, j0, j1, mine.data()),
-            "mc_mean_shift_range");
+      // a failed rank sends ids no read can have, so every rank stops after the same exchange
+      std::string ms_err;
+      try {
+        check(mc_mean_shift_range(ctx, cids.data(), C, off.data(), members.data(), cfg.delta, j0, j1, mine.data()),
+              "mc_mean_shift_range");
+      } catch (const std::exception &e) {
+        ms_err = e.what();
+        std::fill(mine.begin(), mine.end(), 0xffffffffu);
+      }
       if (cfg.comm->allgather(cfg.comm->user, mine.data(), (uint64_t)per * 4, all.data()) != 0)
         throw Error("centre all-gather across ranks failed", 1);
+      for (uint32_t j = 0; j < C; j++)
+        if (all[j] == 0xffffffffu) throw Error(ms_err.empty() ? "mean-shift update failed on another rank" : ms_err, 1);
       std::copy(all.begin(), all.begin() + C, newc.begin());
     } else if (C && !memo) {
       Scope sm(timer, "update.mean_shift");
