@@ -11,12 +11,15 @@ The FASTA is read from the page cache (the file is generated before the timed re
 rate on sequences already resident in HBM (no parse / upload / write) is reported in
 "extra" as resident_sequences_per_s.
 
-With --gpus N (torch.distributed, one rank per GPU) every rank clusters its own batch
-(seed 41 + rank): replicas, weak scaling; no collective is on the data path.  With --shard the
-ranks instead share ONE clustering of the seed-41 batch (meshclust_amd.dist), sharded by
-record: every get_close step is split over the ranks' static bvec blocks and combined with one
-RCCL all-gather per step, every mean-shift iteration is split by centre and the new centres
-all-gathered (strong scaling).
+With --gpus N > 1 (torch.distributed, one rank per GPU) the ranks share ONE clustering of
+BASELINE.json configs[3] (config D: 1,000,000 reads x 1 kb, 10,000 templates, seed 51,
+--id 0.90), sharded by record (strong scaling): every rank's persistent accumulation kernel
+scans only its interleaved tiles of each get_close window and the kernels exchange each step's
+{first maximum, flagged reads} through a host-memory mailbox they all map (no host round trip
+per step); every mean-shift iteration is split by centre and the new centres all-gathered over
+RCCL.  --mode replicas instead gives every rank its own config-B batch (seed 41 + rank: weak
+scaling, no collective on the data path); --mode shard at N = 1 runs the sharded code path on
+one rank.
 
 Prints ONE JSON line on rank 0.
 """
@@ -98,23 +101,29 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--n", type=int, default=100000)
+    ap.add_argument("--mode", choices=["auto", "shard", "replicas"], default="auto",
+                    help="auto: one GPU -> config B, several -> config D shared by the ranks")
+    ap.add_argument("--n", type=int, default=None)
     ap.add_argument("--len", type=int, default=1000)
-    ap.add_argument("--templates", type=int, default=1000)
+    ap.add_argument("--templates", type=int, default=None)
     ap.add_argument("--mut", type=float, default=0.03)
-    ap.add_argument("--seed", type=int, default=41)
+    ap.add_argument("--seed", type=int, default=None)
     ap.add_argument("--id", default="0.90")
-    ap.add_argument("--cpu-repeats", type=int, default=1, help="reference runs (median)")
+    ap.add_argument("--cpu-repeats", type=int, default=3, help="reference runs (median)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--stats-out", default=None)
-    ap.add_argument("--shard", action="store_true", help="ranks share one clustering (strong scaling)")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    shard = a.mode == "shard" or (a.mode == "auto" and world > 1)
+    cfg_d = shard and a.n is None  # the sharded workload: config D unless a size is given
+    a.n = a.n if a.n is not None else (1000000 if cfg_d else 100000)
+    a.templates = a.templates if a.templates is not None else (10000 if cfg_d else 1000)
+    a.seed = a.seed if a.seed is not None else (51 if cfg_d else 41)
     dist = None
-    if world > 1 or a.shard:
+    if world > 1 or shard:
         import torch.distributed as dist  # noqa: F811
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29517")
@@ -123,9 +132,12 @@ def main():
     import meshclust_amd as M
     if rank == 0 and not os.path.exists(M.GPU_LIB):
         M.build()
+    if shard and world == 1:
+        os.environ["MC_SHARD_FORCE"] = "1"  # the sharded code path with one rank
+    if shard and rank == 0:  # one shared input: rank 0 writes it, the others wait
+        ensure_fasta(a.n, a.len, a.templates, a.mut, a.seed)
     if dist:
         dist.barrier()
-    shard = dist is not None and a.shard  # (MC_SHARD_FORCE=1 takes the sharded steps at N = 1 too)
     fasta = ensure_fasta(a.n, a.len, a.templates, a.mut, a.seed + (0 if shard else rank))
     threads = min(16, host_threads())
     eng = M.Engine(local)
@@ -209,7 +221,8 @@ def main():
     dominant = max(fam_ms, key=lambda f: fam_ms[f])
     roof = None
     if fam_n["scan"]:
-        per_launch_bytes = scan_evals * eval_bytes / fam_n["scan"]
+        # (sharded: each rank's kernel scans its 1/world of every window)
+        per_launch_bytes = scan_evals * eval_bytes / fam_n["scan"] / (world if shard else 1)
         avg_s = fam_ms["scan"] / fam_n["scan"] / 1e3
         ach = per_launch_bytes / avg_s / 1e9
         # one launch per clustering = the device-resident accumulation (accum.hip); otherwise
@@ -239,7 +252,7 @@ def main():
                "frac": round(nw_rate / nw_peak, 4) if nw_rate else None,
                "cells_per_step": nw_cells / a.steps, "ms_per_step": round(fam_ms["nw"] / a.steps, 3)}
     cpu = None
-    if not a.no_cpu_baseline and world == 1:  # the reference is timed on rank 0 at N = 1 only
+    if not a.no_cpu_baseline and world == 1 and not shard:  # the reference: rank 0 at N = 1 only
         cpu = cpu_baseline(fasta, ["--id", a.id], a.n, host_threads(), a.cpu_repeats)
     line = {
         "metric": "sequences clustered/sec (+ NW cell-updates/sec) at 1/2/4/8 MI355X",
@@ -253,11 +266,14 @@ def main():
         "scaling": "strong" if shard else "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic (meshclust_amd.synth: %d reads x %d bp, %d templates, mut %.2f, seed %d+rank)"
-                % (a.n, a.len, a.templates, a.mut, a.seed),
-        "config": {"workload": "config B: 100k synthetic 1kb reads, --id %s k-mer mean-shift" % a.id,
-                   "reads_per_gpu": a.n, "read_len": a.len, "k": s0["k"], "histogram_bits": 8 * width,
-                   "parallelism": ("one clustering sharded by record x%d (RCCL all-gather per step)" % world) if shard
+        "data": "synthetic (meshclust_amd.synth: %d reads x %d bp, %d templates, mut %.2f, seed %d%s)"
+                % (a.n, a.len, a.templates, a.mut, a.seed, "" if shard else "+rank"),
+        "config": {"workload": ("config D: %dk synthetic 1kb reads (%d templates), --id %s k-mer mean-shift, "
+                                "one clustering shared by %d GPU(s)" % (a.n // 1000, a.templates, a.id, world)) if shard
+                   else "config B: %dk synthetic 1kb reads, --id %s k-mer mean-shift" % (a.n // 1000, a.id),
+                   "reads": a.n if shard else a.n * world, "read_len": a.len, "k": s0["k"], "histogram_bits": 8 * width,
+                   "parallelism": ("one clustering sharded by record x%d (device mailbox exchange per get_close "
+                                   "step, RCCL all-gather per mean-shift iteration)" % world) if shard
                    else "replicas x%d" % world},
         "roofline": roof,
         "cpu_baseline": cpu,

@@ -234,6 +234,26 @@ int mc_accumulate(mc_ctx *ctx, const uint32_t *bin_lo, const uint64_t *bounds, u
                   uint64_t *stats);
 
 /*
+ * One accumulation shared by `world` ranks, one GPU each (the loop of
+ * ClusterFactory.cpp:717-730 whose get_close steps, Trainer.cpp:81-106, are split by record).
+ * Every rank registers the same host-memory mailbox of mc_mailbox_bytes(world, n) zeroed bytes
+ * (a POSIX shared-memory segment mapped by each rank's process, or one buffer shared by the
+ * threads of one process) with mc_set_mailbox, after mc_set_order; then all ranks call
+ * mc_accumulate with identical arguments.  Each rank's persistent kernel scans only its
+ * interleaved tiles of every window (tile t of the static order belongs to rank t mod world);
+ * per step the kernels exchange {first maximum of combo 0, flagged positions} through the
+ * mailbox without the host, and every rank applies the same remove_available + get_mean, so
+ * every rank returns the same partition as a single-rank run.  A rank that fails stops the
+ * others after the exchange's deadline (MC_ERR_HIP).  world 0 detaches.
+ */
+uint64_t mc_mailbox_bytes(int world, uint64_t n);
+/* share: how many ranks' kernels run on this rank's GPU (>= 1; each then takes that share of
+   the CUs, so they are co-resident: tests put two ranks on one GPU) */
+int mc_set_mailbox(mc_ctx *ctx, void *host, uint64_t bytes, int rank, int world, int share);
+/* the PCI bus id of the context's GPU (ranks sharing a GPU find each other with it) */
+int mc_ctx_pci_bus_id(mc_ctx *ctx, char *buf, int len);
+
+/*
  * One mean-shift iteration over all centres (the omp parallel for of ClusterFactory.cpp:
  * 744-749 around mean_shift_update, :289-380): for centre j, the members of clusters
  * j-delta..j+delta (CSR member_off[C+1]/members, cluster order) are filtered by the

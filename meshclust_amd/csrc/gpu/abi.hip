@@ -10,6 +10,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -188,10 +190,13 @@ int mc_ctx_create(int device, mc_ctx **out) {
   return MC_OK;
 }
 
+static void mailbox_detach(mc_ctx *c);
+
 int mc_ctx_destroy(mc_ctx *c) {
   if (!c) return MC_OK;
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
+  mailbox_detach(c);
   for (Buf *b : {&c->codes, &c->seq_off, &c->seg, &c->seg_off, &c->packed, &c->pk_off, &c->impure, &c->hist, &c->mag, &c->sumsq, &c->len, &c->order,
                  &c->alive, &c->members, &c->member_keys, &c->partials, &c->scan_dev, &c->flags_out, &c->s_a, &c->s_b,
                  &c->s_c, &c->s_d, &c->s_e, &c->s_f, &c->s_g, &c->s_h, &c->s_i, &c->s_j, &c->hs, &c->mag_s, &c->sumsq_s, &c->len_s, &c->ticket,
@@ -785,6 +790,72 @@ int mc_scan_commit(mc_ctx *c, const uint32_t *flagged_pos, uint64_t n, mc_scan_r
   return MC_OK;
 }
 
+// ---- mailbox of several ranks sharing one accumulation -------------------------------------
+// The host range is registered once per process (hipHostRegister is process-wide), counted by
+// the contexts that use it: the threads of `bin/meshclust --devices` share one buffer.
+static std::mutex g_mb_mu;
+static std::map<void *, int> g_mb_refs;
+
+static void mailbox_detach(mc_ctx *c) {
+  if (!c->mb_host) return;
+  std::lock_guard<std::mutex> lk(g_mb_mu);
+  auto it = g_mb_refs.find(c->mb_host);
+  if (it != g_mb_refs.end() && --it->second == 0) {
+    (void)hipHostUnregister(c->mb_host);
+    g_mb_refs.erase(it);
+  }
+  c->mb_host = c->mb_dev = nullptr;
+  c->mb_bytes = 0;
+  c->mb_rank = c->mb_world = 0;
+  c->mb_share = 1;
+}
+
+uint64_t mc_mailbox_bytes(int world, uint64_t n) {
+  if (world < 1) return 0;
+  return 2ull * (uint64_t)world * mailbox_slot_granules((uint32_t)world, n) * 8;
+}
+
+int mc_ctx_pci_bus_id(mc_ctx *c, char *buf, int len) {
+  if (!c || !buf || len < 16) return MC_ERR_ARG;
+  MCG_CHECK(hipDeviceGetPCIBusId(buf, len, c->device));
+  return MC_OK;
+}
+
+int mc_set_mailbox(mc_ctx *c, void *host, uint64_t bytes, int rank, int world, int share) {
+  if (!c) return MC_ERR_ARG;
+  MCG_CHECK(hipSetDevice(c->device));
+  mailbox_detach(c);
+  if (world == 0) return MC_OK;
+  if (!host || world < 1 || world > 64 || rank < 0 || rank >= world || share < 1 || share > world ||
+      ((uintptr_t)host & 7))
+    return MC_ERR_ARG;
+  {
+    std::lock_guard<std::mutex> lk(g_mb_mu);
+    auto it = g_mb_refs.find(host);
+    if (it == g_mb_refs.end()) {
+      const hipError_t e = hipHostRegister(host, bytes, hipHostRegisterMapped | hipHostRegisterPortable);
+      if (e != hipSuccess) return hip_fail(e, "hipHostRegister (mailbox)");
+      g_mb_refs[host] = 1;
+    } else {
+      it->second++;
+    }
+  }
+  void *dev = nullptr;
+  const hipError_t e = hipHostGetDevicePointer(&dev, host, 0);
+  if (e != hipSuccess) {
+    c->mb_host = host;  // (counted above)
+    mailbox_detach(c);
+    return hip_fail(e, "hipHostGetDevicePointer (mailbox)");
+  }
+  c->mb_host = host;
+  c->mb_dev = dev;
+  c->mb_bytes = bytes;
+  c->mb_rank = rank;
+  c->mb_world = world;
+  c->mb_share = share;
+  return MC_OK;
+}
+
 int mc_accumulate(mc_ctx *c, const uint32_t *bin_lo, const uint64_t *bounds, uint32_t nbins, double sim,
                   uint32_t *centre_ids, uint64_t *member_off, uint32_t *member_ids, uint64_t *nclusters,
                   uint64_t *stats) {
@@ -797,6 +868,10 @@ int mc_accumulate(mc_ctx *c, const uint32_t *bin_lo, const uint64_t *bounds, uin
   if (!fused(c) || !accum_supported(c, nbins)) {
     set_error("device-resident accumulation does not take this configuration");
     return MC_ERR_UNSUPPORTED;
+  }
+  if (c->mb_world > 0 && c->mb_bytes < mc_mailbox_bytes(c->mb_world, c->norder)) {
+    set_error("mailbox smaller than mc_mailbox_bytes(world, n)");
+    return MC_ERR_ARG;
   }
   MCG_CHECK(hipSetDevice(c->device));
   const uint64_t n = c->norder;

@@ -59,6 +59,18 @@ constexpr int PART_G = 8;              // granules per partial
 constexpr int INL = 3;                 // flagged positions carried inline in a partial
 constexpr uint32_t PLIST = 1024;       // flagged positions of one step listed in the controller's LDS
 constexpr uint32_t GMAX = 256;         // workgroups: the controller polls the G - 1 workers' partials with one thread each
+// Wide rows (B * w >= 512 bytes: k >= 5 at 8 bits, k >= 4 at 16): a wave scores one candidate
+// (64 lanes over the row, read row-major from `hr`), so a tile of NW candidates is the unit of
+// ownership instead of a 512-position chunk, and a few-hundred-candidate window spreads over
+// dozens of workers instead of the one or two that own its chunks.
+constexpr int WIDE_NCH = 32;
+// Several ranks (GPUs) sharing one accumulation: global tile t belongs to rank t mod W, whose
+// worker (t / W) mod GW scans it.  Each rank's controller keeps the whole (replicated) chain
+// state and exchanges, per step, {first max, flagged positions} with the other ranks' kernels
+// through a mailbox in host memory shared by all of them: MBOX_HDR granules per rank and step,
+// then its flagged positions, every granule tagged with the step; two parities of slots, since
+// a rank can be at most one step ahead of another.
+constexpr int MBOX_HDR = 8;  // best value hi / lo, best position, flagged, scanned, (3 spare)
 
 // Static part of a centre's bvec window (bvec::get_range, bvec.cpp:245-278), per static
 // position: the window lengths, the bins index_of picks, and how many static positions of
@@ -113,6 +125,11 @@ struct AccArgs {
   int prof;             // controller phase timers (MC_ACCUM_PROFILE)
   uint64_t *trace;      // MC_ACCUM_PROFILE>=2: per-step timestamps, TRACE_STEPS x TRACE_W
   int trace_all;        // MC_ACCUM_PROFILE=3: every active worker marks min/max (atomics)
+  // ranks: this one's tiles are t = lt * W + rank; mbox (host memory, device-mapped) non-null
+  // when the ranks' kernels exchange every step, slot_g granules per rank slot
+  uint32_t W, rank;
+  uint64_t *mbox;
+  uint64_t slot_g;
 };
 
 __device__ __forceinline__ uint64_t now() { return __builtin_amdgcn_s_memrealtime(); }
@@ -145,6 +162,27 @@ __device__ __forceinline__ uint32_t ld32(const uint32_t *p) {
   return __hip_atomic_load(const_cast<uint32_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ void drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// the mailbox: host memory shared by every rank's GPU -- system-scope granules
+__device__ __forceinline__ void st64x(uint64_t *p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint64_t ld64x(const uint64_t *p) {
+  return __hip_atomic_load(const_cast<uint64_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// this rank's tiles of global tiles [c0, c1]: local tiles [*lt0, *lt1] (global = lt * W + rank)
+__device__ __forceinline__ bool rank_tiles(uint64_t c0, uint64_t c1, uint32_t W, uint32_t r, uint64_t *lt0,
+                                           uint64_t *lt1) {
+  if (W == 1) {
+    *lt0 = c0;
+    *lt1 = c1;
+    return true;
+  }
+  if (c1 < r) return false;
+  const uint64_t a = c0 <= r ? 0 : (c0 - r + W - 1) / W, b = (c1 - r) / W;
+  *lt0 = a;
+  *lt1 = b;
+  return a <= b;
+}
 __device__ __forceinline__ uint64_t gran(uint32_t tag, uint32_t data) { return ((uint64_t)tag << 32) | data; }
 
 __device__ __forceinline__ uint32_t wave_sum32(uint32_t v) { return wave_sum32_all(v); }
@@ -397,7 +435,7 @@ __device__ __forceinline__ int classify_cand(const Acc<T> &acc, const PInfo &pi,
 // reads row t's chunks conflict-free) and never read from memory again.
 // LDS: record words | alive flags (fcap) | resident rows (res * nch * NT uint4)
 // ============================================================================================
-template <typename T, int NCH>
+template <typename T, int NCH, bool WIDE>
 __device__ __forceinline__ void worker(const AccArgs &A, const DevClassifier &C, uint4 *dyn) {
   __shared__ double s_bv[NW];
   __shared__ uint64_t s_bp[NW];
@@ -409,12 +447,15 @@ __device__ __forceinline__ void worker(const AccArgs &A, const DevClassifier &C,
   const int lane = threadIdx.x & 63, wv = wave_id();
   const int nch = NCH > 0 ? NCH : A.nch;
   const int rec_words = (int)A.rec_g;
+  constexpr uint32_t TS = WIDE ? (uint32_t)NW : (uint32_t)NT;  // positions per owned tile
   uint32_t *srec = reinterpret_cast<uint32_t *>(dyn);
-  const uint4 *clds = dyn;  // centre row = record words 0 .. 4 nch
-  uint8_t *lal = reinterpret_cast<uint8_t *>(dyn + (rec_words + 3) / 4);
+  // centre row: record words 0 .. 4 nch, or (wide rows) loaded from `hr` after the record
+  uint4 *lcen = dyn + (rec_words + 3) / 4;
+  const uint4 *clds = WIDE ? lcen : dyn;
+  uint8_t *lal = reinterpret_cast<uint8_t *>(lcen + (WIDE ? nch : 0));
   uint4 *lrow = reinterpret_cast<uint4 *>(lal + (A.fcap + 15) / 16 * 16);
-  // alive flags of the positions this worker owns (chunks w, w + GW, ...), local index
-  // (chunk / GW) * NT + offset: flagged candidates are cleared by their owner thread, and so
+  // alive flags of the positions this worker owns (tiles w, w + GW, ...), local index
+  // (tile / GW) * TS + offset: flagged candidates are cleared by their owner thread, and so
   // are the controller's pops and erases, which arrive with the step records
   for (uint64_t i = threadIdx.x; i < A.fcap; i += NT) lal[i] = 1;
   const int res = A.res;
@@ -423,7 +464,7 @@ __device__ __forceinline__ void worker(const AccArgs &A, const DevClassifier &C,
   PInfo rinf0{0, 0, 0}, rinf1{0, 0, 0};
   PTerms rterm0{0, 0, 0.0}, rterm1{0, 0, 0.0};
   for (int i = 0; i < res; i++) {
-    const uint64_t pos = ((uint64_t)w + (uint64_t)i * GW) * NT + threadIdx.x;
+    const uint64_t pos = (((uint64_t)w + (uint64_t)i * GW) * A.W + A.rank) * NT + threadIdx.x;
     for (int k = 0; k < nch; k++)
       lrow[((uint64_t)i * nch + k) * NT + threadIdx.x] = pos < A.N ? A.hs[(uint64_t)k * A.npad + pos] : make_uint4(0, 0, 0, 0);
     if (i < 2 && pos < A.N) {
@@ -515,7 +556,7 @@ __device__ __forceinline__ void worker(const AccArgs &A, const DevClassifier &C,
     seen = s_go;
     uint64_t t_seen = 0;
     if (A.trace && threadIdx.x == 0) t_seen = now();  // (recorded only by active workers)
-    const uint32_t *hdr = srec + 4 * nch;
+    const uint32_t *hdr = srec + (WIDE ? 0 : 4 * nch);
     if (hdr[0] == NONE) return;  // accumulation finished
     const uint64_t P_S = hdr[1], P_E = hdr[2];
     const uint32_t kend = hdr[3];
@@ -544,10 +585,11 @@ __device__ __forceinline__ void worker(const AccArgs &A, const DevClassifier &C,
           }
           p = (uint32_t)g;
         }
-        const uint64_t ch = p / NT;
-        if ((p % NT) == (uint32_t)threadIdx.x) {
-          const uint32_t cq = dgw.div((uint32_t)ch);
-          if ((uint32_t)ch - cq * GW == w) lal[(uint64_t)cq * NT + threadIdx.x] = 0;
+        const uint64_t ch = p / TS;
+        if ((p % TS) == (uint32_t)threadIdx.x && (A.W == 1 || ch % A.W == A.rank)) {
+          const uint32_t lt = (uint32_t)(A.W == 1 ? ch : ch / A.W);
+          const uint32_t cq = dgw.div(lt);
+          if (lt - cq * GW == w) lal[(uint64_t)cq * TS + threadIdx.x] = 0;
         }
       }
       kcur = kend;
@@ -555,7 +597,8 @@ __device__ __forceinline__ void worker(const AccArgs &A, const DevClassifier &C,
     uint64_t t_klog = 0, t_sad = 0, t_top = 0;
     if (A.trace && threadIdx.x == 0) t_klog = now();
     // ---- the chunks of the window this worker owns: Trainer::get_close ----------------
-    const uint64_t c0 = P_S / NT, c1 = P_E / NT;
+    uint64_t c0, c1;  // this rank's (local) tiles of the window
+    if (!rank_tiles(P_S / TS, P_E / TS, A.W, A.rank, &c0, &c1)) continue;
     const uint32_t nact = (uint32_t)(c1 - c0 + 1 < (uint64_t)GW ? c1 - c0 + 1 : (uint64_t)GW);
     const uint32_t mine = dgw.mod(w + GW - dgw.mod((uint32_t)c0));
     if (mine >= nact) continue;
@@ -563,6 +606,8 @@ __device__ __forceinline__ void worker(const AccArgs &A, const DevClassifier &C,
       s_nfl = 0;
       s_nscan = 0;
     }
+    if constexpr (WIDE)  // the centre's row (read-only static copy) for this step's tiles
+      for (int c = threadIdx.x; c < nch; c += NT) lcen[c] = A.hr[(uint64_t)hdr[0] * nch + c];
     uint64_t t_w7 = 0, t_bar = 0;
     if (A.trace && threadIdx.x == NT - 64) t_w7 = now();  // (profile: the last wave reaches the barrier)
     __syncthreads();
@@ -578,9 +623,43 @@ __device__ __forceinline__ void worker(const AccArgs &A, const DevClassifier &C,
       if (idx < (uint32_t)INL) s_inl[idx] = (uint32_t)pos;
       else st32(A.fpos + base + idx, (uint32_t)pos);
     };
+    if constexpr (WIDE) {
+      // one candidate per wave: lanes take chunks lane, lane + 64, ... of its row (coalesced
+      // 1 KiB loads), four loads in flight, sums reduced over the wave; every lane then holds
+      // the same statistics and runs the same classifier
+      for (uint64_t ch = c0 + mine; ch <= c1; ch += GW) {
+        const uint64_t li = dgw.div((uint32_t)ch);
+        const uint64_t pos = (ch * A.W + A.rank) * TS + (uint64_t)wv;
+        uint8_t *la = lal + li * TS + wv;
+        if (!(pos >= P_S && pos <= P_E && *la)) continue;
+        if (lane == 0) nscan++;
+        const uint4 *row = A.hr + pos * (uint64_t)nch;
+        Acc<T> acc;
+        int c = lane;
+        for (; c + 192 < nch; c += 256) {
+          const uint4 v0 = row[c], v1 = row[c + 64], v2 = row[c + 128], v3 = row[c + 192];
+          acc.add(v0, clds[c]);
+          acc.add(v1, clds[c + 64]);
+          acc.add(v2, clds[c + 128]);
+          acc.add(v3, clds[c + 192]);
+        }
+        for (; c < nch; c += 64) acc.add(row[c], clds[c]);
+        acc.wave_reduce();
+        const PInfo pi{A.mag_s[pos], A.sumsq_s[pos], A.len_s[pos]};
+        double cv;
+        if (classify_cand<T>(acc, pi, pc, A.B, C, &cv) && lane == 0) {
+          *la = 0;
+          flag_pos(pos);
+        }
+        if (cv > -1.0 && better(cv, pos, best_v, best_p)) {
+          best_v = cv;
+          best_p = pos;
+        }
+      }
+    } else
     for (uint64_t ch = c0 + mine; ch <= c1; ch += GW) {
       const uint64_t li = dgw.div((uint32_t)ch);  // local chunk index
-      const uint64_t pos = ch * NT + threadIdx.x;
+      const uint64_t pos = (ch * A.W + A.rank) * NT + threadIdx.x;
       uint8_t *la = lal + li * NT + threadIdx.x;
       if (!(pos >= P_S && pos <= P_E && *la)) continue;
       nscan++;
@@ -726,7 +805,7 @@ __device__ __forceinline__ void worker(const AccArgs &A, const DevClassifier &C,
 // Controller (WG 0).  LDS: integer mean row | column sums | bvec (counts, Fenwick tree, bin
 // starts, begin bounds, bitmap unless global) | member cache
 // ============================================================================================
-template <typename T, int NCH>
+template <typename T, int NCH, bool WIDE>
 __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
   __shared__ uint64_t s_red[3 * NW];
   __shared__ double s_bv[NW];
@@ -737,6 +816,9 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
   __shared__ uint32_t s_klast[KINL];
   __shared__ int s_abort;
   __shared__ uint64_t s_sumF;
+  __shared__ double s_xv[64];  // the ranks' step headers (mailbox)
+  __shared__ uint64_t s_xp[64];
+  __shared__ uint32_t s_xn[64], s_xs[64];
   constexpr int NC = NCH > 0 ? NCH : 1;
   const uint32_t GW = gridDim.x - 1;
   const int lane = threadIdx.x & 63, wv = wave_id();
@@ -753,7 +835,7 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
   MemberCache mc;
   {
     uint8_t *p = reinterpret_cast<uint8_t *>(lbits + (A.gbits ? 0 : (nwords + 3) / 4 * 4));
-    mc.rp = nch + 1;
+    mc.rp = WIDE ? 0 : nch + 1;  // (wide rows: member metadata only, rows read from `hr`)
     mc.row = reinterpret_cast<uint4 *>(p);
     p += (size_t)A.mrow * mc.rp * 16;
     mc.wt = reinterpret_cast<WinTab *>(p);
@@ -809,7 +891,7 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
         mc.wt[0] = mi.wt;
       }
     }
-    if (A.mrow)
+    if (A.mrow && !WIDE)
       for (int c = threadIdx.x; c < nch; c += NT) mc.row[c] = A.hr[pos * nch + c];
     for (int b = threadIdx.x; b < A.B; b += NT) msum[b] = reinterpret_cast<const T *>(A.hr + pos * nch)[b];
     M = 1;
@@ -838,12 +920,12 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
   // data word j of the record for the current `last` (centre row words, then the header)
   auto rec_word = [&](int j, bool have, uint64_t S, uint64_t E) -> uint32_t {
     const bool cached = last_q < A.mrow;
-    if (j < 4 * nch) {
+    if (!WIDE && j < 4 * nch) {
       if (last == NONE) return 0;
       const uint4 v = cached ? mc.row[(size_t)last_q * mc.rp + j / 4] : A.hr[(uint64_t)last * nch + j / 4];
       return (j & 3) == 0 ? v.x : (j & 3) == 1 ? v.y : (j & 3) == 2 ? v.z : v.w;
     }
-    const int h = j - 4 * nch;
+    const int h = j - (WIDE ? 0 : 4 * nch);
     if (h == 0) return have ? last : NONE;
     if (h == 1) return (uint32_t)S;
     if (h == 2) return (uint32_t)E;
@@ -862,7 +944,9 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
   // member qm of the current cluster is static position p, flagged in this step (key step << 32
   // | p orders members like the bvec walk): member list, cache entry (row, magnitudes, window
   // data from the read-only static arrays) or column sums past the cache, and the bvec kill
-  auto take = [&](uint64_t qm, uint32_t p) {
+  // (wide rows: the row stays in `hr`; its column sums are added here only for a member past
+  // the step's list, `sums`, the others by the column-sum pass over the list)
+  auto take = [&](uint64_t qm, uint32_t p, bool sums) {
     const uint64_t key = ((uint64_t)step << 32) | p;
     st32(A.mem_pos + cl_start + qm, p);
     st64(A.mkeys + cl_start + qm, key);
@@ -875,8 +959,10 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
       mc.info[qm * 3 + 1] = mi.sumsq;
       mc.info[qm * 3 + 2] = mi.len;
       mc.wt[qm] = mi.wt;
-      for (int k = 0; k < nch; k++) mc.row[qm * mc.rp + k] = hrow[k];
-    } else {
+      if (!WIDE)
+        for (int k = 0; k < nch; k++) mc.row[qm * mc.rp + k] = hrow[k];
+    }
+    if (WIDE ? sums : qm >= A.mrow) {
       constexpr int per = 16 / (int)sizeof(T);
       for (int k = 0; k < nch; k++) {
         const uint4 v = hrow[k];
@@ -993,8 +1079,13 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
     if (!have) break;  // the record told the workers to stop
 
     // ============ collect the step (get_close's reduction + get_mean) ======================
-    const uint64_t c0 = S / NT, c1 = E / NT;
-    const uint32_t nact = (uint32_t)(c1 - c0 + 1 < (uint64_t)GW ? c1 - c0 + 1 : (uint64_t)GW);
+    constexpr uint64_t TS = WIDE ? (uint64_t)NW : (uint64_t)NT;
+    uint64_t c0 = 0, c1 = 0;
+    const uint32_t nact = rank_tiles(S / TS, E / TS, A.W, A.rank, &c0, &c1)
+                              ? (uint32_t)(c1 - c0 + 1 < (uint64_t)GW ? c1 - c0 + 1 : (uint64_t)GW)
+                              : 0u;
+    // mailbox: this rank's slot of the step's parity; the local flagged positions go there
+    uint64_t *mslot = A.mbox ? A.mbox + ((uint64_t)(step & 1) * A.W + A.rank) * A.slot_g : nullptr;
     // thread t polls the partial of the t-th active worker until its granules carry the step,
     // then lists that worker's flagged positions (a slot from an LDS counter: member order is
     // irrelevant, the keys step << 32 | position order them like the bvec walk)
@@ -1033,10 +1124,12 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
         for (uint32_t j = 0; j < cnt_w; j++) {
           const uint32_t p = j < (uint32_t)INL ? (uint32_t)g8[5 + j] : ld32(A.fpos + (uint64_t)wk * A.fcap + j);
           const uint32_t slot = atomicAdd(&s_new, 1u);
-          if (slot < PLIST) {
+          if (mslot) {  // (several ranks: every rank takes the union, below)
+            st64x(mslot + MBOX_HDR + slot, gran(step, p));
+          } else if (slot < PLIST) {
             s_plist[slot] = p;
           } else {  // a list overflow: this thread takes the member itself (past the cache)
-            take(M + slot, p);
+            take(M + slot, p, true);
             drain();
           }
         }
@@ -1077,6 +1170,91 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
         best_pos = s_bp[i];
       }
     }
+    if (mslot) {
+      // ---- the ranks' exchange: publish this rank's header, take every rank's ----------
+      // get_close over the union is the serial loop's: is_min = nothing flagged anywhere, the
+      // result the first maximum by (value, static position), every flagged candidate joins
+      if (threadIdx.x < MBOX_HDR) {
+        const uint64_t vb = (uint64_t)__double_as_longlong(best_val);
+        const int j = threadIdx.x;
+        const uint32_t data = j == 0   ? (uint32_t)(vb >> 32)
+                              : j == 1 ? (uint32_t)vb
+                              : j == 2 ? (best_pos == NONE64 ? NONE : (uint32_t)best_pos)
+                              : j == 3 ? (uint32_t)nflag
+                              : j == 4 ? (uint32_t)nsc
+                                       : 0u;
+        st64x(mslot + j, gran(step, data));
+      }
+      uint64_t *mbase = A.mbox + (uint64_t)(step & 1) * A.W * A.slot_g;
+      if (threadIdx.x < A.W) {  // thread r reads rank r's header (W <= 64: wave 0)
+        const uint64_t *h = mbase + (uint64_t)threadIdx.x * A.slot_g;
+        const uint64_t t0 = now();
+        uint64_t g[5];
+        for (uint32_t it = 1;; it++) {
+          bool ok = true;
+#pragma unroll
+          for (int j = 0; j < 5; j++) {
+            g[j] = ld64x(h + j);
+            ok &= (uint32_t)(g[j] >> 32) == step;
+          }
+          if (ok) break;
+          if ((it & 63) == 0 && timed_out(A, t0)) {
+            s_abort = 1;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        s_xv[threadIdx.x] = __longlong_as_double((long long)((g[0] << 32) | (g[1] & 0xffffffffull)));
+        s_xp[threadIdx.x] = (uint32_t)g[2] == NONE ? NONE64 : (uint64_t)(uint32_t)g[2];
+        s_xn[threadIdx.x] = (uint32_t)g[3];
+        s_xs[threadIdx.x] = (uint32_t)g[4];
+      }
+      __syncthreads();
+      if (s_abort) {
+        if (threadIdx.x == 0) atomicMax((unsigned long long *)&A.out[3], 99ull);
+        return;
+      }
+      nflag = 0;
+      nsc = 0;
+      best_val = -1.0;
+      best_pos = NONE64;
+      for (uint32_t r = 0; r < A.W; r++) {
+        nflag += s_xn[r];
+        nsc += s_xs[r];
+        if (s_xp[r] != NONE64 && better(s_xv[r], s_xp[r], best_val, best_pos)) {
+          best_val = s_xv[r];
+          best_pos = s_xp[r];
+        }
+      }
+      // the union of the flagged positions: list entry i is rank r's entry i - (earlier ranks')
+      for (uint64_t i = threadIdx.x; i < nflag; i += NT) {
+        uint32_t r = 0;
+        uint64_t j = i;
+        while (j >= s_xn[r]) j -= s_xn[r++];
+        const uint64_t *e = mbase + (uint64_t)r * A.slot_g + MBOX_HDR + j;
+        const uint64_t t0 = now();
+        uint64_t g = ld64x(e);
+        for (uint32_t it = 1; (uint32_t)(g >> 32) != step; it++) {
+          if ((it & 63) == 0 && timed_out(A, t0)) {
+            s_abort = 1;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+          g = ld64x(e);
+        }
+        if (i < PLIST) {
+          s_plist[i] = (uint32_t)g;
+        } else {
+          take(M + i, (uint32_t)g, true);
+          drain();
+        }
+      }
+      __syncthreads();
+      if (s_abort) {
+        if (threadIdx.x == 0) atomicMax((unsigned long long *)&A.out[3], 99ull);
+        return;
+      }
+    }
     ncand += nsc;
     uint64_t tq = 0;
     if (A.prof && threadIdx.x == 0) {
@@ -1087,15 +1265,37 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
       // remove_available: the new members, one thread each, all their loads in flight at once
       // (member i on thread i + 64: wave 0, which publishes the next record, keeps no
       // outstanding stores for that record's drain to wait on)
-      for (uint64_t i = (threadIdx.x + NT - 64) % NT; i < nflag && i < PLIST; i += NT) take(M + i, s_plist[i]);
+      for (uint64_t i = (threadIdx.x + NT - 64) % NT; i < nflag && i < PLIST; i += NT) take(M + i, s_plist[i], false);
       if (M + nflag > A.mrow) drain();  // members past the cache are read back from mem_pos / mkeys
       __syncthreads();
       if (A.prof && threadIdx.x == 0) t_ws[3] += now() - tq;  // (the takes, inside "column sums")
       // column sums of the cached new members: thread (word w of a row, member slice sl) adds
       // up its 32-bit word over the slice's members, then one LDS atomic per bin and thread
       const uint64_t q0 = M, q1 = M + nflag < A.mrow ? M + nflag : (uint64_t)A.mrow;
+      const uint32_t nlist = nflag < PLIST ? (uint32_t)nflag : PLIST;
       M += nflag;
-      {
+      if constexpr (WIDE) {
+        // column sums of the listed new members straight from `hr`: thread (chunk c, member
+        // slice sl) adds its 16-byte chunk over the slice's members (independent loads), then one
+        // LDS atomic per bin and thread
+        constexpr int per = 16 / (int)sizeof(T);
+        const int nsl = nch >= NT ? 1 : NT / nch;
+        for (int t = threadIdx.x; t < nch * nsl; t += NT) {
+          const int c = t % nch, sl = t / nch;
+          uint32_t sum[per];
+#pragma unroll
+          for (int e = 0; e < per; e++) sum[e] = 0;
+          for (uint32_t i = (uint32_t)sl; i < nlist; i += (uint32_t)nsl) {
+            const uint4 v = A.hr[(uint64_t)s_plist[i] * nch + c];
+            const T *pv = reinterpret_cast<const T *>(&v);
+#pragma unroll
+            for (int e = 0; e < per; e++) sum[e] += pv[e];
+          }
+#pragma unroll
+          for (int e = 0; e < per; e++)
+            if (sum[e] && c * per + e < A.B) atomicAdd((unsigned long long *)&msum[c * per + e], (unsigned long long)sum[e]);
+        }
+      } else {
         constexpr int per = 4 / (int)sizeof(T);  // bins per 32-bit word
         const int wpr = (A.B + per - 1) / per;
         const int nsl = wpr >= NT ? 1 : NT / wpr;
@@ -1142,6 +1342,35 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
       const uint4 *F4 = reinterpret_cast<const uint4 *>(Fl);
       double bd = __builtin_inf();
       uint64_t bk = NONE64, bq = 0;
+      if constexpr (WIDE) {
+        // one member per wave (rows from `hr`, 64 lanes over the row): every lane ends with
+        // the wave's first minimum
+        for (uint64_t q = wv; q < M; q += NW) {
+          const uint32_t r = q < A.mrow ? mc.pos[q] : ld32(A.mem_pos + cl_start + q);
+          const uint4 *row = A.hr + (uint64_t)r * nch;
+          Acc<T> acc;
+          int c = lane;
+          for (; c + 192 < nch; c += 256) {
+            const uint4 v0 = row[c], v1 = row[c + 64], v2 = row[c + 128], v3 = row[c + 192];
+            acc.add(v0, F4[c]);
+            acc.add(v1, F4[c + 64]);
+            acc.add(v2, F4[c + 128]);
+            acc.add(v3, F4[c + 192]);
+          }
+          for (; c < nch; c += 64) acc.add(row[c], F4[c]);
+          acc.wave_reduce();
+          const uint64_t mp = q < A.mrow ? mc.info[q * 3] : A.mag_s[r];
+          const uint64_t key = q < A.mrow ? mc.key[q] : ld64(A.mkeys + cl_start + q);
+          const PS s = acc.finish(mp, sumF);
+          const double frac = (double)(2 * s.smin) / (double)(mp + sumF);
+          const double d = __builtin_fma(-frac, frac, 1.0) * 10000.0;
+          if (d < bd || (d == bd && key < bk)) {
+            bd = d;
+            bk = key;
+            bq = q;
+          }
+        }
+      } else
       for (uint64_t q = threadIdx.x; q < M; q += NT) {
         Acc<T> acc;
         uint64_t mp, key;
@@ -1252,11 +1481,11 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
 }
 
 // NCH: compile-time chunks per row (0: A.nch at run time).
-template <typename T, int NCH>
+template <typename T, int NCH, bool WIDE = false>
 __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
   extern __shared__ __attribute__((aligned(16))) uint4 dyn[];
-  if (blockIdx.x == 0) controller<T, NCH>(A, dyn);
-  else worker<T, NCH>(A, C, dyn);
+  if (blockIdx.x == 0) controller<T, NCH, WIDE>(A, dyn);
+  else worker<T, NCH, WIDE>(A, C, dyn);
 }
 
 __global__ void bits_init_kernel(uint32_t *bits, uint64_t n) {
@@ -1271,6 +1500,7 @@ struct AccPlan {
   const void *fn = nullptr;
   int res = 0;         // chunks per worker resident in its LDS (0: streaming)
   bool gbits = false;  // bitmap in global memory
+  bool wide = false;   // a wave per candidate (accum_kernel<T, 0, true>)
   uint32_t mrow = 0;   // member cache entries
   size_t lds = 0;
   uint32_t G = 0;
@@ -1282,6 +1512,9 @@ struct AccPlan {
 uint32_t accum_grid(const mc_ctx *c) {
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess) cus = 256;
+  // MC_ACCUM_GRID (tests): fewer workgroups, e.g. two ranks' kernels sharing one GPU
+  if (const char *g = getenv("MC_ACCUM_GRID")) cus = std::min(cus, atoi(g));
+  if (c->mb_world > 0 && c->mb_share > 1) cus /= c->mb_share;  // ranks sharing this GPU
   uint32_t G = (uint32_t)cus / 8 * 8;
   if (G > GMAX) G = GMAX;
   if (G < 8) G = 8;
@@ -1296,20 +1529,28 @@ bool accum_plan(const mc_ctx *c, uint32_t nb, AccPlan *pl) {
   if (c->norder >= (1ull << 31)) return false;
   const int nch = (int)((c->B * c->width + 15) / 16);
   const uint32_t G = accum_grid(c), GW = G - 1;
-  const uint64_t chunks = (c->norder + NT - 1) / NT;
+  const bool wide = nch >= WIDE_NCH && !getenv("MC_ACCUM_NARROW");
+  const uint64_t ts = wide ? NW : NT;
+  const uint64_t W = c->mb_world > 0 ? (uint64_t)c->mb_world : 1;
+  const uint64_t chunks = ((c->norder + ts - 1) / ts + W - 1) / W;  // this rank's tiles
+  if (chunks >= (1ull << 22)) return false;  // (Div32's range)
   const uint64_t per_w = (chunks + GW - 1) / GW;
   pl->G = G;
-  pl->fcap = per_w * NT;
-  pl->rec_g = (uint32_t)(4 * nch + REC_HDR);
-  pl->fn = c->width == 1 ? (nch == 16 ? reinterpret_cast<const void *>(&accum_kernel<uint8_t, 16>)
-                                      : reinterpret_cast<const void *>(&accum_kernel<uint8_t, 0>))
-                         : reinterpret_cast<const void *>(&accum_kernel<uint16_t, 0>);
+  pl->wide = wide;
+  pl->fcap = per_w * ts;
+  pl->rec_g = (uint32_t)(wide ? REC_HDR : 4 * nch + REC_HDR);
+  pl->fn = wide ? (c->width == 1 ? reinterpret_cast<const void *>(&accum_kernel<uint8_t, 0, true>)
+                                 : reinterpret_cast<const void *>(&accum_kernel<uint16_t, 0, true>))
+       : c->width == 1 ? (nch == 16 ? reinterpret_cast<const void *>(&accum_kernel<uint8_t, 16>)
+                                    : reinterpret_cast<const void *>(&accum_kernel<uint8_t, 0>))
+                       : reinterpret_cast<const void *>(&accum_kernel<uint16_t, 0>);
   const size_t static_lds = 12 * 1024;  // both roles' __shared__ words, with margin
   const size_t cap = 160 * 1024 - static_lds;
-  // worker: record words, alive flags, resident rows
-  const size_t wfix = (size_t)(pl->rec_g + 3) / 4 * 16 + (pl->fcap + 15) / 16 * 16;
+  // worker: record words, centre row (wide), alive flags, resident rows (not wide)
+  const size_t wfix = (size_t)(pl->rec_g + 3) / 4 * 16 + (wide ? (size_t)nch * 16 : 0) + (pl->fcap + 15) / 16 * 16;
   const size_t chunk_bytes = (size_t)nch * NT * 16;
-  pl->res = (!getenv("MC_ACCUM_STREAM") && wfix + per_w * chunk_bytes <= cap) ? (int)per_w : 0;
+  pl->res = (!wide && !getenv("MC_ACCUM_STREAM") && wfix + per_w * chunk_bytes <= cap) ? (int)per_w : 0;
+  if (wfix >= cap) return false;
   // controller: mean row, column sums, bvec (+ bitmap unless global), member cache
   auto cfix = [&](bool gbits) {
     size_t s = (size_t)nch * 16 + (size_t)c->B * 8;
@@ -1317,7 +1558,7 @@ bool accum_plan(const mc_ctx *c, uint32_t nb, AccPlan *pl) {
     if (!gbits) s += (size_t)((c->norder + 31) / 32 + 3) / 4 * 16;
     return s;
   };
-  const size_t per_entry = (size_t)(nch + 1) * 16 + sizeof(WinTab) + 24 + 8 + 4;
+  const size_t per_entry = (wide ? 0 : (size_t)(nch + 1) * 16) + sizeof(WinTab) + 24 + 8 + 4;
   // MC_ACCUM_GBITS=1 (tests): the global-bitmap variant that N >~ 900k needs, at any N
   for (int gb = getenv("MC_ACCUM_GBITS") ? 1 : 0; gb < 2; gb++) {
     const size_t f = cfix(gb != 0);
@@ -1334,6 +1575,10 @@ bool accum_plan(const mc_ctx *c, uint32_t nb, AccPlan *pl) {
 }
 
 }  // namespace
+
+uint64_t mailbox_slot_granules(uint32_t world, uint64_t n) {
+  return MBOX_HDR + (n + world - 1) / world + NT;  // header + the most positions a rank owns
+}
 
 bool accum_supported(const mc_ctx *c, uint32_t nb) {
   AccPlan pl;
@@ -1416,6 +1661,10 @@ int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, 
   A.cl_off = d_cl_off;
   A.out = d_out;
   A.budget = 20ull * 100000000ull;  // a single hand-off never takes 20 s: give up, report error 99
+  A.W = c->mb_world > 0 ? (uint32_t)c->mb_world : 1u;
+  A.rank = c->mb_world > 0 ? (uint32_t)c->mb_rank : 0u;
+  A.mbox = c->mb_world > 0 ? (uint64_t *)c->mb_dev : nullptr;
+  A.slot_g = mailbox_slot_granules(A.W, c->norder);
   A.prof = getenv("MC_ACCUM_PROFILE") ? 1 : 0;
   A.trace = nullptr;
   if (getenv("MC_ACCUM_PROFILE") && atoi(getenv("MC_ACCUM_PROFILE")) >= 2) {
@@ -1425,12 +1674,19 @@ int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, 
     A.trace_all = atoi(getenv("MC_ACCUM_PROFILE")) >= 3;
   }
   if (getenv("MC_ACCUM_PROFILE"))
-    fprintf(stderr, "[accum] variant: width %d nch %d resident chunks/worker %d global-bitmap %d member-cache %u lds %zu G %u\n",
-            c->width, nch, pl.res, (int)pl.gbits, pl.mrow, pl.lds, G);
+    fprintf(stderr, "[accum] variant: width %d nch %d wide %d resident chunks/worker %d global-bitmap %d member-cache %u lds %zu G %u rank %u/%u\n",
+            c->width, nch, (int)pl.wide, pl.res, (int)pl.gbits, pl.mrow, pl.lds, G, A.rank, A.W);
   DevClassifier cls = c->cls;
   void *args[] = {&A, &cls};
   timed_begin(c);
-  MCG_CHECK(hipLaunchCooperativeKernel(pl.fn, dim3(G), dim3(NT), args, (unsigned)pl.lds, c->stream));
+  // One workgroup per CU (the LDS plan admits no second): a cooperative launch guarantees
+  // they are all resident.  Several ranks' kernels (mailbox) may share a GPU in tests, where a
+  // second cooperative launch would wait for the first; they take a plain launch (every
+  // hand-off has its 20 s deadline either way).
+  if (A.mbox || getenv("MC_ACCUM_PLAIN_LAUNCH"))
+    MCG_CHECK(hipLaunchKernel(pl.fn, dim3(G), dim3(NT), args, (unsigned)pl.lds, c->stream));
+  else
+    MCG_CHECK(hipLaunchCooperativeKernel(pl.fn, dim3(G), dim3(NT), args, (unsigned)pl.lds, c->stream));
   timed_end(c, F_SCAN);
   return MC_OK;
 }

@@ -56,6 +56,7 @@ struct Acc<uint8_t> {
       dot += __shfl_xor(dot, o, 64);
     }
   }
+  __device__ __forceinline__ void wave_reduce();  // the whole wave's sums in every lane
   __device__ __forceinline__ PS finish(uint64_t magp, uint64_t magq) const {
     const uint32_t sa = sad + (s4[0] + s4[1]) + (s4[2] + s4[3]);
     const uint32_t dt = dot + (d4[0] + d4[1]) + (d4[2] + d4[3]);
@@ -127,6 +128,12 @@ __device__ __forceinline__ void wave_best_all(V &v, uint64_t &k, Better better) 
       (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)k, 63);
 }
 
+__device__ __forceinline__ void Acc<uint8_t>::wave_reduce() {
+  fold();
+  sad = wave_sum32_all(sad);
+  dot = wave_sum32_all(dot);
+}
+
 __device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int o) {
   uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
   lo = __shfl_xor(lo, o, 64);
@@ -163,6 +170,11 @@ struct Acc {
       sabs += shfl_xor64(sabs, o);
       sdot += shfl_xor64(sdot, o);
     }
+  }
+  __device__ __forceinline__ void wave_reduce() {
+    smin = wave_sum64_all(smin);
+    sabs = wave_sum64_all(sabs);
+    sdot = wave_sum64_all(sdot);
   }
   __device__ __forceinline__ PS finish(uint64_t, uint64_t) const { return PS{smin, sabs, sdot}; }
 };

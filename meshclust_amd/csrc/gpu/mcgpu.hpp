@@ -120,6 +120,10 @@ struct mc_ctx {
   std::vector<uint8_t> h_alive;
   mcg::Buf ident_s, al_a, al_b, al_out;
   mcg::Buf acc_out;  // device-resident accumulation: counters / error word
+  // several ranks sharing one accumulation (mc_set_mailbox): host-memory mailbox, mapped
+  void *mb_host = nullptr, *mb_dev = nullptr;
+  uint64_t mb_bytes = 0;
+  int mb_rank = 0, mb_world = 0, mb_share = 1;
   // scratch
   mcg::Buf s_a, s_b, s_c, s_d, s_e, s_f, s_g, s_h, s_i, s_j;
   std::vector<void *> pinned;
@@ -159,6 +163,7 @@ int launch_mean_shift(mc_ctx *c, const uint32_t *d_cid, uint32_t C, const uint64
                       uint32_t j1);
 int build_static(mc_ctx *c);
 bool accum_supported(const mc_ctx *c, uint32_t nb);
+uint64_t mailbox_slot_granules(uint32_t world, uint64_t n);  // mailbox granules per rank slot
 int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, uint32_t nb, double sim,
                  uint32_t *d_mem_pos, uint64_t *d_mkeys, uint32_t *d_cl_centre, uint64_t *d_cl_off, uint64_t *d_out);
 // nparts > 0: a sharded step (mc_scan_part) over this rank's static blocks only

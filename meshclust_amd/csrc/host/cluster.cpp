@@ -2,7 +2,10 @@
 #include "cluster.hpp"
 
 #include <fcntl.h>
+#include <sys/mman.h>
 #include <unistd.h>
+
+#include <chrono>
 
 #include <algorithm>
 #include <cerrno>
@@ -196,6 +199,66 @@ void sharded_step(mc_ctx *ctx, const ShardComm &comm, uint32_t centre, uint64_t 
   res->n_flagged = total;
 }
 
+// The ranks' step mailbox for the device-sharded accumulation (mc_set_mailbox): a POSIX
+// shared-memory segment that rank 0 creates and every rank maps (one process per GPU, or the
+// threads of one process), registered with each rank's context.  Collective over `comm`;
+// every rank learns whether all of them attached, so they all take the same path.
+struct SharedMailbox {
+  void *p = nullptr;
+  size_t bytes = 0;
+  mc_ctx *ctx = nullptr;
+  ~SharedMailbox() {
+    if (ctx) mc_set_mailbox(ctx, nullptr, 0, 0, 0, 1);
+    if (p) munmap(p, bytes);
+  }
+};
+
+static bool attach_mailbox(const ShardComm &comm, mc_ctx *ctx, uint64_t n, SharedMailbox &mb) {
+  struct Blk {
+    char name[56];
+    int32_t ok, pad;
+    char pci[64];  // this rank's GPU: ranks on one GPU split its CUs
+  };
+  static_assert(sizeof(Blk) == 128, "mailbox exchange block");
+  const int W = comm.world;
+  const size_t bytes = mc_mailbox_bytes(W, n);
+  Blk mine{};
+  if (mc_ctx_pci_bus_id(ctx, mine.pci, sizeof mine.pci) != MC_OK) mine.pci[0] = 0;
+  int fd = -1;
+  if (comm.rank == 0) {
+    snprintf(mine.name, sizeof mine.name, "/mcl_mbox_%d_%llx", (int)getpid(),
+             (unsigned long long)std::chrono::steady_clock::now().time_since_epoch().count());
+    fd = shm_open(mine.name, O_CREAT | O_EXCL | O_RDWR, 0600);
+    mine.ok = fd >= 0 && ftruncate(fd, (off_t)bytes) == 0;  // (zero-filled: no granule carries a tag)
+  }
+  std::vector<Blk> all(W);
+  if (comm.allgather(comm.user, &mine, sizeof mine, all.data()) != 0)
+    throw Error("mailbox all-gather across ranks failed", 1);
+  bool ok = all[0].ok != 0;
+  if (ok && comm.rank != 0) fd = shm_open(all[0].name, O_RDWR, 0600);
+  if (ok && fd >= 0) {
+    void *p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    if (p != MAP_FAILED) {
+      mb.p = p;
+      mb.bytes = bytes;
+    }
+  }
+  if (fd >= 0) close(fd);
+  int share = 0;
+  for (const auto &b : all) share += strncmp(b.pci, mine.pci, sizeof mine.pci) == 0;
+  if (mb.p && mc_set_mailbox(ctx, mb.p, bytes, comm.rank, W, std::max(share, 1)) == MC_OK) mb.ctx = ctx;
+  mine.ok = mb.ctx != nullptr;
+  if (comm.allgather(comm.user, &mine, sizeof mine, all.data()) != 0)
+    throw Error("mailbox all-gather across ranks failed", 1);
+  if (comm.rank == 0 && all[0].name[0]) shm_unlink(all[0].name);  // every rank has mapped it (or failed)
+  for (const auto &b : all) ok &= b.ok != 0;
+  if (!ok && mb.ctx) {
+    mc_set_mailbox(ctx, nullptr, 0, 0, 0, 1);
+    mb.ctx = nullptr;
+  }
+  return ok;
+}
+
 // accumulate (ClusterFactory.cpp:637-714): grow one cluster around `last` until get_close
 // finds no similar candidate; returns the next seed through *last_ptr.  With `shard`, every
 // get_close step is split over the ranks (sharded_step).
@@ -315,10 +378,17 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
   // MC_SHARD_FORCE=1 (tests) takes the sharded code path with a single rank too.
   const bool multi = cfg.comm && (cfg.comm->world > 1 || getenv("MC_SHARD_FORCE"));
   const ShardComm *shard = (multi && !memo && cfg.width <= 2 && !getenv("MC_SHARD_REPLICATE")) ? cfg.comm : nullptr;
+  // Sharded ranks run ONE device-resident loop together: every rank's persistent kernel
+  // scans its tiles and the kernels exchange each step through the shared mailbox
+  // (mc_set_mailbox); MC_SHARD_HOST_STEPS=1, or a mailbox that cannot be attached on every
+  // rank, keeps the host-driven sharded steps (mc_scan_part + all-gather + mc_scan_commit).
+  SharedMailbox mbox;
+  const bool dev_shard = shard && !getenv("MC_SHARD_HOST_STEPS") && !getenv("MC_ACCUM_STEPS") &&
+                         attach_mailbox(*shard, ctx, order.size(), mbox);
   // The device-resident loop (mc_accumulate) unless alignment mode or the configuration
   // asks for the step API; MC_ACCUM_STEPS=1 forces the host-driven loop (both are GPU paths).
   bool done = false;
-  if (shard) {
+  if (shard && !dev_shard) {
     stats.accum_path = "sharded steps x" + std::to_string(shard->world);
   } else if (!memo && !getenv("MC_ACCUM_STEPS")) {
     Scope s(timer, "accumulate");
@@ -340,9 +410,11 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
       timer.add("accumulate.dev_wait", st[3] / 1000.0);
       timer.add("accumulate.dev_collect", st[4] / 1000.0);
       done = true;
-      stats.accum_path = "device";
+      stats.accum_path = dev_shard ? "device x" + std::to_string(shard->world) : "device";
     } else if (rc != MC_ERR_UNSUPPORTED) {
       check(rc, "mc_accumulate");
+    } else if (dev_shard) {  // (every rank: the same configuration) -> the host-driven sharded steps
+      stats.accum_path = "sharded steps x" + std::to_string(shard->world);
     } else {
       // both loops are GPU paths and give identical partitions; say which one ran
       stats.accum_path = std::string("steps (") + mc_last_error() + ")";

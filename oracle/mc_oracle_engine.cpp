@@ -412,6 +412,18 @@ int mc_accumulate(mc_ctx *, const uint32_t *, const uint64_t *, uint32_t, double
   return fail(MC_ERR_UNSUPPORTED, "the CPU oracle engine drives accumulation step by step");
 }
 
+// The device-sharded accumulation's mailbox is read by the ranks' persistent kernels; the CPU
+// engine's ranks take the host-driven sharded steps instead.
+uint64_t mc_mailbox_bytes(int world, uint64_t n) { return world < 1 ? 0 : 2ull * world * (8 + n / world + 513) * 8; }
+int mc_ctx_pci_bus_id(mc_ctx *, char *buf, int len) {
+  if (!buf || len < 16) return MC_ERR_ARG;
+  snprintf(buf, len, "cpu");
+  return MC_OK;
+}
+int mc_set_mailbox(mc_ctx *, void *, uint64_t, int, int world, int) {
+  return world == 0 ? MC_OK : fail(MC_ERR_UNSUPPORTED, "no device-sharded accumulation in the CPU oracle engine");
+}
+
 // RCCL is a GPU-side transport: the CPU engine's ranks exchange through the caller's callback.
 int mc_comm_unique_id(uint8_t *) { return fail(MC_ERR_UNSUPPORTED, "no RCCL in the CPU oracle engine"); }
 int mc_comm_create(int, int, int, const uint8_t *, mc_comm **) {

@@ -41,12 +41,20 @@ def e2e_input(name, tmpdir):
     """Regenerate the FASTA of an e2e golden and check its SHA-256 against the manifest."""
     import hashlib
     import importlib.util
-    spec = manifest()["e2e"][name]
+    man = manifest()
+    spec = man["e2e"][name] if name in man["e2e"] else man["e2e_gpu"][name]
     path = os.path.join(str(tmpdir), name + ".fa")
     gen = spec["generator"]
     mg = importlib.util.spec_from_file_location("make_golden", golden("make_golden.py"))
     mod = importlib.util.module_from_spec(mg)
     mg.loader.exec_module(mod)
+    if gen[0] == "multi":
+        # several input files: the first is returned as the input, the others lead the flags
+        gen = ("multi", [(b, tuple(s)) for b, s in gen[1]])
+        h = mod.make_input(gen, path)
+        files = mod.multi_paths(gen, path)
+        assert h == spec["sha256"], "synthetic generator drifted for %s" % name
+        return files[0], files[1:] + spec["flags"]
     mod.make_input(tuple(gen), path)
     h = hashlib.sha256(open(path, "rb").read()).hexdigest()
     assert h == spec["sha256"], "synthetic generator drifted for %s" % name

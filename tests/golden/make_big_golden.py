@@ -39,6 +39,9 @@ REF = os.path.join(ROOT, "oracle", "_ref", "meshclust")
 BIG = {
     "B100k": ((100000, 1000, 1000, 0.03, 41), ["--id", "0.90"]),
     "D1M": ((1000000, 1000, 10000, 0.03, 51), ["--id", "0.90"]),
+    # config D's shape (10 reads per template, 10,000 clusters) at a size the serial
+    # reference finishes in about an hour
+    "D100k": ((100000, 1000, 10000, 0.03, 51), ["--id", "0.90"]),
 }
 
 

@@ -56,6 +56,18 @@ E2E = {
     "al300": ((300, 500, 10, 0.03, 7), ["--align", "--id", "0.9"]),
     "al_fam400_id55": (("family", 400, 16, 4, 0.25, 0.05, 31), ["--id", "0.55"]),
     "al_mix300": (("mixed", 300, 10, 0.08, 32), ["--align", "--id", "0.8", "--delta", "3"]),
+    # two input files given out of basename order, with different mean lengths: the basename
+    # sort, find_k's per-file integer mean (k = 5 here; the pooled mean would give k = 4) and
+    # the ids numbered across files (Runner.cpp:253-262, 265-292)
+    "two_files": (("multi", [("zz_long", (300, 2000, 10, 0.03, 81)),
+                             ("aa_short", (900, 300, 30, 0.03, 82))]), ["--id", "0.90"]),
+}
+# Goldens only the GPU tests use (the CPU harness would take as long as the reference):
+# config C's shape (100 reads per template, 1 kb, --id 0.55 --align) at 2,000
+# reads, and its 0.15-mutation variant whose identities straddle 0.55.
+E2E_GPU = {
+    "c2k_al55": ((2000, 1000, 20, 0.03, 41), ["--id", "0.55", "--align"]),
+    "c2k_m15_al55": ((2000, 1000, 20, 0.15, 41), ["--id", "0.55", "--align"]),
 }
 TRAIN = {"a1k": ("a1k", 3, 0.90)}
 
@@ -150,7 +162,21 @@ def noisy_reads(n, n_templates, mut, seed, length=1000):
         yield hdr, bytes(s)
 
 
+def multi_paths(spec, path):
+    """Files of a ("multi", [(basename, spec), ...]) input, in command-line order."""
+    d = path[:-3] + "_files"
+    return [os.path.join(d, b + ".fa") for b, _ in spec[1]]
+
+
 def make_input(spec, path):
+    if spec[0] == "multi":
+        # one FASTA per part; headers prefixed with the part's basename so they stay unique
+        h = hashlib.sha256()
+        for (b, sub), fp in zip(spec[1], multi_paths(spec, path)):
+            os.makedirs(os.path.dirname(fp), exist_ok=True)
+            synth.write_fasta(fp, ((b.encode() + b"_" + hdr, seq) for hdr, seq in synth.reads(*sub)))
+            h.update(sha256(fp).encode())
+        return h.hexdigest()
     if spec[0] == "noisy":
         _, n, t, mut, seed = spec
         synth.write_fasta(path, noisy_reads(n, t, mut, seed))
@@ -391,8 +417,9 @@ def golden_train(name, fa, k, ident, npts=40):
 def golden_e2e(name, spec, flags, tmp):
     fa = os.path.join(tmp, name + ".fa")
     digest = make_input(spec, fa)
+    files = multi_paths(spec, fa) if spec[0] == "multi" else [fa]
     out = os.path.join(tmp, name + ".clstr")
-    log = subprocess.run([REF, fa] + flags + ["--threads", "1", "--output", out],
+    log = subprocess.run([REF] + files + flags + ["--threads", "1", "--output", out],
                          capture_output=True, text=True)
     if log.returncode != 0:
         raise RuntimeError("reference failed on %s: %s" % (name, log.stderr[-2000:]))
@@ -421,10 +448,19 @@ def main():
                 fa = os.path.join(tmp, e2e_name + "_train.fa")
                 make_input(E2E[e2e_name][0], fa)
                 golden_train(name, fa, k, ident)
-        todo = [(n, s, f) for n, (s, f) in E2E.items() if want is None or n in want]
+        todo = [("e2e", n, s, f) for n, (s, f) in E2E.items() if want is None or n in want]
+        todo += [("e2e_gpu", n, s, f) for n, (s, f) in E2E_GPU.items() if want is not None and n in want]
+        results = {}
         with ThreadPoolExecutor(max_workers=6) as ex:
-            for name, meta in ex.map(lambda a: golden_e2e(a[0], a[1], a[2], tmp), todo):
-                manifest["e2e"][name] = meta
+            for (sec, *_), (name, meta) in zip(todo, ex.map(lambda a: golden_e2e(a[1], a[2], a[3], tmp), todo)):
+                results.setdefault(sec, {})[name] = meta
+    # re-read: make_big_golden.py may have updated the manifest while the reference ran
+    fresh = json.load(open(man_path)) if os.path.exists(man_path) else {}
+    for key in ("big", "configs"):
+        if key in fresh:
+            manifest[key] = fresh[key]
+    for sec, metas in results.items():
+        manifest.setdefault(sec, {}).update(metas)
     with open(man_path, "w") as f:
         json.dump(manifest, f, indent=1, sort_keys=True)
 

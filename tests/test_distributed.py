@@ -16,6 +16,7 @@ import socket
 import subprocess
 import sys
 
+import numpy as np
 import pytest
 
 import fixtures
@@ -30,23 +31,35 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _run_world(name, tmp_path, gpu, world=2, rccl=False, env_extra=None):
-    fa, flags = fixtures.e2e_input(name, tmp_path)
-    out = str(tmp_path / (name + ".clstr"))
+def _launch(fa, flags, out, gpu, world, rccl=False, env_extra=None, timeout=600):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), WORKER]
     cmd += (["--gpu"] if gpu else []) + (["--rccl"] if rccl else []) + [fa, out, "--"] + flags
     env = dict(os.environ, OMP_NUM_THREADS="2", **(env_extra or {}))
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
-    with gzip.open(fixtures.golden("e2e_%s.clstr.gz" % name), "rb") as f:
-        assert open(out, "rb").read() == f.read()
     ranks = [json.load(open(out + ".rank%d.json" % i)) for i in range(world)]
     for rk in ranks:
-        assert rk["accum_path"] == "sharded steps x%d" % world, rk["accum_path"]
-        # one exchange per get_close step (+ the long-list ones) and one per mean-shift iteration
-        assert rk["calls"] >= rk["scan_steps"] > 0 and rk["calls"] == ranks[0]["calls"]
         assert rk["clusters"] == ranks[0]["clusters"]
+    return ranks
+
+
+def _run_world(name, tmp_path, gpu, world=2, rccl=False, env_extra=None):
+    """Rank 0's .clstr against the reference golden.  The GPU ranks run ONE device-resident
+    accumulation together (mailbox exchange between their kernels: "device xW"), unless
+    MC_SHARD_HOST_STEPS asks for the host-driven sharded steps (one all-gather per step: the
+    CPU engine's only form)."""
+    fa, flags = fixtures.e2e_input(name, tmp_path)
+    out = str(tmp_path / (name + ".clstr"))
+    ranks = _launch(fa, flags, out, gpu, world, rccl, env_extra)
+    with gzip.open(fixtures.golden("e2e_%s.clstr.gz" % name), "rb") as f:
+        assert open(out, "rb").read() == f.read()
+    host_steps = not gpu or "MC_SHARD_HOST_STEPS" in (env_extra or {})
+    for rk in ranks:
+        assert rk["accum_path"] == ("sharded steps x%d" if host_steps else "device x%d") % world, rk["accum_path"]
+        assert rk["calls"] == ranks[0]["calls"]
+        if host_steps:  # one exchange per get_close step (+ the long-list ones) and per iteration
+            assert rk["calls"] >= rk["scan_steps"] > 0
     return ranks
 
 
@@ -61,12 +74,86 @@ def test_sharded_gloo_cpu_byte_identical(cpu_lib, name, world, tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["a1k", "fam2k", "m2k_id80", "big2_3k"])
+@pytest.mark.parametrize("name", ["a1k", "fam2k", "m2k_id80", "big2_3k", "s1k_k5"])
 def test_world2_gpu_byte_identical(name, tmp_path):
+    """Two ranks' kernels on the one GPU of the test box (each takes half of the CUs), the
+    step exchange through the shared host-memory mailbox, gloo for the mean-shift all-gather."""
     _run_world(name, tmp_path, gpu=True)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["a1k", "fam2k"])
-def test_rccl_sharded_path_gpu_byte_identical(name, tmp_path):
-    _run_world(name, tmp_path, gpu=True, world=1, rccl=True, env_extra={"MC_SHARD_FORCE": "1"})
+@pytest.mark.parametrize("name", ["fam2k", "big2_3k"])
+def test_world2_gpu_host_steps_byte_identical(name, tmp_path):
+    _run_world(name, tmp_path, gpu=True, env_extra={"MC_SHARD_HOST_STEPS": "1"})
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,env", [("a1k", {}), ("fam2k", {}), ("fam2k", {"MC_SHARD_HOST_STEPS": "1"})])
+def test_rccl_sharded_path_gpu_byte_identical(name, env, tmp_path):
+    _run_world(name, tmp_path, gpu=True, world=1, rccl=True, env_extra=dict(env, MC_SHARD_FORCE="1"))
+
+
+# ---- the sharded paths at the BASELINE sizes --------------------------------------------
+sys.path.insert(0, fixtures.GOLDEN)
+import make_big_golden as BG  # noqa: E402
+
+
+def _big_input(name):
+    from meshclust_amd import synth
+    gen, _ = BG.BIG[name]
+    d = os.environ.get("MC_TEST_CACHE", os.path.join("/tmp", "mc_test_cache_%d" % os.getuid()))
+    os.makedirs(d, exist_ok=True)
+    fa = os.path.join(d, "%s.fa" % name)
+    if not os.path.exists(fa):
+        synth.generate(fa + ".tmp", *gen)
+        os.replace(fa + ".tmp", fa)
+    return fa
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("world,rccl,env", [(1, True, {"MC_SHARD_FORCE": "1"}),
+                                            (1, True, {"MC_SHARD_FORCE": "1", "MC_SHARD_HOST_STEPS": "1"}),
+                                            (2, False, {})])
+def test_sharded_B100k_equals_reference(world, rccl, env, tmp_path):
+    """Config B (100k x 1 kb) through the sharded paths against the reference's partition."""
+    g = np.load(fixtures.golden("cfg_B100k.npz"))
+    fa = _big_input("B100k")
+    out = str(tmp_path / "B100k.clstr")
+    ranks = _launch(fa, ["--id", "0.90"], out, True, world, rccl, env, timeout=800)
+    want = "sharded steps x%d" if "MC_SHARD_HOST_STEPS" in env else "device x%d"
+    assert ranks[0]["accum_path"] == want % world
+    assert BG.canonical_digest(BG.clusters_of(out)) == str(g["digest"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,env", [(1, {"MC_SHARD_FORCE": "1"}), (2, {})])
+def test_sharded_E91_equals_reference(world, env, tmp_path):
+    """Config E (k = 6, the wide accumulation rows) through the sharded path."""
+    import clstr
+    from meshclust_amd import synth
+    fa = str(tmp_path / "E91.fa")
+    synth.write_fasta(fa, synth.families(7, 13, 8000, 12000, 0.05, 0.15, 61))
+    out = str(tmp_path / "E91.clstr")
+    ranks = _launch(fa, ["--id", "0.80"], out, True, world, world == 1, env)
+    assert ranks[0]["accum_path"] == "device x%d" % world
+    assert clstr.canonical(out) == clstr.canonical(fixtures.golden("cfg_E91.clstr.gz"))
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(1200)
+def test_sharded_D1M_equals_single_gpu(tmp_path):
+    """Config D (1M x 1 kb, 10,000 templates): two ranks' kernels sharing the accumulation
+    give the single-GPU device loop's partition and centres (no reference partition exists at
+    this size; tests/test_gpu_configs.py pins the device loop against the host-driven steps)."""
+    import meshclust_amd as M
+    M.build()
+    fa = _big_input("D1M")
+    one = str(tmp_path / "D1M.one.clstr")
+    r = subprocess.run([M.BIN, fa, "--id", "0.90", "--output", one, "--quiet", "--threads", "16"],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = str(tmp_path / "D1M.two.clstr")
+    ranks = _launch(fa, ["--id", "0.90"], out, True, 2, False, {}, timeout=900)
+    assert ranks[0]["accum_path"] == "device x2"
+    assert BG.canonical_digest(BG.clusters_of(out)) == BG.canonical_digest(BG.clusters_of(one))

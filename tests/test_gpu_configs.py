@@ -52,12 +52,16 @@ def product():
     return M.BIN
 
 
-def test_config_E91_partition_equals_reference(product, tmp_path):
+@pytest.mark.parametrize("env", [{}, {"MC_ACCUM_NARROW": "1"}, {"MC_ACCUM_STEPS": "1"}])
+def test_config_E91_partition_equals_reference(product, tmp_path, env):
+    """k = 6 (4 KiB rows): the accumulation kernel's wide form (default), its lane-per-candidate
+    form and the host-driven get_close steps, each against the reference's partition."""
     fa = str(tmp_path / "E91.fa")
     synth.write_fasta(fa, synth.families(7, 13, 8000, 12000, 0.05, 0.15, 61))
     out = str(tmp_path / "E91.clstr")
-    st = _run(fa, ["--id", "0.80"], out, 300)
+    st = _run(fa, ["--id", "0.80"], out, 300, env)
     assert st["k"] == 6 and st["n"] == 91
+    assert st["accum_path"] == ("device" if "MC_ACCUM_STEPS" not in env else "steps (MC_ACCUM_STEPS)")
     assert clstr.canonical(out) == clstr.canonical(fixtures.golden("cfg_E91.clstr.gz"))
 
 

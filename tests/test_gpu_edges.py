@@ -110,3 +110,26 @@ def test_clusters_past_member_cache_equal_reference(eng, tmp_path, steps):
     assert r.returncode == 0, r.stderr[-3000:]
     with gzip.open(fixtures.golden("e2e_big2_3k.clstr.gz"), "rb") as f:
         assert open(out, "rb").read() == f.read()
+
+
+# The accumulation kernel's row variants (accum.hip): rows of >= 512 bytes take the wide form
+# (a wave per candidate, NW-candidate tiles, column sums and closest member from the row-major
+# copy); MC_ACCUM_NARROW keeps the lane-per-candidate form.  k = 5 at 8 bits (1 KiB rows) and
+# k = 4 forced to 16 bits (512-byte rows: the same feature values as the reference's 8-bit
+# ones, so the same output) against the reference's own .clstr; big2_3k's 1,500-member
+# clusters flag more than the controller's 1,024-entry step list in one step.
+@pytest.mark.parametrize("name,env,wide", [("s1k_k5", {}, True), ("s1k_k5", {"MC_ACCUM_NARROW": "1"}, False),
+                                           ("big2_3k", {"MC_FORCE_WIDTH": "2"}, True),
+                                           ("fam2k", {"MC_FORCE_WIDTH": "2"}, True),
+                                           ("fam2k", {"MC_FORCE_WIDTH": "2", "MC_ACCUM_NARROW": "1"}, False)])
+def test_accum_row_variants_equal_reference(eng, tmp_path, name, env, wide):
+    fa, flags = fixtures.e2e_input(name, tmp_path)
+    out = str(tmp_path / "o.clstr")
+    st = str(tmp_path / "st.json")
+    r = subprocess.run([M.BIN, fa] + flags + ["--output", out, "--stats-json", st, "--quiet"], capture_output=True,
+                       text=True, timeout=600, env=dict(os.environ, MC_ACCUM_PROFILE="1", **env))
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert json.load(open(st))["accum_path"] == "device"
+    assert ("wide %d" % int(wide)) in r.stderr
+    with gzip.open(fixtures.golden("e2e_%s.clstr.gz" % name), "rb") as f:
+        assert open(out, "rb").read() == f.read()

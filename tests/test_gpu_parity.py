@@ -232,7 +232,9 @@ def test_nw_loaded_sequences(eng, a1k):
     assert np.array_equal(ident, pos[:64, 2])
 
 
-E2E = sorted(fixtures.manifest()["e2e"])
+# every e2e golden, plus the ones only the GPU runs in reasonable time: config C's shape at
+# 2,000 reads (--id 0.55 --align: one NW per centre x candidate, memoised, Feature.cpp:221-243)
+E2E = sorted(fixtures.manifest()["e2e"]) + sorted(fixtures.manifest().get("e2e_gpu", {}))
 
 
 @pytest.mark.parametrize("name", E2E)
