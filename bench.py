@@ -132,6 +132,7 @@ def main():
     import meshclust_amd as M
     if rank == 0 and not os.path.exists(M.GPU_LIB):
         M.build()
+    M.tune_host_heap()  # this process runs many clusterings: keep large freed blocks
     if shard and world == 1:
         os.environ["MC_SHARD_FORCE"] = "1"  # the sharded code path with one rank
     if shard and rank == 0:  # one shared input: rank 0 writes it, the others wait

@@ -121,8 +121,15 @@ def host_lib():
         lib.mcl_run_sharded.restype = C.c_int
         lib.mcl_run_sharded.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_char_p), C.c_int, C.c_char_p,
                                         C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+        lib.mcl_tune_host_heap.restype = C.c_int
         _host = lib
     return _host
+
+
+def tune_host_heap():
+    """Opt in (process-global): keep large freed host blocks in the heap, so repeated parses and
+    clusterings in this process touch no new pages (what bin/meshclust does for itself)."""
+    return bool(host_lib().mcl_tune_host_heap())
 
 
 def _check(rc, what):

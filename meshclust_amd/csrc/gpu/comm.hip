@@ -10,9 +10,12 @@
 #include <dlfcn.h>
 #include <rccl/rccl.h>
 
+#include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 
 #include "mcgpu.hpp"
 
@@ -115,6 +118,10 @@ int mc_comm_create(int device, int rank, int world, const uint8_t *id, mc_comm *
 
 int mc_comm_allgather(mc_comm *c, const void *in, uint64_t bytes, void *out) {
   if (!c || (bytes && (!in || !out))) return MC_ERR_ARG;
+  if (!c->comm) {
+    mcg::set_error("RCCL communicator was aborted");
+    return MC_ERR_STATE;
+  }
   const Rccl &r = rccl();
   c->calls++;
   c->bytes += bytes * (uint64_t)c->world;
@@ -140,7 +147,23 @@ int mc_comm_allgather(mc_comm *c, const void *in, uint64_t bytes, void *out) {
   ncclResult_t e = r.all_gather(c->d_send, c->d_recv, bytes, ncclUint8, c->comm, c->stream);
   if (e != ncclSuccess) return rccl_fail(e, "ncclAllGather");
   MCG_CHECK(hipMemcpyAsync(c->h_recv, c->d_recv, bytes * c->world, hipMemcpyDeviceToHost, c->stream));
-  MCG_CHECK(hipStreamSynchronize(c->stream));
+  // A rank that failed before this all-gather never joins it: wait with a deadline
+  // (MC_COMM_TIMEOUT_S, default 300 s) and abort the communicator, so every waiting rank
+  // returns an error instead of blocking forever.
+  const double limit = getenv("MC_COMM_TIMEOUT_S") ? atof(getenv("MC_COMM_TIMEOUT_S")) : 300.0;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t it = 0;; it++) {
+    const hipError_t q = hipStreamQuery(c->stream);
+    if (q == hipSuccess) break;
+    if (q != hipErrorNotReady) return mcg::hip_fail(q, "all-gather stream");
+    if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit) {
+      r.abort(c->comm);
+      c->comm = nullptr;
+      mcg::set_error("RCCL all-gather timed out (a rank did not join: MC_COMM_TIMEOUT_S)");
+      return MC_ERR_HIP;
+    }
+    if (it > 2000) std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
   memcpy(out, c->h_recv, bytes * c->world);
   return MC_OK;
 }

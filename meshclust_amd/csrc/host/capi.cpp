@@ -23,6 +23,10 @@ void *mcl_parse(const char *const *files, int nfiles, int threads, char *err, in
 
 uint64_t mcl_num_seqs(void *ds) { return ((mc::Dataset *)ds)->size(); }
 
+// Opt-in for a host process that runs many clusterings: keep large freed blocks in the heap
+// (runner.cpp tune_host_heap).  Process-global, so never done implicitly by the library.
+int mcl_tune_host_heap(void) { return mc::tune_host_heap() ? 1 : 0; }
+
 // Read-only view of a parsed dataset (what the reference's Chromosome objects hold after
 // ChromListMaker::makeChromOneDigitList): the concatenated one-digit codes with per-record
 // offsets, the [start, end] segment pairs with per-record pair offsets.  Pointers stay valid

@@ -19,6 +19,14 @@
 
 namespace mc {
 
+void fault_point(const ShardComm *comm, const char *stage) {
+  const char *f = getenv("MC_FAULT");
+  if (!f || !comm) return;
+  const char *colon = strchr(f, ':');
+  if (colon && atoi(f) == comm->rank && strcmp(colon + 1, stage) == 0)
+    throw Error(std::string("injected fault (MC_FAULT) at ") + stage + " on rank " + std::to_string(comm->rank), 1);
+}
+
 namespace {
 
 // Replay of Feature::align's memo table (Feature.cpp:221-243) for alignment mode.
@@ -382,6 +390,7 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
   // scans its tiles and the kernels exchange each step through the shared mailbox
   // (mc_set_mailbox); MC_SHARD_HOST_STEPS=1, or a mailbox that cannot be attached on every
   // rank, keeps the host-driven sharded steps (mc_scan_part + all-gather + mc_scan_commit).
+  fault_point(cfg.comm, "accumulate");
   SharedMailbox mbox;
   const bool dev_shard = shard && !getenv("MC_SHARD_HOST_STEPS") && !getenv("MC_ACCUM_STEPS") &&
                          attach_mailbox(*shard, ctx, order.size(), mbox);
@@ -453,21 +462,24 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
       // this rank's share of the centres, then the centre-reassignment all-gather
       const uint32_t W = (uint32_t)cfg.comm->world, per = (C + W - 1) / W;
       const uint32_t j0 = std::min<uint32_t>(C, per * (uint32_t)cfg.comm->rank), j1 = std::min<uint32_t>(C, j0 + per);
-      std::vector<uint32_t> mine(per, 0), all((size_t)per * W, 0);
-      // a failed rank sends ids no read can have, so every rank stops after the same exchange
+      // block: [status word, this rank's `per` new centres]; a failed rank sends status 1, so
+      // every rank (also one whose share is empty, C < W) stops after the same exchange
+      const uint32_t blk = per + 1;
+      std::vector<uint32_t> mine(blk, 0), all((size_t)blk * W, 0);
       std::string ms_err;
       try {
-        check(mc_mean_shift_range(ctx, cids.data(), C, off.data(), members.data(), cfg.delta, j0, j1, mine.data()),
+        fault_point(cfg.comm, "update");
+        check(mc_mean_shift_range(ctx, cids.data(), C, off.data(), members.data(), cfg.delta, j0, j1, mine.data() + 1),
               "mc_mean_shift_range");
       } catch (const std::exception &e) {
         ms_err = e.what();
-        std::fill(mine.begin(), mine.end(), 0xffffffffu);
+        mine[0] = 1;
       }
-      if (cfg.comm->allgather(cfg.comm->user, mine.data(), (uint64_t)per * 4, all.data()) != 0)
+      if (cfg.comm->allgather(cfg.comm->user, mine.data(), (uint64_t)blk * 4, all.data()) != 0)
         throw Error("centre all-gather across ranks failed", 1);
-      for (uint32_t j = 0; j < C; j++)
-        if (all[j] == 0xffffffffu) throw Error(ms_err.empty() ? "mean-shift update failed on another rank" : ms_err, 1);
-      std::copy(all.begin(), all.begin() + C, newc.begin());
+      for (uint32_t r = 0; r < W; r++)
+        if (all[(size_t)r * blk]) throw Error(ms_err.empty() ? "mean-shift update failed on rank " + std::to_string(r) : ms_err, 1);
+      for (uint32_t j = 0; j < C; j++) newc[j] = all[(size_t)(j / per) * blk + 1 + j % per];
     } else if (C && !memo) {
       Scope sm(timer, "update.mean_shift");
       check(mc_mean_shift(ctx, cids.data(), C, off.data(), members.data(), cfg.delta, newc.data()), "mc_mean_shift");

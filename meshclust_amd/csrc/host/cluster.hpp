@@ -29,6 +29,11 @@ struct ShardComm {
   void *user = nullptr;
 };
 
+// Fault injection for the multi-rank tests: MC_FAULT=<rank>:<stage> makes that rank throw at
+// that stage ("upload", "train", "accumulate", "update"), so the tests can check that every
+// other rank stops with an error instead of waiting in an exchange forever.
+void fault_point(const ShardComm *comm, const char *stage);
+
 struct ClusterConfig {
   const ShardComm *comm = nullptr;  // null: one rank
   double sim = 0.90;

@@ -329,16 +329,6 @@ void parse_chunk(const char *buf, size_t a, size_t z, bool first, bool eof, cons
 
 }  // namespace
 
-// Large blocks stay in the heap once freed (no mmap / munmap per block, no trimming), so a
-// repeated parse or run touches no new pages (the driver does the same: runner.cpp).
-static void keep_heap() {
-  static std::once_flag once;
-  std::call_once(once, [] {
-    mallopt(M_MMAP_THRESHOLD, 1 << 30);
-    mallopt(M_TRIM_THRESHOLD, 1 << 30);
-  });
-}
-
 void parse_fasta_files(const std::vector<std::string> &files, Dataset &ds, int threads) {
   if (threads < 1) threads = 1;
   if (ds.seq_off.empty()) {
@@ -368,7 +358,6 @@ void parse_fasta_files(const std::vector<std::string> &files, Dataset &ds, int t
     // cache as copies, and a repeated parse reuses the heap's already-touched pages (the
     // heap keeps large blocks, see keep_heap), where an mmap pays page-table population and
     // teardown for every file (MAP_POPULATE + munmap: 13 ms of a 30 ms parse of 100 MB).
-    keep_heap();
     std::unique_ptr<char, void (*)(void *)> mem((char *)malloc(n + 64), free);
     if (!mem) {
       close(fd);

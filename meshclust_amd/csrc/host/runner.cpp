@@ -10,7 +10,10 @@
 #include <cerrno>
 #include <chrono>
 #include <cmath>
+#include <atomic>
+#include <condition_variable>
 #include <exception>
+#include <mutex>
 #include <thread>
 #include <cstdio>
 #include <cstdlib>
@@ -123,20 +126,19 @@ static int find_k(const Dataset &ds, bool verbose) {
   return newk;
 }
 
-// The training sampler allocates ~150 MB of short-lived host arrays per clustering (split keys,
-// the per-pivot sort inputs).  Keep freed blocks in the heap instead of returning them to the
-// kernel, so repeated clusterings in one process (serving, bench.py) do not pay the page
-// faults again.  Process-wide, set once.
-static void keep_host_heap() {
-  static bool done = false;
-  if (done) return;
-  done = true;
-  mallopt(M_MMAP_THRESHOLD, 1 << 30);
-  mallopt(M_TRIM_THRESHOLD, 1 << 30);
+// The parser's file buffer and the training sampler's short-lived arrays (~150 MB per
+// clustering at config B: split keys, the per-pivot sort inputs) are large blocks.  This keeps
+// freed blocks in the heap -- no mmap for large blocks (M_MMAP_MAX 0: glibc caps
+// M_MMAP_THRESHOLD at 32 MiB, so a threshold cannot cover them), no trimming -- so repeated
+// parses and clusterings in one process touch no new pages.  Process-global: the CLI calls it
+// for its own process; a host embedding the library opts in with mcl_tune_host_heap.
+bool tune_host_heap() {
+  static int ok = -1;
+  if (ok < 0) ok = mallopt(M_MMAP_MAX, 0) == 1 && mallopt(M_TRIM_THRESHOLD, 1 << 30) == 1;
+  return ok == 1;
 }
 
 RunResult run_pipeline(const Dataset &ds, mc_ctx *ctx, Options opt, bool upload, const ShardComm *comm) {
-  keep_host_heap();
   RunResult rr;
   rr.n = ds.size();
   const bool verbose = !opt.quiet;
@@ -152,6 +154,7 @@ RunResult run_pipeline(const Dataset &ds, mc_ctx *ctx, Options opt, bool upload,
   if (opt.k < 1 || opt.k > 12) throw Error("k must be in 1..12 on this engine (4^k-bin dense histograms)", 1);
   rr.k = opt.k;
   auto t0 = std::chrono::steady_clock::now();
+  fault_point(comm, "upload");
   if (upload) {
     Scope s(rr.timer, "upload");
     check(mc_load_packed(ctx, ds.packed.data(), ds.pk_off.data(), ds.seq_off.data(), ds.size(), ds.exc_pos.data(),
@@ -204,6 +207,7 @@ RunResult run_pipeline(const Dataset &ds, mc_ctx *ctx, Options opt, bool upload,
     Scope s(rr.timer, "bvec.wait");
     bvec_thread.join();
   }
+  fault_point(comm, "train");
   rr.timer.add("bvec.overlapped", bvec_ms);
   if (bvec_err) std::rethrow_exception(bvec_err);
   mc_classifier cls = tr.classifier();
@@ -255,48 +259,107 @@ static void write_stats(const std::string &path, const RunResult &rr, double par
   fclose(f);
 }
 
-// --devices: one host thread per GPU, each with its own context and RCCL rank, sharing one
-// clustering (cluster.cpp: sharded get_close steps, centre all-gather per mean-shift
-// iteration).  Every rank ends with the same partition; rank 0's is written.
-static int allgather_rccl(void *user, const void *in, uint64_t bytes, void *out) {
-  return mc_comm_allgather((mc_comm *)user, in, bytes, out);
+// --devices: one host thread per GPU, each with its own context, sharing one clustering
+// (cluster.cpp: the device-sharded accumulation whose kernels exchange through the mailbox,
+// the centre all-gather per mean-shift iteration).  The ranks are threads of this process, so
+// their host-side all-gathers are a shared buffer and a condition variable; the first thread
+// that fails aborts the exchange, and every thread waiting in it returns an error.
+struct ThreadComm {
+  int world;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<uint8_t> buf;
+  uint64_t bytes = 0, gen = 0;
+  int arrived = 0, left = 0;
+  bool draining = false, aborted = false;
+
+  explicit ThreadComm(int w) : world(w) {}
+  void abort() {
+    std::lock_guard<std::mutex> lk(mu);
+    aborted = true;
+    cv.notify_all();
+  }
+  int allgather(int rank, const void *in, uint64_t n, void *out) {
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait(lk, [&] { return aborted || !draining; });  // the previous round fully copied out
+    if (aborted) return 1;
+    if (arrived == 0) {
+      bytes = n;
+      buf.resize(n * world);
+    }
+    if (n != bytes) {  // ranks disagree on the block size: a driver bug, stop every rank
+      aborted = true;
+      cv.notify_all();
+      return 1;
+    }
+    if (n) memcpy(buf.data() + (size_t)rank * n, in, n);
+    const uint64_t g = gen;
+    if (++arrived == world) {
+      arrived = 0;
+      gen++;
+      draining = true;
+      left = world;
+      cv.notify_all();
+    } else {
+      cv.wait(lk, [&] { return aborted || gen != g; });
+      if (aborted) return 1;
+    }
+    if (n) memcpy(out, buf.data(), n * world);
+    if (--left == 0) {
+      draining = false;
+      cv.notify_all();
+    }
+    return 0;
+  }
+};
+
+struct ThreadRank {
+  ThreadComm *tc;
+  int rank;
+};
+
+static int allgather_threads(void *user, const void *in, uint64_t bytes, void *out) {
+  auto *r = (ThreadRank *)user;
+  return r->tc->allgather(r->rank, in, bytes, out);
 }
 
 static RunResult run_multi_gpu(const Dataset &ds, const Options &opt) {
   const int W = (int)opt.devices.size();
-  uint8_t id[MC_COMM_ID_BYTES];
-  check(mc_comm_unique_id(id), "mc_comm_unique_id");
+  ThreadComm tc(W);
+  std::atomic<int> first{-1};
+  std::vector<ThreadRank> tr(W);
   std::vector<RunResult> res(W);
   std::vector<std::exception_ptr> err(W);
   std::vector<std::thread> th;
   for (int r = 0; r < W; r++)
     th.emplace_back([&, r]() {
       mc_ctx *ctx = nullptr;
-      mc_comm *comm = nullptr;
       try {
         check(mc_ctx_create(opt.devices[r], &ctx), "mc_ctx_create");
-        check(mc_comm_create(opt.devices[r], r, W, id, &comm), "mc_comm_create");
+        tr[r] = ThreadRank{&tc, r};
         ShardComm sc;
         sc.rank = r;
         sc.world = W;
-        sc.allgather = allgather_rccl;
-        sc.user = comm;
+        sc.allgather = allgather_threads;
+        sc.user = &tr[r];
         Options o = opt;
         o.quiet = opt.quiet || r != 0;
         res[r] = run_pipeline(ds, ctx, o, true, &sc);
       } catch (...) {
         err[r] = std::current_exception();
+        int none = -1;
+        first.compare_exchange_strong(none, r);  // the root cause, not the aborted exchanges
+        tc.abort();
       }
-      if (comm) mc_comm_destroy(comm, err[r] ? 1 : 0);
       if (ctx) mc_ctx_destroy(ctx);
     });
   for (auto &t : th) t.join();
-  for (int r = 0; r < W; r++)
-    if (err[r]) std::rethrow_exception(err[r]);
+  if (first >= 0) std::rethrow_exception(err[first]);
   return std::move(res[0]);
 }
 
 int meshclust_main(int argc, char **argv) {
+  tune_host_heap();
   Options opt;
   try {
     opt = parse_options(argc, argv);

@@ -45,6 +45,7 @@ struct RunResult {
 };
 
 // Full pipeline on an already parsed dataset and an open context (bench.py reuses both).
+bool tune_host_heap();  // process-global malloc settings (runner.cpp); true when applied
 RunResult run_pipeline(const Dataset &ds, mc_ctx *ctx, Options opt, bool upload = true,
                        const ShardComm *comm = nullptr);
 

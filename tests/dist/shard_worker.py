@@ -21,8 +21,12 @@ def main():
     ap.add_argument("--rccl", action="store_true")
     ap.add_argument("flags", nargs="*")
     a = ap.parse_args()
+    import datetime
     import torch.distributed as dist
-    dist.init_process_group("gloo", init_method="env://")
+    # a rank that fails (tests inject faults, MC_FAULT) never joins the next exchange: the others
+    # give up after MC_DIST_TIMEOUT_S instead of gloo's 30 minutes
+    dist.init_process_group("gloo", init_method="env://",
+                            timeout=datetime.timedelta(seconds=float(os.environ.get("MC_DIST_TIMEOUT_S", "600"))))
     from meshclust_amd.dist import RcclShardComm, TorchShardComm
     if a.gpu:
         import meshclust_amd as M

@@ -157,3 +157,72 @@ def test_sharded_D1M_equals_single_gpu(tmp_path):
     ranks = _launch(fa, ["--id", "0.90"], out, True, 2, False, {}, timeout=900)
     assert ranks[0]["accum_path"] == "device x2"
     assert BG.canonical_digest(BG.clusters_of(out)) == BG.canonical_digest(BG.clusters_of(one))
+
+
+# ---- one process, several ranks (bin/meshclust --devices): threads sharing a host exchange ----
+HARNESS = os.path.join(ROOT, "oracle", "_build", "meshclust_cpu")
+
+
+def _cli(binary, name, tmp_path, devices, env_extra=None, timeout=600):
+    fa, flags = fixtures.e2e_input(name, tmp_path)
+    out = str(tmp_path / (name + ".clstr"))
+    st = out + ".json"
+    r = subprocess.run([binary, fa] + flags + ["--devices", devices, "--output", out, "--stats-json", st, "--quiet",
+                        "--threads", "4"], capture_output=True, text=True, timeout=timeout,
+                       env=dict(os.environ, **(env_extra or {})))
+    return r, out, st
+
+
+@pytest.mark.parametrize("name", ["a1k", "fam2k"])
+def test_devices_threads_cpu_byte_identical(cpu_lib, name, tmp_path):
+    """--devices 0,1 on the CPU engine: two threads, the in-process exchange, host-driven
+    sharded steps (the CPU engine has no device mailbox)."""
+    r, out, st = _cli(HARNESS, name, tmp_path, "0,1")
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert json.load(open(st))["accum_path"] == "sharded steps x2"
+    with gzip.open(fixtures.golden("e2e_%s.clstr.gz" % name), "rb") as f:
+        assert open(out, "rb").read() == f.read()
+
+
+@pytest.mark.parametrize("stage", ["upload", "train", "accumulate", "update"])
+def test_devices_threads_fault_stops_every_rank(cpu_lib, stage, tmp_path):
+    """A failure on one rank at any stage ends the whole run with an error (no rank left
+    waiting in an exchange): MC_FAULT injects it on rank 1."""
+    import time
+    t0 = time.time()
+    r, _, _ = _cli(HARNESS, "a1k", tmp_path, "0,1", {"MC_FAULT": "1:" + stage}, timeout=120)
+    assert r.returncode != 0
+    assert "injected fault" in r.stderr, r.stderr[-2000:]
+    assert time.time() - t0 < 60
+
+
+@pytest.mark.parametrize("stage", ["train", "update"])
+def test_processes_fault_stops_every_rank(cpu_lib, stage, tmp_path):
+    """The same with one process per rank (gloo): the surviving rank's exchange fails or the
+    launcher stops it, and the job exits non-zero promptly."""
+    import time
+    fa, flags = fixtures.e2e_input("a1k", tmp_path)
+    out = str(tmp_path / "a1k.clstr")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), WORKER, fa, out, "--"] + flags
+    t0 = time.time()
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, OMP_NUM_THREADS="2", MC_FAULT="1:" + stage, MC_DIST_TIMEOUT_S="30"))
+    assert r.returncode != 0
+    assert time.time() - t0 < 200
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,devices", [("fam2k", "0"), ("fam2k", "0,0"), ("big2_3k", "0,0"), ("s1k_k5", "0,0")])
+def test_devices_cli_gpu_byte_identical(name, devices, tmp_path):
+    """bin/meshclust --devices on the product: one GPU, or two ranks (threads, contexts) on the
+    test box's one GPU sharing the accumulation through the mailbox (each kernel takes half of
+    the CUs)."""
+    import meshclust_amd as M
+    M.build()
+    r, out, st = _cli(M.BIN, name, tmp_path, devices)
+    assert r.returncode == 0, r.stderr[-3000:]
+    w = len(devices.split(","))
+    assert json.load(open(st))["accum_path"] == ("device x%d" % w if w > 1 else "device")
+    with gzip.open(fixtures.golden("e2e_%s.clstr.gz" % name), "rb") as f:
+        assert open(out, "rb").read() == f.read()
