@@ -127,6 +127,21 @@ def test_sharded_B100k_equals_reference(world, rccl, env, tmp_path):
 
 
 @pytest.mark.gpu
+@pytest.mark.timeout(900)
+def test_sharded_D100k_equals_reference(tmp_path):
+    """Config D's shape (10,000 clusters of 10 reads) at 100k reads: two ranks' kernels sharing
+    the accumulation against the reference's partition (cfg_D100k.npz)."""
+    g = np.load(fixtures.golden("cfg_D100k.npz"))
+    fa = _big_input("D100k")
+    out = str(tmp_path / "D100k.clstr")
+    ranks = _launch(fa, ["--id", "0.90"], out, True, 2, False, {}, timeout=800)
+    assert ranks[0]["accum_path"] == "device x2"
+    got = BG.clusters_of(out)
+    assert sorted(c for c, _ in got) == [int(x) for x in g["centres"]]
+    assert BG.canonical_digest(got) == str(g["digest"])
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("world,env", [(1, {"MC_SHARD_FORCE": "1"}), (2, {})])
 def test_sharded_E91_equals_reference(world, env, tmp_path):
     """Config E (k = 6, the wide accumulation rows) through the sharded path."""

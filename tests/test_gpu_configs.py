@@ -108,6 +108,15 @@ def test_config_B100k_global_bitmap_equals_reference(product):
     assert st["accum_path"] == "device"
 
 
+@pytest.mark.parametrize("env", [{}, {"MC_ACCUM_STEPS": "1"}])
+def test_config_D100k_partition_equals_reference(product, env):
+    """Config D's shape (10 reads per template, 10,000 clusters) at 100k reads: the device loop
+    and the host-driven steps against the reference's own partition (tests/golden/cfg_D100k.npz,
+    oracle/_ref/meshclust --threads 1, 48 min here)."""
+    st = _big("D100k", product, 300, env=env, tag=".steps" if env else "")
+    assert st["accum_path"] == ("device" if not env else "steps (MC_ACCUM_STEPS)")
+
+
 def _partition(path):
     got = BG.clusters_of(path)
     ids = np.concatenate([np.array(m, np.int64) for _, m in got])
