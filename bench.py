@@ -252,6 +252,9 @@ def main():
     nw_roof = {"bound": "valu", "achieved": nw_rate, "peak": nw_peak, "unit": "cells/s",
                "frac": round(nw_rate / nw_peak, 4) if nw_rate else None,
                "cells_per_step": nw_cells / a.steps, "ms_per_step": round(fam_ms["nw"] / a.steps, 3)}
+    nwc = os.path.join(ROOT, "profiles", "nw_counters.json")
+    if os.path.exists(nwc):  # rocprofv3 SQ counter pass on the NW kernels (scripts/prof_summary.py)
+        nw_roof["counters"] = json.load(open(nwc))
     cpu = None
     if not a.no_cpu_baseline and world == 1 and not shard:  # the reference: rank 0 at N = 1 only
         cpu = cpu_baseline(fasta, ["--id", a.id], a.n, host_threads(), a.cpu_repeats)

@@ -67,10 +67,12 @@ constexpr int WIDE_NCH = 32;
 // Several ranks (GPUs) sharing one accumulation: global tile t belongs to rank t mod W, whose
 // worker (t / W) mod GW scans it.  Each rank's controller keeps the whole (replicated) chain
 // state and exchanges, per step, {first max, flagged positions} with the other ranks' kernels
-// through a mailbox in host memory shared by all of them: MBOX_HDR granules per rank and step,
-// then its flagged positions, every granule tagged with the step; two parities of slots, since
-// a rank can be at most one step ahead of another.
-constexpr int MBOX_HDR = 8;  // best value hi / lo, best position, flagged, scanned, (3 spare)
+// through a mailbox in host memory shared by all of them: MBOX_HDR granules per rank and step
+// (the first MBOX_INL flagged positions inline, so a step with few flags per rank needs one
+// read round), then its further flagged positions, every granule tagged with the step; two
+// parities of slots, since a rank can be at most one step ahead of another.
+constexpr int MBOX_HDR = 16;  // best value hi / lo, best position, flagged, scanned, inline flags
+constexpr int MBOX_INL = MBOX_HDR - 5;
 
 // Static part of a centre's bvec window (bvec::get_range, bvec.cpp:245-278), per static
 // position: the window lengths, the bins index_of picks, and how many static positions of
@@ -818,7 +820,7 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
   __shared__ uint64_t s_sumF;
   __shared__ double s_xv[64];  // the ranks' step headers (mailbox)
   __shared__ uint64_t s_xp[64];
-  __shared__ uint32_t s_xn[64], s_xs[64];
+  __shared__ uint32_t s_xn[64], s_xs[64], s_xi[64][MBOX_INL];
   constexpr int NC = NCH > 0 ? NCH : 1;
   const uint32_t GW = gridDim.x - 1;
   const int lane = threadIdx.x & 63, wv = wave_id();
@@ -1125,7 +1127,7 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
           const uint32_t p = j < (uint32_t)INL ? (uint32_t)g8[5 + j] : ld32(A.fpos + (uint64_t)wk * A.fcap + j);
           const uint32_t slot = atomicAdd(&s_new, 1u);
           if (mslot) {  // (several ranks: every rank takes the union, below)
-            st64x(mslot + MBOX_HDR + slot, gran(step, p));
+            st64x(mslot + (slot < (uint32_t)MBOX_INL ? 5 + slot : MBOX_HDR - MBOX_INL + slot), gran(step, p));
           } else if (slot < PLIST) {
             s_plist[slot] = p;
           } else {  // a list overflow: this thread takes the member itself (past the cache)
@@ -1182,18 +1184,19 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
                               : j == 2 ? (best_pos == NONE64 ? NONE : (uint32_t)best_pos)
                               : j == 3 ? (uint32_t)nflag
                               : j == 4 ? (uint32_t)nsc
-                                       : 0u;
-        st64x(mslot + j, gran(step, data));
+                                       : NONE;
+        // (inline slots of this rank's flagged positions were written while collecting)
+        if (j < 5 || (uint64_t)(j - 5) >= nflag) st64x(mslot + j, gran(step, data));
       }
       uint64_t *mbase = A.mbox + (uint64_t)(step & 1) * A.W * A.slot_g;
       if (threadIdx.x < A.W) {  // thread r reads rank r's header (W <= 64: wave 0)
         const uint64_t *h = mbase + (uint64_t)threadIdx.x * A.slot_g;
         const uint64_t t0 = now();
-        uint64_t g[5];
+        uint64_t g[MBOX_HDR];
         for (uint32_t it = 1;; it++) {
           bool ok = true;
 #pragma unroll
-          for (int j = 0; j < 5; j++) {
+          for (int j = 0; j < MBOX_HDR; j++) {
             g[j] = ld64x(h + j);
             ok &= (uint32_t)(g[j] >> 32) == step;
           }
@@ -1208,6 +1211,8 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
         s_xp[threadIdx.x] = (uint32_t)g[2] == NONE ? NONE64 : (uint64_t)(uint32_t)g[2];
         s_xn[threadIdx.x] = (uint32_t)g[3];
         s_xs[threadIdx.x] = (uint32_t)g[4];
+#pragma unroll
+        for (int j = 0; j < MBOX_INL; j++) s_xi[threadIdx.x][j] = (uint32_t)g[5 + j];
       }
       __syncthreads();
       if (s_abort) {
@@ -1231,9 +1236,9 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
         uint32_t r = 0;
         uint64_t j = i;
         while (j >= s_xn[r]) j -= s_xn[r++];
-        const uint64_t *e = mbase + (uint64_t)r * A.slot_g + MBOX_HDR + j;
+        const uint64_t *e = mbase + (uint64_t)r * A.slot_g + MBOX_HDR - MBOX_INL + j;
         const uint64_t t0 = now();
-        uint64_t g = ld64x(e);
+        uint64_t g = j < (uint64_t)MBOX_INL ? gran(step, s_xi[r][j]) : ld64x(e);
         for (uint32_t it = 1; (uint32_t)(g >> 32) != step; it++) {
           if ((it & 63) == 0 && timed_out(A, t0)) {
             s_abort = 1;

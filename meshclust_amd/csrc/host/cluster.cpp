@@ -408,8 +408,34 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
     std::vector<uint32_t> centres(n), ids(n);
     std::vector<uint64_t> moff(n + 1);
     uint64_t ncl = 0, st[5] = {0, 0, 0, 0, 0};
-    const int rc = mc_accumulate(ctx, bin_lo.data(), bv.begin_bounds().data(), (uint32_t)bins.size(), cfg.sim,
-                                 centres.data(), moff.data(), ids.data(), &ncl, st);
+    int rc = mc_accumulate(ctx, bin_lo.data(), bv.begin_bounds().data(), (uint32_t)bins.size(), cfg.sim,
+                           centres.data(), moff.data(), ids.data(), &ncl, st);
+    std::string mbox_note;
+    if (dev_shard) {
+      // every rank learns every rank's outcome: a mailbox the ranks' GPUs could not all see
+      // (each kernel's hand-off deadline expired) sends all of them to the host-driven sharded
+      // steps together; any other failure stops all of them
+      int32_t mine[2] = {rc, 0}, all[2 * 64];
+      if (shard->allgather(shard->user, mine, sizeof mine, all) != 0) throw Error("all-gather across ranks failed", 1);
+      int worst = MC_OK;  // MC_OK < timeouts / unsupported (fall back) < anything else (stop)
+      for (int r = 0; r < shard->world; r++) {
+        const int e = all[2 * r];
+        if (e == MC_OK) continue;
+        if (e == MC_ERR_HIP || e == MC_ERR_UNSUPPORTED) {
+          if (worst == MC_OK) worst = e;
+        } else {
+          worst = e;
+          break;
+        }
+      }
+      if (worst == MC_ERR_HIP) {
+        fprintf(stderr, "meshclust: device-sharded accumulation: the ranks' mailbox hand-offs failed or timed out; "
+                        "taking the host-driven sharded steps\n");
+        mbox_note = " (mailbox timed out)";
+        worst = MC_ERR_UNSUPPORTED;
+      }
+      rc = worst;
+    }
     if (rc == MC_OK) {
       for (uint64_t c = 0; c < ncl; c++)
         part.push_back(Center{centres[c], std::vector<uint32_t>(ids.begin() + moff[c], ids.begin() + moff[c + 1]), false});
@@ -423,7 +449,7 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
     } else if (rc != MC_ERR_UNSUPPORTED) {
       check(rc, "mc_accumulate");
     } else if (dev_shard) {  // (every rank: the same configuration) -> the host-driven sharded steps
-      stats.accum_path = "sharded steps x" + std::to_string(shard->world);
+      stats.accum_path = "sharded steps x" + std::to_string(shard->world) + mbox_note;
     } else {
       // both loops are GPU paths and give identical partitions; say which one ran
       stats.accum_path = std::string("steps (") + mc_last_error() + ")";
