@@ -420,6 +420,39 @@ __device__ __forceinline__ void add_rows(const RowRef &R, const uint32_t *rows, 
   }
 }
 
+// Column sums for wide rows (>= 32 chunks): thread t owns chunks t, t + NTH, ... and adds them
+// up over all M rows in registers (a wave reads 64 consecutive chunks of one row: 1 KiB
+// contiguous), then stores its bins -- no atomics, which at B = 4,096 bins would be M x 4,096
+// per workgroup.  Overwrites sum[0..B).
+template <typename T, int NTH>
+__device__ __forceinline__ void add_rows_owned(const RowRef &R, const uint32_t *rows, uint32_t M, int nch, int B,
+                                               uint64_t *sum) {
+  constexpr int per = 16 / (int)sizeof(T);
+  for (int c = threadIdx.x; c < nch; c += NTH) {
+    uint32_t acc[per];
+#pragma unroll
+    for (int e = 0; e < per; e++) acc[e] = 0;
+    uint32_t q = 0;
+    for (; q + 4 <= M; q += 4) {  // four rows' loads in flight
+      const uint4 v0 = R.chunk(rows[q], c), v1 = R.chunk(rows[q + 1], c), v2 = R.chunk(rows[q + 2], c),
+                  v3 = R.chunk(rows[q + 3], c);
+      const T *p0 = reinterpret_cast<const T *>(&v0), *p1 = reinterpret_cast<const T *>(&v1),
+              *p2 = reinterpret_cast<const T *>(&v2), *p3 = reinterpret_cast<const T *>(&v3);
+#pragma unroll
+      for (int e = 0; e < per; e++) acc[e] += (uint32_t)p0[e] + (uint32_t)p1[e] + (uint32_t)p2[e] + (uint32_t)p3[e];
+    }
+    for (; q < M; q++) {
+      const uint4 v = R.chunk(rows[q], c);
+      const T *pv = reinterpret_cast<const T *>(&v);
+#pragma unroll
+      for (int e = 0; e < per; e++) acc[e] += pv[e];
+    }
+#pragma unroll
+    for (int e = 0; e < per; e++)
+      if (c * per + e < B) sum[c * per + e] = acc[e];
+  }
+}
+
 // One workgroup.  rows[q] (q < M) are row indices into R with magnitudes mags[rows[q]];
 // keys[q] (or q itself) orders ties like the reference's serial first-min scan.
 // sum: B u64 holding the column sums of the M rows.  Fl: nch uint4 (LDS).  Returns the winner.
@@ -451,6 +484,35 @@ __device__ uint64_t mean_closest_fast(const RowRef &R, const uint32_t *rows, con
   const uint64_t sumF = sF;
   double bd = __builtin_inf();
   uint64_t bk = ~0ull, br = 0;
+  if (nch >= 32) {
+    // wide rows: one row per wave, 64 lanes over its chunks; every lane ends with the wave's
+    // first minimum (the reductions below then see equal values in every lane)
+    const int lane = threadIdx.x & 63;
+    for (uint32_t q = threadIdx.x >> 6; q < M; q += NTH / 64) {
+      const uint64_t r = rows[q];
+      Acc<T> acc;
+      int c = lane;
+      for (; c + 192 < nch; c += 256) {
+        const uint4 v0 = R.chunk(r, c), v1 = R.chunk(r, c + 64), v2 = R.chunk(r, c + 128), v3 = R.chunk(r, c + 192);
+        acc.add(v0, Fl[c]);
+        acc.add(v1, Fl[c + 64]);
+        acc.add(v2, Fl[c + 128]);
+        acc.add(v3, Fl[c + 192]);
+      }
+      for (; c < nch; c += 64) acc.add(R.chunk(r, c), Fl[c]);
+      acc.wave_reduce();
+      const uint64_t mp = mags[r];
+      const PS s = acc.finish(mp, sumF);
+      const double frac = (double)(2 * s.smin) / (double)(mp + sumF);
+      const double d = __builtin_fma(-frac, frac, 1.0) * 10000.0;
+      const uint64_t key = keys ? keys[q] : q;
+      if (d < bd || (d == bd && key < bk)) {
+        bd = d;
+        bk = key;
+        br = r;
+      }
+    }
+  } else
   for (uint32_t q = threadIdx.x; q < M; q += NTH) {
     const uint64_t r = rows[q];
     Acc<T> acc;

@@ -433,16 +433,21 @@ __global__ __launch_bounds__(NT) void mean_shift_kernel(HistView H, DevClassifie
     if (threadIdx.x == 0) newc[j] = centre;
     return;
   }
-  double *mbuf = H.B <= 2048 ? mean : gmean + (uint64_t)j * H.B;
+  // (launch_mean_shift's LDS plan: the sums stay in LDS when the chunks and B doubles fit 64 KiB)
+  double *mbuf = nch * 16 + H.B * 8 <= 65536 ? mean : gmean + (uint64_t)j * H.B;
   if constexpr (sizeof(T) <= 2) {
     // integer mean + SAD closest (tests/test_identities.py); sums reuse the mean buffer
     const RowRef R{reinterpret_cast<const uint4 *>(H.hist), H.pitch / 16, 1};
     uint4 *Fl = clds;  // the centre chunks are no longer needed
     uint64_t *sums = reinterpret_cast<uint64_t *>(mbuf);
     __syncthreads();
-    for (int b = threadIdx.x; b < H.B; b += NT) sums[b] = 0;
-    __syncthreads();
-    add_rows<T, NT>(R, mine, M, nch, sums);
+    if (nch >= 32) {
+      add_rows_owned<T, NT>(R, mine, M, nch, H.B, sums);
+    } else {
+      for (int b = threadIdx.x; b < H.B; b += NT) sums[b] = 0;
+      __syncthreads();
+      add_rows<T, NT>(R, mine, M, nch, sums);
+    }
     __syncthreads();
     const uint64_t win = mean_closest_fast<T, NT>(R, mine, nullptr, M, H.mag, H.B, nch, sums, Fl);
     if (threadIdx.x == 0) newc[j] = (uint32_t)win;
@@ -558,7 +563,7 @@ int launch_mean_shift(mc_ctx *c, const uint32_t *d_cid, uint32_t C, const uint64
   }
   if (ensure(c->s_d, (C + 1) * 8) || ensure(c->s_e, std::max<uint64_t>(soff[C], 1) * 4) || ensure(c->s_f, (size_t)C * 4))
     return MC_ERR_OOM;
-  const bool gm = H.B > 2048;
+  const bool gm = (size_t)nch * 16 + (size_t)H.B * 8 > 65536;  // column sums / mean in LDS when they fit
   if (gm && ensure(c->s_g, (size_t)C * H.B * 8)) return MC_ERR_OOM;
   MCG_CHECK(hipMemcpyAsync(c->s_d.p, soff.data(), (C + 1) * 8, hipMemcpyHostToDevice, c->stream));
   const size_t lds = (size_t)nch * 16 + (gm ? 0 : (size_t)H.B * 8);
