@@ -246,9 +246,11 @@ def main():
                 roof["algorithmic_bytes_per_launch"] = round(per_launch_bytes)
     nw_cells = sum(s["nw_cells"] for s in stats)
     nw_rate = nw_cells / (fam_ms["nw"] / 1e3) if fam_ms["nw"] else None
-    # NW is VALU-bound (DESIGN.md §3): 26.5 VALU instructions per cell in the throughput form;
-    # int32 VALU issue peak 256 CU x 4 SIMD x 32 lanes/clk x 2.4 GHz = 78.6e12 lane-ops/s
-    nw_peak = 256 * 4 * 32 * 2.4e9 / 26.5
+    # NW is VALU-bound (DESIGN.md §3.2): 26.5 VALU instructions per cell in the throughput form;
+    # a wave64 VALU instruction holds its SIMD 4 cycles (MI355X_MICROARCH.md issue costs), so
+    # the int32 issue peak is 256 CU x 4 SIMD x 16 lanes/clk x 2.4 GHz = 39.3e12 lane-ops/s
+    # (SQ_INSTS_VALU agrees: profiles/r03_v4/config_c.json, 0.98 of it in the throughput form)
+    nw_peak = 256 * 4 * 16 * 2.4e9 / 26.5
     nw_roof = {"bound": "valu", "achieved": nw_rate, "peak": nw_peak, "unit": "cells/s",
                "frac": round(nw_rate / nw_peak, 4) if nw_rate else None,
                "cells_per_step": nw_cells / a.steps, "ms_per_step": round(fam_ms["nw"] / a.steps, 3)}

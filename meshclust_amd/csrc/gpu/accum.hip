@@ -437,7 +437,7 @@ __device__ __forceinline__ int classify_cand(const Acc<T> &acc, const PInfo &pi,
 // reads row t's chunks conflict-free) and never read from memory again.
 // LDS: record words | alive flags (fcap) | resident rows (res * nch * NT uint4)
 // ============================================================================================
-template <typename T, int NCH, bool WIDE, bool STREAM>
+template <typename T, int NCH, bool WIDE>
 __device__ __forceinline__ void worker(const AccArgs &A, const DevClassifier &C, uint4 *dyn) {
   __shared__ double s_bv[NW];
   __shared__ uint64_t s_bp[NW];
@@ -657,56 +657,6 @@ __device__ __forceinline__ void worker(const AccArgs &A, const DevClassifier &C,
           best_v = cv;
           best_p = pos;
         }
-      }
-    } else if constexpr (STREAM) {
-      // streaming (rows too many for the workers' LDS: config D), software-pipelined: a worker
-      // owns several chunks of a window, and the next one's row loads are in flight while this
-      // one's candidate is scored
-      uint4 v[NC], vn[NC];
-      PInfo pi{0, 0, 0}, pn{0, 0, 0};
-      bool live = false, liven = false;
-      uint64_t pos = 0, posn = 0;
-      uint8_t *la = nullptr, *lan = nullptr;
-      auto fetch = [&](uint64_t c, uint4(&vv)[NC], PInfo &pp, bool &lv, uint64_t &ps, uint8_t *&lp) {
-        const uint64_t li = dgw.div((uint32_t)c);
-        ps = (c * A.W + A.rank) * NT + threadIdx.x;
-        lp = lal + li * NT + threadIdx.x;
-        lv = ps >= P_S && ps <= P_E && *lp;
-        if (lv) {
-          const uint4 *col = A.hs + ps;
-#pragma unroll
-          for (int k = 0; k < NC; k++) vv[k] = col[(uint64_t)k * A.npad];
-          pp = PInfo{A.mag_s[ps], A.sumsq_s[ps], A.len_s[ps]};
-        }
-      };
-      uint64_t ch = c0 + mine;
-      if (ch <= c1) fetch(ch, v, pi, live, pos, la);
-      while (ch <= c1) {
-        const uint64_t cn = ch + GW;
-        liven = false;
-        if (cn <= c1) fetch(cn, vn, pn, liven, posn, lan);
-        if (live) {
-          nscan++;
-          Acc<T> acc;
-          double cv;
-#pragma unroll
-          for (int k = 0; k < NC; k++) acc.add(v[k], clds[k]);
-          if (classify_cand<T>(acc, pi, pc, A.B, C, &cv)) {
-            *la = 0;
-            flag_pos(pos);
-          }
-          if (cv > -1.0 && better(cv, pos, best_v, best_p)) {
-            best_v = cv;
-            best_p = pos;
-          }
-        }
-        ch = cn;
-#pragma unroll
-        for (int k = 0; k < NC; k++) v[k] = vn[k];
-        pi = pn;
-        live = liven;
-        pos = posn;
-        la = lan;
       }
     } else
     for (uint64_t ch = c0 + mine; ch <= c1; ch += GW) {
@@ -1536,12 +1486,11 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
 }
 
 // NCH: compile-time chunks per row (0: A.nch at run time).
-// STREAM: rows stream from memory every step (no resident chunks), software-pipelined scan
-template <typename T, int NCH, bool WIDE = false, bool STREAM = false>
+template <typename T, int NCH, bool WIDE = false>
 __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
   extern __shared__ __attribute__((aligned(16))) uint4 dyn[];
   if (blockIdx.x == 0) controller<T, NCH, WIDE>(A, dyn);
-  else worker<T, NCH, WIDE, STREAM>(A, C, dyn);
+  else worker<T, NCH, WIDE>(A, C, dyn);
 }
 
 __global__ void bits_init_kernel(uint32_t *bits, uint64_t n) {
@@ -1607,8 +1556,6 @@ bool accum_plan(const mc_ctx *c, uint32_t nb, AccPlan *pl) {
   const size_t chunk_bytes = (size_t)nch * NT * 16;
   pl->res = (!wide && !getenv("MC_ACCUM_STREAM") && wfix + per_w * chunk_bytes <= cap) ? (int)per_w : 0;
   if (wfix >= cap) return false;
-  if (!wide && nch == 16 && c->width == 1 && pl->res == 0 && !getenv("MC_ACCUM_NO_PIPE"))
-    pl->fn = reinterpret_cast<const void *>(&accum_kernel<uint8_t, 16, false, true>);
   // controller: mean row, column sums, bvec (+ bitmap unless global), member cache
   auto cfix = [&](bool gbits) {
     size_t s = (size_t)nch * 16 + (size_t)c->B * 8;

@@ -19,6 +19,8 @@
 //   M(i,j) [matches]  = max(M, X, Y at (i-1,j-1)) + s(i,j)           ties: M, then X, then Y
 //   X(i,j) [lowerGap] = max(M(i-1,j) - (o+e), X(i-1,j) - e)          ties: from M
 // with the reference's finite "-infinity" and boundary rows/columns (:125-170, :250-256).
+#include <algorithm>
+
 #include "mcgpu.hpp"
 
 namespace mcg {
@@ -666,7 +668,15 @@ int launch_nw(mc_ctx *c, const uint8_t *d_A, const uint64_t *d_aoff, const uint3
   std::vector<uint32_t> bucket[NB];
   std::vector<uint64_t> boff[NB];
   uint64_t scratch[NB] = {0};
-  for (uint64_t i = 0; i < m; i++) {
+  // longest pairs first (by DP cells): the dispatcher hands workgroups to free slots in launch
+  // order, so the longest ones do not start last and leave a tail (config E: 8-12 kb genomes,
+  // cells vary 2.3x).  Results go to each pair's own slot; the order changes nothing else.
+  std::vector<uint32_t> order(m);
+  for (uint64_t i = 0; i < m; i++) order[i] = (uint32_t)i;
+  std::stable_sort(order.begin(), order.end(),
+                   [&](uint32_t x, uint32_t y) { return alen[x] * blen[x] > alen[y] * blen[y]; });
+  for (uint64_t oi = 0; oi < m; oi++) {
+    const uint64_t i = order[oi];
     const uint64_t la = alen[i], lb = blen[i];
     const bool wide = la + lb >= 65535;
     int r, bk;
