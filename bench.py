@@ -141,12 +141,17 @@ def main():
         dist.barrier()
     fasta = ensure_fasta(a.n, a.len, a.templates, a.mut, a.seed + (0 if shard else rank))
     threads = min(16, host_threads())
+    # MC_BENCH_ONE_GPU=1 (rehearsal on a one-GPU box): every rank on GPU 0, the ranks' kernels
+    # splitting its CUs, gloo for the host-side all-gathers (RCCL takes one rank per GPU)
+    one_gpu = os.environ.get("MC_BENCH_ONE_GPU") == "1"
+    if one_gpu:
+        local = 0
     eng = M.Engine(local)
     args = ["--id", a.id, "--threads", str(threads)]
     comm = None
     if shard:  # libmcgpu's RCCL communicator, called from C++ (torch.distributed only hands out its id)
-        from meshclust_amd.dist import RcclShardComm
-        comm = RcclShardComm(local)
+        from meshclust_amd.dist import RcclShardComm, TorchShardComm
+        comm = TorchShardComm() if one_gpu else RcclShardComm(local)
     # The GPU is driven by libmcgpu alone: torch's own HIP runtime (a second HIP/HSA runtime in
     # the process, from torch's bundled ROCm) is never initialised here -- two runtimes on one
     # GPU made the process fault in the system HSA runtime's exit handler under rocprofv3.
@@ -238,7 +243,7 @@ def main():
                 "avg_launch_us": round(avg_s * 1e6, 2),
                 "us_per_step": round(fam_ms["scan"] * 1e3 / sum(s["scan_steps"] for s in stats), 2)}
         pmc = os.path.join(ROOT, "profiles", "pmc_latest.json")
-        if os.path.exists(pmc):  # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (scripts/pmc_summary.py)
+        if os.path.exists(pmc) and not shard:  # (counters of the config-B launch)  # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (scripts/pmc_summary.py)
             e = next((v for k2, v in sorted(json.load(open(pmc)).items()) if k2.startswith(kname)), None)
             if e and "hbm_bytes_per_dispatch" in e:
                 roof["traffic"] = round(e["hbm_bytes_per_dispatch"])

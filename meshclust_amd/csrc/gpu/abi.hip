@@ -199,7 +199,7 @@ int mc_ctx_destroy(mc_ctx *c) {
   mailbox_detach(c);
   for (Buf *b : {&c->codes, &c->seq_off, &c->seg, &c->seg_off, &c->packed, &c->pk_off, &c->impure, &c->hist, &c->mag, &c->sumsq, &c->len, &c->order,
                  &c->alive, &c->members, &c->member_keys, &c->partials, &c->scan_dev, &c->flags_out, &c->s_a, &c->s_b,
-                 &c->s_c, &c->s_d, &c->s_e, &c->s_f, &c->s_g, &c->s_h, &c->s_i, &c->s_j, &c->hs, &c->mag_s, &c->sumsq_s, &c->len_s, &c->ticket,
+                 &c->s_c, &c->s_d, &c->s_e, &c->s_f, &c->s_g, &c->s_h, &c->s_i, &c->s_j, &c->s_k, &c->hs, &c->mag_s, &c->sumsq_s, &c->len_s, &c->ticket,
                  &c->msum, &c->ident_s, &c->al_a, &c->al_b, &c->al_out, &c->acc_out})
     release(*b);
   if (c->h_scan) (void)hipHostFree(c->h_scan);

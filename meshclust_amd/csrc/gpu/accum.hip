@@ -116,6 +116,7 @@ struct AccArgs {
   uint32_t *fpos;      // worker w's flagged positions beyond the INL inline ones, at w * fcap
   uint64_t fcap;
   int res;        // chunks per worker whose rows live in its LDS (0: rows stream from memory)
+  uint4 *cc;      // streaming: per-chunk compacted copies of the alive rows (null: read hs)
   uint32_t mrow;  // member cache entries (LDS)
   // output
   uint32_t *mem_pos;    // N: member static positions, cluster after cluster
@@ -135,6 +136,14 @@ struct AccArgs {
 };
 
 __device__ __forceinline__ uint64_t now() { return __builtin_amdgcn_s_memrealtime(); }
+
+// 16-byte load that bypasses the CU's L1 (`nt`): the compacted row copies are rewritten by the
+// same workgroup between steps, and L2 has the fresh bytes
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ld_nt16(const uint4 *p) {
+  const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t *>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
 
 // Step trace (MC_ACCUM_PROFILE=2/3), words per step: 0 record published, 7 controller has
 // every partial, 8 collect done, 9 active workers; =3: 1/2 first/last worker saw it, 3/4
@@ -437,11 +446,11 @@ __device__ __forceinline__ int classify_cand(const Acc<T> &acc, const PInfo &pi,
 // reads row t's chunks conflict-free) and never read from memory again.
 // LDS: record words | alive flags (fcap) | resident rows (res * nch * NT uint4)
 // ============================================================================================
-template <typename T, int NCH, bool WIDE>
+template <typename T, int NCH, bool WIDE, bool CPT>
 __device__ __forceinline__ void worker(const AccArgs &A, const DevClassifier &C, uint4 *dyn) {
   __shared__ double s_bv[NW];
   __shared__ uint64_t s_bp[NW];
-  __shared__ uint32_t s_nfl, s_nscan, s_go, s_inl[INL];
+  __shared__ uint32_t s_nfl, s_nscan, s_go, s_inl[INL], s_nfl_w[NW];
   __shared__ int s_abort;
   constexpr int NC = NCH > 0 ? NCH : 1;
   const uint32_t GW = gridDim.x - 1, w = blockIdx.x - 1;
@@ -456,10 +465,17 @@ __device__ __forceinline__ void worker(const AccArgs &A, const DevClassifier &C,
   const uint4 *clds = WIDE ? lcen : dyn;
   uint8_t *lal = reinterpret_cast<uint8_t *>(lcen + (WIDE ? nch : 0));
   uint4 *lrow = reinterpret_cast<uint4 *>(lal + (A.fcap + 15) / 16 * 16);
+  // streaming with compaction (A.cc): per local chunk, its compacted entries' slots (lrow's place)
+  uint16_t *clist = reinterpret_cast<uint16_t *>(lrow);
+  __shared__ uint32_t s_ccnt[64], s_alive;  // (fcap / NT <= 64 chunks per worker when A.cc)
   // alive flags of the positions this worker owns (tiles w, w + GW, ...), local index
   // (tile / GW) * TS + offset: flagged candidates are cleared by their owner thread, and so
   // are the controller's pops and erases, which arrive with the step records
   for (uint64_t i = threadIdx.x; i < A.fcap; i += NT) lal[i] = 1;
+  if (CPT) {
+    for (uint64_t i = threadIdx.x; i < A.fcap; i += NT) clist[i] = (uint16_t)(i % NT);
+    for (uint64_t i = threadIdx.x; i < A.fcap / NT; i += NT) s_ccnt[i] = NT | 0x80000000u;  // (bit 31: rows still in hs)
+  }
   const int res = A.res;
   // resident chunks' per-candidate data (res <= 2 kept in registers; fixed indices only, so
   // nothing is spilled to scratch)
@@ -656,6 +672,90 @@ __device__ __forceinline__ void worker(const AccArgs &A, const DevClassifier &C,
         if (cv > -1.0 && better(cv, pos, best_v, best_p)) {
           best_v = cv;
           best_p = pos;
+        }
+      }
+    } else if constexpr (CPT) {
+      // streaming with compaction: a chunk's rows stream from HBM every step, and once half of
+      // its listed entries are dead the worker rewrites the alive rows densely (A.cc, entry
+      // order = slot order) -- the loads of dead neighbours' cache lines went with them
+      // (config D: 1.8x the algorithmic bytes fetched without this, profiles/r03_v4)
+      for (uint64_t ch = c0 + mine; ch <= c1; ch += GW) {
+        const uint32_t li = dgw.div((uint32_t)ch);
+        const uint64_t cbase = (ch * A.W + A.rank) * NT;
+        uint4 *creg = A.cc + ch * (uint64_t)NC * NT;  // (local chunk ch: its region of cc)
+        const uint32_t cw = s_ccnt[li];
+        const bool in_hs = (cw >> 31) != 0;
+        const uint32_t n = cw & 0xffffu;
+        const uint32_t t = threadIdx.x;
+        const uint32_t slot = t < n ? (uint32_t)clist[(uint64_t)li * NT + t] : 0u;
+        const bool alive = t < n && lal[(uint64_t)li * NT + slot];
+        // rebuild when fewer than half of the listed entries are alive (one WG-uniform decision)
+        if (t == 0) s_alive = 0;
+        __syncthreads();
+        {
+          const uint32_t c = wave_sum32(alive ? 1u : 0u);
+          if (lane == 0 && c) atomicAdd(&s_alive, c);
+        }
+        __syncthreads();
+        const uint32_t nal = s_alive;
+        uint32_t e = t;  // this lane's entry after the (possible) rebuild
+        bool mine_alive = alive;
+        uint32_t myslot = slot;
+        if (nal * 2 < n && n > 64) {
+          // rank of this alive entry among the alive ones (entry order = slot order)
+          const uint64_t bal = __ballot(alive);
+          const uint32_t below = (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+          if (lane == 0) s_nfl_w[wv] = (uint32_t)__popcll(bal);
+          uint4 row[NC];
+          if (alive) {
+#pragma unroll
+            for (int k = 0; k < NC; k++)
+              row[k] = in_hs ? A.hs[(uint64_t)k * A.npad + cbase + slot] : ld_nt16(creg + (uint64_t)k * NT + t);
+          }
+          __syncthreads();  // every read of the old entries before any write
+          uint32_t r = below;
+          for (int i = 0; i < wv; i++) r += s_nfl_w[i];
+          if (alive) {
+#pragma unroll
+            for (int k = 0; k < NC; k++) creg[(uint64_t)k * NT + r] = row[k];
+            clist[(uint64_t)li * NT + r] = (uint16_t)slot;
+          }
+          e = alive ? r : NT;  // (dead lanes hold no entry now)
+          if (t == 0) s_ccnt[li] = nal;
+          __syncthreads();
+          mine_alive = alive;
+          myslot = slot;
+        }
+        (void)e;
+        const uint32_t cw2 = s_ccnt[li];
+        const bool from_hs = (cw2 >> 31) != 0;
+        const uint32_t n2 = cw2 & 0xffffu;
+        // scan: lane t takes entry t of the (possibly rebuilt) list
+        {
+          const bool rebuilt = (cw2 != cw);
+          const uint32_t sl = rebuilt ? (t < n2 ? (uint32_t)clist[(uint64_t)li * NT + t] : 0u) : myslot;
+          const bool al = rebuilt ? (t < n2) : mine_alive;
+          const uint64_t pos = cbase + sl;
+          if (al && pos >= P_S && pos <= P_E && lal[(uint64_t)li * NT + sl]) {
+            nscan++;
+            uint4 v[NC];
+#pragma unroll
+            for (int k = 0; k < NC; k++)
+              v[k] = from_hs ? A.hs[(uint64_t)k * A.npad + pos] : ld_nt16(creg + (uint64_t)k * NT + t);
+            const PInfo pi{A.mag_s[pos], A.sumsq_s[pos], A.len_s[pos]};
+            Acc<T> acc;
+            double cv;
+#pragma unroll
+            for (int k = 0; k < NC; k++) acc.add(v[k], clds[k]);
+            if (classify_cand<T>(acc, pi, pc, A.B, C, &cv)) {
+              lal[(uint64_t)li * NT + sl] = 0;
+              flag_pos(pos);
+            }
+            if (cv > -1.0 && better(cv, pos, best_v, best_p)) {
+              best_v = cv;
+              best_p = pos;
+            }
+          }
         }
       }
     } else
@@ -1486,11 +1586,12 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
 }
 
 // NCH: compile-time chunks per row (0: A.nch at run time).
-template <typename T, int NCH, bool WIDE = false>
+// CPT: streaming rows with per-chunk compaction (A.cc; the resident form compiled out)
+template <typename T, int NCH, bool WIDE = false, bool CPT = false>
 __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
   extern __shared__ __attribute__((aligned(16))) uint4 dyn[];
   if (blockIdx.x == 0) controller<T, NCH, WIDE>(A, dyn);
-  else worker<T, NCH, WIDE>(A, C, dyn);
+  else worker<T, NCH, WIDE, CPT>(A, C, dyn);
 }
 
 __global__ void bits_init_kernel(uint32_t *bits, uint64_t n) {
@@ -1506,6 +1607,7 @@ struct AccPlan {
   int res = 0;         // chunks per worker resident in its LDS (0: streaming)
   bool gbits = false;  // bitmap in global memory
   bool wide = false;   // a wave per candidate (accum_kernel<T, 0, true>)
+  bool compact = false;  // streaming rows with per-chunk compaction (A.cc)
   uint32_t mrow = 0;   // member cache entries
   size_t lds = 0;
   uint32_t G = 0;
@@ -1556,6 +1658,10 @@ bool accum_plan(const mc_ctx *c, uint32_t nb, AccPlan *pl) {
   const size_t chunk_bytes = (size_t)nch * NT * 16;
   pl->res = (!wide && !getenv("MC_ACCUM_STREAM") && wfix + per_w * chunk_bytes <= cap) ? (int)per_w : 0;
   if (wfix >= cap) return false;
+  // streaming rows (config D): compacted per chunk by its worker, the slot list in LDS
+  pl->compact = !wide && nch == 16 && c->width == 1 && pl->res == 0 && per_w <= 64 && !getenv("MC_ACCUM_NO_COMPACT") &&
+                wfix + pl->fcap * 2 <= cap;
+  if (pl->compact) pl->fn = reinterpret_cast<const void *>(&accum_kernel<uint8_t, 16, false, true>);
   // controller: mean row, column sums, bvec (+ bitmap unless global), member cache
   auto cfix = [&](bool gbits) {
     size_t s = (size_t)nch * 16 + (size_t)c->B * 8;
@@ -1572,7 +1678,7 @@ bool accum_plan(const mc_ctx *c, uint32_t nb, AccPlan *pl) {
     if (m >= 64 || (gb == 1 && m >= 1)) {
       pl->gbits = gb != 0;
       pl->mrow = (uint32_t)m;
-      pl->lds = std::max(f + m * per_entry, wfix + (size_t)pl->res * chunk_bytes);
+      pl->lds = std::max(f + m * per_entry, wfix + (size_t)pl->res * chunk_bytes + (pl->compact ? pl->fcap * 2 : 0));
       return true;
     }
   }
@@ -1619,6 +1725,9 @@ int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, 
     return MC_ERR_OOM;
   if (ensure(c->s_i, c->norder * sizeof(MInfo) + 64) || ensure(c->s_j, c->norder * (size_t)nch * 16 + 64))
     return MC_ERR_OOM;
+  // compacted row copies: one region of NT rows per local chunk (this rank's chunks)
+  const size_t cc_bytes = pl.compact ? (size_t)(pl.fcap / NT) * GW * NT * (size_t)nch * 16 : 0;
+  if (cc_bytes && ensure(c->s_k, cc_bytes)) return MC_ERR_OOM;
   MInfo *d_minfo = (MInfo *)c->s_i.p;
   uint4 *d_hr = (uint4 *)c->s_j.p;
   uint32_t *d_bits = pl.gbits ? (uint32_t *)((char *)c->s_b.p + part_bytes) : nullptr;
@@ -1659,6 +1768,7 @@ int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, 
   A.klog = (uint64_t *)(sc + fpos_bytes);
   A.fcap = fcap;
   A.res = pl.res;
+  A.cc = pl.compact ? (uint4 *)c->s_k.p : nullptr;
   A.mrow = pl.mrow;
   A.mem_pos = d_mem_pos;
   A.mkeys = d_mkeys;
@@ -1679,8 +1789,8 @@ int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, 
     A.trace_all = atoi(getenv("MC_ACCUM_PROFILE")) >= 3;
   }
   if (getenv("MC_ACCUM_PROFILE"))
-    fprintf(stderr, "[accum] variant: width %d nch %d wide %d resident chunks/worker %d global-bitmap %d member-cache %u lds %zu G %u rank %u/%u\n",
-            c->width, nch, (int)pl.wide, pl.res, (int)pl.gbits, pl.mrow, pl.lds, G, A.rank, A.W);
+    fprintf(stderr, "[accum] variant: width %d nch %d wide %d resident chunks/worker %d compact %d global-bitmap %d member-cache %u lds %zu G %u rank %u/%u\n",
+            c->width, nch, (int)pl.wide, pl.res, (int)pl.compact, (int)pl.gbits, pl.mrow, pl.lds, G, A.rank, A.W);
   DevClassifier cls = c->cls;
   void *args[] = {&A, &cls};
   timed_begin(c);

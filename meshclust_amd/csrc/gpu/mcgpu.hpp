@@ -125,7 +125,7 @@ struct mc_ctx {
   uint64_t mb_bytes = 0;
   int mb_rank = 0, mb_world = 0, mb_share = 1;
   // scratch
-  mcg::Buf s_a, s_b, s_c, s_d, s_e, s_f, s_g, s_h, s_i, s_j;
+  mcg::Buf s_a, s_b, s_c, s_d, s_e, s_f, s_g, s_h, s_i, s_j, s_k;
   std::vector<void *> pinned;
   // timers: event pairs recorded around kernels, resolved lazily after the next stream sync
   hipEvent_t ev0 = nullptr, ev1 = nullptr;

@@ -19,6 +19,13 @@
 //   M(i,j) [matches]  = max(M, X, Y at (i-1,j-1)) + s(i,j)           ties: M, then X, then Y
 //   X(i,j) [lowerGap] = max(M(i-1,j) - (o+e), X(i-1,j) - e)          ties: from M
 // with the reference's finite "-infinity" and boundary rows/columns (:125-170, :250-256).
+//
+// The kernels keep every state as T = score + i + j.  Each comparison above is between values
+// of one cell (the three states of (i-1,j-1), of (i,j-1) or of (i-1,j), or of (la,lb) at the
+// end), so a per-cell offset changes no decision; in T the recurrences read
+//   Y = max(M - (o+e-1), Y + (1-e)),  X likewise,  M = max3 + s + 2,
+// and with e = 1 a gap extension adds nothing: one VALU instruction less per state and cell.
+// The score is T(la,lb) - (la + lb).
 #include <algorithm>
 
 #include "mcgpu.hpp"
@@ -28,6 +35,8 @@ namespace mcg {
 namespace {
 
 constexpr int GO = 2, GE = 1, MATCH = 1, MISMATCH = -1;
+// the same moves in T = score + i + j (see above)
+constexpr int OPEN_T = GO + GE - 1, EXT_T = 1 - GE, MATCH_T = MATCH + 2, MISMATCH_T = MISMATCH + 2;
 
 template <typename P>
 struct Pack;
@@ -103,10 +112,10 @@ __global__ __launch_bounds__(64) void nw_kernel(NWPairs q) {
     for (int r = 0; r < R; r++) {
       const int i = itop + r;
       ac[r] = i <= la ? a[i - 1] : (uint8_t)0xFF;
-      // column 0 (GlobAlignE.cpp:140-160): M = Y = -inf, X = -o - i*e, lengths i
-      M[r] = NINF;
-      Y[r] = NINF;
-      X[r] = -GO - i * GE;
+      // column 0 (GlobAlignE.cpp:140-160): M = Y = -inf, X = -o - i*e, lengths i (T: + i)
+      M[r] = NINF + i;
+      Y[r] = NINF + i;
+      X[r] = -GO - i * GE + i;
       MP[r] = XP[r] = YP[r] = 0;  // i gap moves, no diagonal
     }
     // diagonal input for column 1: row itop-1 at column 0
@@ -119,10 +128,10 @@ __global__ __launch_bounds__(64) void nw_kernel(NWPairs q) {
         dX = NINF;
         dY = -GO;
         dMP = dXP = dYP = 0;
-      } else {
-        dM = NINF;
-        dX = -GO - i * GE;
-        dY = NINF;
+      } else {  // (T: + i)
+        dM = NINF + i;
+        dX = -GO - i * GE + i;
+        dY = NINF + i;
         dMP = dXP = dYP = 0;
       }
     }
@@ -147,10 +156,10 @@ __global__ __launch_bounds__(64) void nw_kernel(NWPairs q) {
       const int b0 = __builtin_amdgcn_readlane(bcur, t & 63);
       if (lane == 0) {
         bc = (j >= 1 && j <= lb) ? (uint8_t)b0 : 0;
-        if (blk == 0) {  // row 0 at column j: M = X = -inf, Y = -o - j*e, lengths j
-          uM = NINF;
-          uX = NINF;
-          uY = -GO - j * GE;
+        if (blk == 0) {  // row 0 at column j: M = X = -inf, Y = -o - j*e, lengths j (T: + j)
+          uM = NINF + j;
+          uX = NINF + j;
+          uY = -GO - j * GE + j;
           uMP = uXP = uYP = 0;
         } else if (j >= 1 && j <= lb) {
           const int *s = bnd + 6 * j;
@@ -180,13 +189,13 @@ __global__ __launch_bounds__(64) void nw_kernel(NWPairs q) {
           const int pM = M[r], pX = X[r], pY = Y[r];  // (i, j-1): this row's previous column
           const P pMP = MP[r], pXP = XP[r], pYP = YP[r];
           // upperGap (GlobAlignE.cpp:233-251)
-          const int yb = pM - (GO + GE), yc = pY - GE;
+          const int yb = pM - OPEN_T, yc = pY + EXT_T;
           const bool yFromM = yb >= yc;
           Y[r] = yFromM ? yb : yc;
           YP[r] = yFromM ? pMP : pYP;
           // matches (:255-299)
           const bool hit = ac[r] == bc;
-          const int s = hit ? MATCH : MISMATCH;
+          const int s = hit ? MATCH_T : MISMATCH_T;
           // M on ties, then X, then Y: M iff gM >= max(gX, gY), else X iff gX >= gY
           const bool xy = gX >= gY;
           const int mxy = xy ? gX : gY;
@@ -197,7 +206,7 @@ __global__ __launch_bounds__(64) void nw_kernel(NWPairs q) {
           M[r] = best + s;
           MP[r] = bestP + LEN1 + (hit ? (P)1 : (P)0);
           // lowerGap (:316-330), from the row above in this column
-          const int xb = aM - (GO + GE), xc = aX - GE;
+          const int xb = aM - OPEN_T, xc = aX + EXT_T;
           const bool xFromM = xb >= xc;
           X[r] = xFromM ? xb : xc;
           XP[r] = xFromM ? aMP : aXP;
@@ -264,7 +273,7 @@ __global__ __launch_bounds__(64) void nw_kernel(NWPairs q) {
       // GlobAlignE.cpp:278-291: M, then lowerGap (X), then upperGap (Y)
       int sc = mM > mX ? mM : mX;
       sc = sc > mY ? sc : mY;
-      fin_score = sc;
+      fin_score = sc - (la + lb);  // (T -> score)
       fin_pay = sc == mM ? pM : (sc == mX ? pX : pY);
     }
     __syncthreads();
@@ -355,9 +364,9 @@ __global__ __launch_bounds__(64 * W) void nw_mw_kernel(NWPairs q) {
     for (int r = 0; r < R; r++) {
       const int i = itop + r;
       ac[r] = i <= la ? a[i - 1] : (uint8_t)0xFF;
-      M[r] = NINF;  // column 0 (GlobAlignE.cpp:140-160)
-      Y[r] = NINF;
-      X[r] = -GO - i * GE;
+      M[r] = NINF + i;  // column 0 (GlobAlignE.cpp:140-160), T = score + i
+      Y[r] = NINF + i;
+      X[r] = -GO - i * GE + i;
       MP[r] = XP[r] = YP[r] = 0;  // i gap moves, no diagonal
     }
     int dM, dX, dY;
@@ -370,9 +379,9 @@ __global__ __launch_bounds__(64 * W) void nw_mw_kernel(NWPairs q) {
         dY = -GO;
         dMP = dXP = dYP = 0;
       } else {
-        dM = NINF;
-        dX = -GO - i * GE;
-        dY = NINF;
+        dM = NINF + i;
+        dX = -GO - i * GE + i;
+        dY = NINF + i;
         dMP = dXP = dYP = 0;
       }
     }
@@ -435,10 +444,10 @@ __global__ __launch_bounds__(64 * W) void nw_mw_kernel(NWPairs q) {
         if (lane == 0) {
           bc = (j >= 1 && j <= lb) ? b0 : 0;
           if (j >= 1 && j <= lb) {
-            if (row0) {  // row 0: M = X = -inf, Y = -o - j*e, lengths j
-              uM = NINF;
-              uX = NINF;
-              uY = -GO - j * GE;
+            if (row0) {  // row 0: M = X = -inf, Y = -o - j*e, lengths j (T: + j)
+              uM = NINF + j;
+              uX = NINF + j;
+              uY = -GO - j * GE + j;
               uMP = uXP = uYP = 0;
             } else {  // bottom row of wave w-1 (or of the previous row block) at column j
               uM = nM;
@@ -454,7 +463,7 @@ __global__ __launch_bounds__(64 * W) void nw_mw_kernel(NWPairs q) {
       } else {
         const bool l0 = lane == 0;
         bc = l0 ? b0 : bc;
-        const int hM = row0 ? NINF : nM, hX = row0 ? NINF : nX, hY = row0 ? -GO - j * GE : nY;
+        const int hM = row0 ? NINF + j : nM, hX = row0 ? NINF + j : nX, hY = row0 ? -GO - j * GE + j : nY;
         const P hMP = row0 ? (P)0 : nMP, hXP = row0 ? (P)0 : nXP, hYP = row0 ? (P)0 : nYP;
         uM = l0 ? hM : uM;
         uX = l0 ? hX : uX;
@@ -496,12 +505,12 @@ __global__ __launch_bounds__(64 * W) void nw_mw_kernel(NWPairs q) {
         for (int r = 0; r < R; r++) {
           const int pM = M[r], pX = X[r], pY = Y[r];
           const P pMP = MP[r], pXP = XP[r], pYP = YP[r];
-          const int yb = pM - (GO + GE), yc = pY - GE;  // upperGap (GlobAlignE.cpp:233-251)
+          const int yb = pM - OPEN_T, yc = pY + EXT_T;  // upperGap (GlobAlignE.cpp:233-251)
           const bool yFromM = yb >= yc;
           Y[r] = yFromM ? yb : yc;
           YP[r] = yFromM ? pMP : pYP;
           const bool hit = ac[r] == (uint8_t)bc;  // matches (:255-299)
-          const int sc = hit ? MATCH : MISMATCH;
+          const int sc = hit ? MATCH_T : MISMATCH_T;
           // M on ties, then X, then Y: M iff gM >= max(gX, gY), else X iff gX >= gY
           const bool xy = gX >= gY;
           const int mxy = xy ? gX : gY;
@@ -511,7 +520,7 @@ __global__ __launch_bounds__(64 * W) void nw_mw_kernel(NWPairs q) {
           const P bestP = fromM ? gMP : pxy;
           M[r] = best + sc;
           MP[r] = bestP + LEN1 + (hit ? (P)1 : (P)0);
-          const int xb = aM - (GO + GE), xc = aX - GE;  // lowerGap (:316-330)
+          const int xb = aM - OPEN_T, xc = aX + EXT_T;  // lowerGap (:316-330)
           const bool xFromM = xb >= xc;
           X[r] = xFromM ? xb : xc;
           XP[r] = xFromM ? aMP : aXP;
@@ -596,7 +605,7 @@ __global__ __launch_bounds__(64 * W) void nw_mw_kernel(NWPairs q) {
         }
       int sc = mM > mX ? mM : mX;  // GlobAlignE.cpp:278-291
       sc = sc > mY ? sc : mY;
-      fin_score = sc;
+      fin_score = sc - (la + lb);  // (T -> score)
       fin_pay = sc == mM ? pM : (sc == mX ? pX : pY);
     }
     __threadfence_block();

@@ -134,7 +134,8 @@ static int find_k(const Dataset &ds, bool verbose) {
 // for its own process; a host embedding the library opts in with mcl_tune_host_heap.
 bool tune_host_heap() {
   static int ok = -1;
-  if (ok < 0) ok = mallopt(M_MMAP_MAX, 0) == 1 && mallopt(M_TRIM_THRESHOLD, 1 << 30) == 1;
+  // (trim threshold at mallopt's int maximum: config D's 1 GB file buffer stays in the heap)
+  if (ok < 0) ok = mallopt(M_MMAP_MAX, 0) == 1 && mallopt(M_TRIM_THRESHOLD, std::numeric_limits<int>::max()) == 1;
   return ok == 1;
 }
 
