@@ -171,10 +171,12 @@ void sharded_step(mc_ctx *ctx, const ShardComm &comm, uint32_t centre, uint64_t 
   memcpy(mine.flagged, flag_buf.data(), std::min<uint64_t>(loc.n_flagged, ShardBlock::kInline) * 4);
   std::vector<ShardBlock> all(W);
   if (comm.allgather(comm.user, &mine, sizeof mine, all.data()) != 0)
-    throw Error("get_close all-gather across ranks failed", 1);
+    throw PeerError("get_close all-gather across ranks failed");
   for (int r = 0; r < W; r++)
-    if (all[r].failed)
-      throw Error(scan_err.empty() ? "get_close failed on rank " + std::to_string(r) : scan_err, 1);
+    if (all[r].failed) {
+      if (scan_err.empty()) throw PeerError("get_close failed on rank " + std::to_string(r));
+      throw Error(scan_err, 1);
+    }
   memset(res, 0, sizeof *res);
   res->is_min = 1;
   res->best_val = -1.0;
@@ -195,7 +197,7 @@ void sharded_step(mc_ctx *ctx, const ShardComm &comm, uint32_t centre, uint64_t 
     std::vector<uint32_t> big(most, 0), gathered(most * W);
     std::copy(flag_buf.begin(), flag_buf.begin() + loc.n_flagged, big.begin());
     if (comm.allgather(comm.user, big.data(), most * 4, gathered.data()) != 0)
-      throw Error("get_close all-gather across ranks failed", 1);
+      throw PeerError("get_close all-gather across ranks failed");
     for (int r = 0; r < W; r++)
       all_flagged.insert(all_flagged.end(), gathered.begin() + most * r, gathered.begin() + most * r + all[r].n_flagged);
   } else {
@@ -241,7 +243,7 @@ static bool attach_mailbox(const ShardComm &comm, mc_ctx *ctx, uint64_t n, Share
   }
   std::vector<Blk> all(W);
   if (comm.allgather(comm.user, &mine, sizeof mine, all.data()) != 0)
-    throw Error("mailbox all-gather across ranks failed", 1);
+    throw PeerError("mailbox all-gather across ranks failed");
   bool ok = all[0].ok != 0;
   if (ok && comm.rank != 0) fd = shm_open(all[0].name, O_RDWR, 0600);
   if (ok && fd >= 0) {
@@ -257,7 +259,7 @@ static bool attach_mailbox(const ShardComm &comm, mc_ctx *ctx, uint64_t n, Share
   if (mb.p && mc_set_mailbox(ctx, mb.p, bytes, comm.rank, W, std::max(share, 1)) == MC_OK) mb.ctx = ctx;
   mine.ok = mb.ctx != nullptr;
   if (comm.allgather(comm.user, &mine, sizeof mine, all.data()) != 0)
-    throw Error("mailbox all-gather across ranks failed", 1);
+    throw PeerError("mailbox all-gather across ranks failed");
   if (comm.rank == 0 && all[0].name[0]) shm_unlink(all[0].name);  // every rank has mapped it (or failed)
   for (const auto &b : all) ok &= b.ok != 0;
   if (!ok && mb.ctx) {
@@ -416,7 +418,7 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
       // (each kernel's hand-off deadline expired) sends all of them to the host-driven sharded
       // steps together; any other failure stops all of them
       int32_t mine[2] = {rc, 0}, all[2 * 64];
-      if (shard->allgather(shard->user, mine, sizeof mine, all) != 0) throw Error("all-gather across ranks failed", 1);
+      if (shard->allgather(shard->user, mine, sizeof mine, all) != 0) throw PeerError("all-gather across ranks failed");
       int worst = MC_OK;  // MC_OK < timeouts / unsupported (fall back) < anything else (stop)
       for (int r = 0; r < shard->world; r++) {
         const int e = all[2 * r];
@@ -502,9 +504,12 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
         mine[0] = 1;
       }
       if (cfg.comm->allgather(cfg.comm->user, mine.data(), (uint64_t)blk * 4, all.data()) != 0)
-        throw Error("centre all-gather across ranks failed", 1);
+        throw PeerError("centre all-gather across ranks failed");
       for (uint32_t r = 0; r < W; r++)
-        if (all[(size_t)r * blk]) throw Error(ms_err.empty() ? "mean-shift update failed on rank " + std::to_string(r) : ms_err, 1);
+        if (all[(size_t)r * blk]) {
+          if (ms_err.empty()) throw PeerError("mean-shift update failed on rank " + std::to_string(r));
+          throw Error(ms_err, 1);
+        }
       for (uint32_t j = 0; j < C; j++) newc[j] = all[(size_t)(j / per) * blk + 1 + j % per];
     } else if (C && !memo) {
       Scope sm(timer, "update.mean_shift");

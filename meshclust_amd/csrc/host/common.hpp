@@ -18,6 +18,11 @@ struct Error : std::runtime_error {
   int code;
   explicit Error(const std::string &m, int c = 1) : std::runtime_error(m), code(c) {}
 };
+// A rank stopping because another rank reported a failure (or an exchange was aborted): the
+// multi-rank driver reports the failing rank's own error in preference to these.
+struct PeerError : Error {
+  explicit PeerError(const std::string &m) : Error(m, 1) {}
+};
 
 // Throws mc::Error when an ABI call fails (no fallback path exists).
 inline void check(int rc, const char *what) {

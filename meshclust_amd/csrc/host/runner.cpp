@@ -327,7 +327,7 @@ static int allgather_threads(void *user, const void *in, uint64_t bytes, void *o
 static RunResult run_multi_gpu(const Dataset &ds, const Options &opt) {
   const int W = (int)opt.devices.size();
   ThreadComm tc(W);
-  std::atomic<int> first{-1};
+  std::atomic<int> first{-1}, first_peer{-1};  // the first own failure; the first peer-reported one
   std::vector<ThreadRank> tr(W);
   std::vector<RunResult> res(W);
   std::vector<std::exception_ptr> err(W);
@@ -348,14 +348,22 @@ static RunResult run_multi_gpu(const Dataset &ds, const Options &opt) {
         res[r] = run_pipeline(ds, ctx, o, true, &sc);
       } catch (...) {
         err[r] = std::current_exception();
+        bool peer = false;
+        try {
+          std::rethrow_exception(err[r]);
+        } catch (const PeerError &) {
+          peer = true;
+        } catch (...) {
+        }
         int none = -1;
-        first.compare_exchange_strong(none, r);  // the root cause, not the aborted exchanges
+        (peer ? first_peer : first).compare_exchange_strong(none, r);  // the root cause, not the aborted exchanges
         tc.abort();
       }
       if (ctx) mc_ctx_destroy(ctx);
     });
   for (auto &t : th) t.join();
   if (first >= 0) std::rethrow_exception(err[first]);
+  if (first_peer >= 0) std::rethrow_exception(err[first_peer]);
   return std::move(res[0]);
 }
 
