@@ -107,6 +107,8 @@ struct AccArgs {
   uint32_t *gbits;         // alive bitmap in global memory (n too large for LDS), else null
   // hand-off
   uint64_t *ring;  // RING records of rec_g granules
+  uint64_t *ringb;  // spec: RING x 2 granules, the exact window {S, E} of step s (NONE: no scan)
+  int spec;         // the record carries a superset of the window; the exact one follows (dense)
   uint32_t rec_g;
   uint64_t *klog;      // static positions killed by the controller (pop / erase), append-only,
                        // entry e a granule tagged e + 1 (a reader checks the tag: no drain
@@ -904,10 +906,363 @@ __device__ __forceinline__ void worker(const AccArgs &A, const DevClassifier &C,
 }
 
 // ============================================================================================
+// Dense resident workers (narrow rows, at most NT candidates per worker).  Tiles of DT static
+// positions are dealt round-robin over the workers (tile t -> worker t mod GW), so a window
+// spreads over all of them instead of the one or two hundred that own its 512-position
+// chunks.  A worker keeps its alive candidates DENSE -- entry e is thread e, its row is LDS row
+// e (chunk-major: lane e reads row e conflict-free), entries sorted by static position -- and
+// compacts them after every step in which some died (flagged, or popped / erased by the
+// controller), while the controller collects: a step runs ceil(alive / 64) waves, not eight.
+// Per-entry magnitudes and pair-independent terms live in the entry's thread's registers.
+// LDS: record words | rows (nch * NT uint4) | entry positions (NT u32, compaction staging)
+// ============================================================================================
+constexpr int DT = 64;
+constexpr int DMAXCH = 16;  // chunks per row the dense form takes (a row per thread in registers while compacting)
+
+template <typename T, int NCH>
+__device__ __forceinline__ void worker_dense(const AccArgs &A, const DevClassifier &C, uint4 *dyn) {
+  __shared__ double s_bv[NW];
+  __shared__ uint64_t s_bp[NW];
+  __shared__ uint32_t s_nfl, s_nscan, s_go, s_inl[INL], s_wc[NW];
+  __shared__ int s_abort;
+  __shared__ uint64_t s_b[2];  // spec: part B of the step, {tag << 32 | S}, {tag << 32 | E}
+  constexpr int NC = NCH > 0 ? NCH : DMAXCH;
+  const uint32_t GW = gridDim.x - 1, w = blockIdx.x - 1;
+  const Div32 dgw(GW);
+  const int lane = threadIdx.x & 63, wv = wave_id();
+  const uint32_t t = threadIdx.x;
+  const int nch = NCH > 0 ? NCH : A.nch;
+  const int rec_words = (int)A.rec_g;
+  uint32_t *srec = reinterpret_cast<uint32_t *>(dyn);
+  const uint4 *clds = dyn;  // the centre row: record words 0 .. 4 nch
+  uint4 *lrow = dyn + (rec_words + 3) / 4;
+  uint32_t *lpos = reinterpret_cast<uint32_t *>(lrow + (size_t)nch * NT);
+  // entry t: this worker's (t / DT)-th tile, offset t % DT -- positions increase with t, so the
+  // entries below N are a prefix
+  uint32_t pos_t = 0;
+  bool al_t = false;
+  {
+    const uint64_t lt = (uint64_t)w + (uint64_t)(t / DT) * GW;
+    const uint64_t pos = (lt * A.W + A.rank) * DT + (t % DT);
+    al_t = t < A.fcap && pos < A.N;
+    if (al_t) {
+      pos_t = (uint32_t)pos;
+      for (int k = 0; k < nch; k++) lrow[(uint64_t)k * NT + t] = A.hs[(uint64_t)k * A.npad + pos];
+    }
+  }
+  uint32_t n_ent = (uint32_t)__syncthreads_count(al_t);
+  PInfo pi_t{0, 0, 0};
+  PTerms pt_t{0, 0, 0.0};
+  if (al_t) {
+    pi_t = PInfo{A.mag_s[pos_t], A.sumsq_s[pos_t], A.len_s[pos_t]};
+    pt_t = pterms(pi_t.mag, pi_t.sumsq, A.B);
+  }
+  if (t == 0) {
+    s_abort = 0;
+    s_b[0] = s_b[1] = 0;
+  }
+  __syncthreads();
+  uint32_t kcur = 0, seen = 0;
+  for (;;) {
+    // ---- wait for the next step's record (wave 0), as `worker` ---------------------------
+    if (wv == 0) {
+      const uint64_t t0 = now();
+      const uint32_t want = seen + 1;
+      int state = 0;
+      uint32_t got = want;
+      bool late = false;
+      const uint64_t *rn = A.ring + (uint64_t)(want % RING) * A.rec_g;
+      for (uint32_t it = 1;; it++) {
+        bool ok = true, ahead = false;
+        for (int j = lane; j < rec_words; j += 64) {
+          const uint64_t x = ld64(rn + j);
+          const uint32_t tg = (uint32_t)(x >> 32);
+          ok &= tg == want;
+          ahead |= (int32_t)(tg - want) > 0;
+          srec[j] = (uint32_t)x;
+        }
+        if (__ballot(!ok) == 0) {
+          state = 1;
+          break;
+        }
+        if (__ballot(ahead) != 0) {
+          late = true;
+          break;
+        }
+        if ((it & 255) == 0 && timed_out(A, t0)) {
+          state = 2;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      while (late && state == 0) {
+        uint32_t v = 0;
+        if (lane == 0) {
+          for (uint32_t it = 1; (v = ld32(A.go)) == seen; it++) {
+            if ((it & 255) == 0 && timed_out(A, t0)) break;
+            __builtin_amdgcn_s_sleep(1);
+          }
+        }
+        v = (uint32_t)__builtin_amdgcn_readlane((int)v, 0);
+        if (v == seen) {
+          state = 2;
+          break;
+        }
+        const uint64_t *r = A.ring + (uint64_t)(v % RING) * A.rec_g;
+        bool ok = true;
+        for (int j = lane; j < rec_words; j += 64) {
+          const uint64_t x = ld64(r + j);
+          ok &= (uint32_t)(x >> 32) == v;
+          srec[j] = (uint32_t)x;
+        }
+        if (__ballot(!ok) == 0) {
+          state = 1;
+          got = v;
+        }
+      }
+      if (lane == 0) {
+        if (state == 2) s_abort = 1;
+        s_go = got;
+        s_nfl = 0;
+        s_nscan = 0;
+      }
+    }
+    __syncthreads();
+    if (s_abort) {
+      if (t == 0) atomicMax((unsigned long long *)&A.out[3], 99ull);
+      return;
+    }
+    seen = s_go;
+    uint64_t t_seen = 0, t_klog = 0, t_scanned = 0;
+    if (A.trace && t == 0) t_seen = now();
+    const uint32_t *hdr = srec + 4 * nch;
+    if (hdr[0] == NONE) return;  // accumulation finished
+    const uint64_t P_S = hdr[1], P_E = hdr[2];
+    const uint32_t kend = hdr[3];
+    const PInfo pc{(uint64_t)hdr[4 + KINL] | ((uint64_t)hdr[5 + KINL] << 32),
+                   (uint64_t)hdr[6 + KINL] | ((uint64_t)hdr[7 + KINL] << 32),
+                   (uint64_t)hdr[8 + KINL] | ((uint64_t)hdr[9 + KINL] << 32)};
+    const PTerms tq = pterms(pc.mag, pc.sumsq, A.B);
+    // the controller's kills since the last record: every thread compares them with its own
+    // entry (one or two per step; no search, no barrier)
+    {
+      const uint32_t kinl0 = kend > (uint32_t)KINL ? kend - KINL : 0;
+      const uint64_t t0k = kinl0 > kcur ? now() : 0;
+      for (uint32_t e = kcur; e < kend; e++) {
+        uint32_t p;
+        if (e >= kinl0) {
+          p = hdr[4 + KINL - (kend - e)];
+        } else {
+          uint64_t g = ld64(A.klog + e);
+          for (uint32_t it = 1; (uint32_t)(g >> 32) != e + 1; it++) {
+            if ((it & 255) == 0 && timed_out(A, t0k)) {
+              s_abort = 1;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            g = ld64(A.klog + e);
+          }
+          p = (uint32_t)g;
+        }
+        if (p == pos_t) al_t = false;
+      }
+      kcur = kend;
+    }
+    if (A.trace && t == 0) t_klog = now();
+    // ---- scores of the record's span: the exact window, or (spec) a superset of it --------
+    const bool comp = al_t && pos_t >= P_S && pos_t <= P_E;
+    int d_t = 0;
+    double cv_t = -1.0;
+    if (comp) {
+      Acc<T> acc;
+      const uint4 *rr = lrow + t;
+      constexpr int HB = NC >= 8 ? 8 : NC;
+      if constexpr (NCH > 0) {
+#pragma unroll
+        for (int k0 = 0; k0 < NC; k0 += HB) {
+          uint4 rv[HB], cvv[HB];
+#pragma unroll
+          for (int k = 0; k < HB; k++) {
+            rv[k] = rr[(uint64_t)(k0 + k) * NT];
+            cvv[k] = clds[k0 + k];
+          }
+#pragma unroll
+          for (int k = 0; k < HB; k++) acc.add(rv[k], cvv[k]);
+        }
+      } else {
+        for (int k = 0; k < nch; k++) acc.add(rr[(uint64_t)k * NT], clds[k]);
+      }
+      d_t = C.layout ? classify_std(C, acc.finish(pi_t.mag, pc.mag), pi_t, pt_t, pc, tq, A.B, &cv_t)
+                     : classify_cand<T>(acc, pi_t, pc, A.B, C, &cv_t);
+    }
+    if (A.trace && t == 0) t_scanned = now();
+    uint64_t W_S = P_S, W_E = P_E;  // the exact window
+    bool abandon = false;
+    if (A.spec) {
+      // part B: from the LDS copy once a wave has it, else polled by this wave's lanes 0 / 1
+      const uint64_t *rb = A.ringb + (uint64_t)(seen % RING) * 2;
+      const uint64_t t0 = now();
+      for (uint32_t it = 1;; it++) {
+        const uint64_t b0 = __hip_atomic_load(&s_b[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const uint64_t b1 = __hip_atomic_load(&s_b[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if ((uint32_t)(b0 >> 32) == seen && (uint32_t)(b1 >> 32) == seen) break;
+        const uint64_t g = lane < 2 ? ld64(rb + lane) : 0;
+        const uint64_t g0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(g >> 32), 0) << 32) |
+                            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)g, 0);
+        const uint64_t g1 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(g >> 32), 1) << 32) |
+                            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)g, 1);
+        if ((uint32_t)(g0 >> 32) == seen && (uint32_t)(g1 >> 32) == seen) {
+          if (lane == 0) {
+            __hip_atomic_store(&s_b[0], g0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_store(&s_b[1], g1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          }
+          break;
+        }
+        if ((it & 255) == 0 && timed_out(A, t0)) {
+          if (lane == 0) s_abort = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      __syncthreads();
+      if (s_abort) {
+        if (t == 0) atomicMax((unsigned long long *)&A.out[3], 99ull);
+        return;
+      }
+      W_S = (uint32_t)s_b[0];
+      W_E = (uint32_t)s_b[1];
+      abandon = (uint32_t)W_S == NONE;
+    }
+    uint64_t c0 = 0, c1 = 0;
+    const bool any_tile = !abandon && rank_tiles(W_S / DT, W_E / DT, A.W, A.rank, &c0, &c1);
+    const uint32_t nact = any_tile ? (uint32_t)(c1 - c0 + 1 < (uint64_t)GW ? c1 - c0 + 1 : (uint64_t)GW) : 0u;
+    const uint32_t mine = any_tile ? dgw.mod(w + GW - dgw.mod((uint32_t)c0)) : 0u;
+    const bool active = any_tile && mine < nact;
+    bool died = false;
+    if (active) {
+      double best_v = -1.0;
+      uint64_t best_p = NONE64;
+      uint32_t nscan = 0;
+      const uint64_t base = (uint64_t)w * A.fcap;
+      if (comp && pos_t >= W_S && pos_t <= W_E) {
+        nscan = 1;
+        if (d_t) {
+          al_t = false;
+          const uint32_t idx = atomicAdd(&s_nfl, 1u);
+          if (idx < (uint32_t)INL) s_inl[idx] = pos_t;
+          else st32(A.fpos + base + idx, pos_t);
+        }
+        if (cv_t > -1.0) {
+          best_v = cv_t;
+          best_p = pos_t;
+        }
+      }
+      wave_best_all(best_v, best_p, better);
+      nscan = wave_sum32(nscan);
+      if (lane == 0) {
+        s_bv[wv] = best_v;
+        s_bp[wv] = best_p;
+        if (nscan) atomicAdd(&s_nscan, nscan);
+      }
+      drain();  // this wave's flagged-list stores are complete before the partial announces them
+      __syncthreads();
+      if (t < PART_G) {
+        double v = s_bv[0];
+        uint64_t p = s_bp[0];
+        for (int i = 1; i < NW; i++)
+          if (better(s_bv[i], s_bp[i], v, p)) {
+            v = s_bv[i];
+            p = s_bp[i];
+          }
+        const uint64_t vb = (uint64_t)__double_as_longlong(v);
+        const int j = (int)t;
+        const uint32_t nfl = s_nfl;
+        const uint32_t data = j == 0   ? (uint32_t)(vb >> 32)
+                              : j == 1 ? (uint32_t)vb
+                              : j == 2 ? (p == NONE64 ? NONE : (uint32_t)p)
+                              : j == 3 ? nfl
+                              : j == 4 ? s_nscan
+                                       : ((uint32_t)(j - 5) < nfl ? s_inl[j - 5] : NONE);
+        st64(A.partials + (uint64_t)w * PART_G + j, gran(seen, data));
+        if (A.trace && !A.trace_all && j == 0 && mine == nact / 2 && seen < TRACE_STEPS) {
+          uint64_t *tr = A.trace + (uint64_t)seen * TRACE_W;
+          tr[10] = t_seen;
+          tr[11] = t_klog;
+          tr[12] = t_scanned;
+          tr[13] = t_scanned;
+          tr[14] = now();
+        }
+        if (A.trace && A.trace_all && j == 0) {
+          const uint64_t tn = now();
+          trace_mark(A, seen, 1, t_seen);
+          trace_mark(A, seen, 3, t_scanned);
+          trace_mark(A, seen, 5, tn);
+        }
+      }
+    }
+    // ---- compaction (off the critical path: the controller is collecting) ----------------
+    died = t < n_ent && !al_t;
+    if (__syncthreads_or(died)) {
+      const bool keep = t < n_ent && al_t;
+      const uint64_t bal = __ballot(keep);
+      if (lane == 0) s_wc[wv] = (uint32_t)__popcll(bal);
+      __syncthreads();
+      uint32_t r = (uint32_t)__popcll(bal & ((1ull << lane) - 1ull)), tot = 0;
+      for (int i = 0; i < NW; i++) {
+        if (i < wv) r += s_wc[i];
+        tot += s_wc[i];
+      }
+      const bool move = keep && r != t;
+      // rows move down in groups of eight chunks: every read of a group before any write
+      for (int k0 = 0; k0 < nch; k0 += 8) {
+        uint4 v0, v1, v2, v3, v4, v5, v6, v7;
+        const int kn = nch - k0;
+        uint4 *src = lrow + (uint64_t)k0 * NT + t;
+        if (move) {
+          v0 = src[0];
+          if (kn > 1) v1 = src[NT];
+          if (kn > 2) v2 = src[2 * NT];
+          if (kn > 3) v3 = src[3 * NT];
+          if (kn > 4) v4 = src[4 * NT];
+          if (kn > 5) v5 = src[5 * NT];
+          if (kn > 6) v6 = src[6 * NT];
+          if (kn > 7) v7 = src[7 * NT];
+        }
+        __syncthreads();
+        uint4 *dst = lrow + (uint64_t)k0 * NT + r;
+        if (move) {
+          dst[0] = v0;
+          if (kn > 1) dst[NT] = v1;
+          if (kn > 2) dst[2 * NT] = v2;
+          if (kn > 3) dst[3 * NT] = v3;
+          if (kn > 4) dst[4 * NT] = v4;
+          if (kn > 5) dst[5 * NT] = v5;
+          if (kn > 6) dst[6 * NT] = v6;
+          if (kn > 7) dst[7 * NT] = v7;
+        }
+        __syncthreads();
+      }
+      if (keep) lpos[r] = pos_t;
+      __syncthreads();
+      n_ent = tot;
+      al_t = t < n_ent;
+      if (al_t) {
+        const uint32_t np = lpos[t];
+        if (np != pos_t) {
+          pos_t = np;
+          pi_t = PInfo{A.mag_s[pos_t], A.sumsq_s[pos_t], A.len_s[pos_t]};
+          pt_t = pterms(pi_t.mag, pi_t.sumsq, A.B);
+        }
+      }
+    }
+  }
+}
+
+// ============================================================================================
 // Controller (WG 0).  LDS: integer mean row | column sums | bvec (counts, Fenwick tree, bin
 // starts, begin bounds, bitmap unless global) | member cache
 // ============================================================================================
-template <typename T, int NCH, bool WIDE>
+template <typename T, int NCH, bool WIDE, int TSZ>
 __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
   __shared__ uint64_t s_red[3 * NW];
   __shared__ double s_bv[NW];
@@ -1043,6 +1398,16 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
     return hi ? (uint32_t)(v >> 32) : (uint32_t)v;
   };
 
+  // publish the record of `step` for the current `last` (wave 0: one granule per lane, every
+  // granule tagged with the step).  Kill-log entries are tagged granules: a worker that needs
+  // one checks its tag, so the record is not held back until they land.  `go` is only a hint
+  // for a worker that fell RING steps behind: it re-validates the record's tags after reading.
+  auto publish = [&](uint64_t S, uint64_t E, bool have) {
+    uint64_t *r = A.ring + (uint64_t)(step % RING) * A.rec_g;
+    for (int j = lane; j < rec_words; j += 64) st64(r + j, gran(step, rec_word(j, have, S, E)));
+    if (lane == 0) st32(A.go, step);
+  };
+
   // member qm of the current cluster is static position p, flagged in this step (key step << 32
   // | p orders members like the bvec walk): member list, cache entry (row, magnitudes, window
   // data from the read-only static arrays) or column sums past the cache, and the bvec kill
@@ -1117,8 +1482,16 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
         t_ws[0] += t - t_mark;
         t_mark = t;
       }
+      const bool fast = wt.fb < A.nb && wt.bb < A.nb && cnt[wt.fb] > 0 && cnt[wt.bb] > 0;
+      if (A.spec) {
+        // publish the centre now, with a superset of its window: the fast form's window lies in
+        // the two edge bins' span [lo[fb], lo[bb + 1]) (bv_fast_window), the general one anywhere.
+        // The workers score that span while the exact window is computed (part B, below).
+        step++;
+        if (wv == 0) publish(fast ? lo[wt.fb] : 0, fast ? lo[wt.bb + 1] - 1 : A.N - 1, true);
+      }
       int64_t count = 0;
-      if (wt.fb < A.nb && wt.bb < A.nb && cnt[wt.fb] > 0 && cnt[wt.bb] > 0) {
+      if (fast) {
         // nearest-alive form (bv_fast_window): four one-wave queries side by side
         if (wv < 4) {
           const uint64_t pf = lo[wt.fb] + wt.kf, qb = lo[wt.bb] + wt.kble;
@@ -1141,6 +1514,7 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
         count = bv_window(bv, f, b, &S, &E, &e);
         if (e) {
           err = 10 + e;
+          if (A.spec && wv == 0 && lane < 2) st64(A.ringb + (uint64_t)(step % RING) * 2 + lane, gran(step, NONE));
           break;
         }
       }
@@ -1151,26 +1525,21 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
       }
       if (count > 0) {
         have = true;
+        if (A.spec && wv == 0 && lane < 2) st64(A.ringb + (uint64_t)(step % RING) * 2 + lane, gran(step, (uint32_t)(lane ? E : S)));
         break;
       }
+      // part B: no scan for this step (the workers drop their scores)
+      if (A.spec && wv == 0 && lane < 2) st64(A.ringb + (uint64_t)(step % RING) * 2 + lane, gran(step, NONE));
       // the OpenMP loop ran no iteration: is_min with a NULL result -> pop a new seed
       const uint64_t p = pop();
       finish_cluster();
       last = p == NONE64 ? NONE : (uint32_t)p;
       if (p != NONE64) new_cluster(p);
     }
-    step++;
     if (have) nsteps++;
-    // publish the step record, one granule per lane of wave 0, every granule tagged with the
-    // step; the kill-log entries are drained first (a late reader finds them there)
-    if (wv == 0) {
-      uint64_t *r = A.ring + (uint64_t)(step % RING) * A.rec_g;
-      // (kill-log entries are tagged granules: a worker that needs one checks its tag, so the
-      // record is not held back until they land)
-      for (int j = lane; j < rec_words; j += 64) st64(r + j, gran(step, rec_word(j, have, S, E)));
-      // `go` is only a hint for a worker that fell RING steps behind: it re-validates the
-      // record's tags after reading it
-      if (lane == 0) st32(A.go, step);
+    if (!A.spec || !have) {
+      step++;
+      if (wv == 0) publish(S, E, have);
     }
     if (A.prof && threadIdx.x == 0) {
       const uint64_t t = now();
@@ -1181,7 +1550,7 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
     if (!have) break;  // the record told the workers to stop
 
     // ============ collect the step (get_close's reduction + get_mean) ======================
-    constexpr uint64_t TS = WIDE ? (uint64_t)NW : (uint64_t)NT;
+    constexpr uint64_t TS = (uint64_t)TSZ;  // positions per tile of the workers' ownership
     uint64_t c0 = 0, c1 = 0;
     const uint32_t nact = rank_tiles(S / TS, E / TS, A.W, A.rank, &c0, &c1)
                               ? (uint32_t)(c1 - c0 + 1 < (uint64_t)GW ? c1 - c0 + 1 : (uint64_t)GW)
@@ -1587,10 +1956,13 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
 
 // NCH: compile-time chunks per row (0: A.nch at run time).
 // CPT: streaming rows with per-chunk compaction (A.cc; the resident form compiled out)
-template <typename T, int NCH, bool WIDE = false, bool CPT = false>
+// DENSE: dense resident workers (worker_dense, DT-position tiles)
+template <typename T, int NCH, bool WIDE = false, bool CPT = false, bool DENSE = false>
 __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
   extern __shared__ __attribute__((aligned(16))) uint4 dyn[];
-  if (blockIdx.x == 0) controller<T, NCH, WIDE>(A, dyn);
+  constexpr int TSZ = DENSE ? DT : WIDE ? NW : NT;
+  if (blockIdx.x == 0) controller<T, NCH, WIDE, TSZ>(A, dyn);
+  else if constexpr (DENSE) worker_dense<T, NCH>(A, C, dyn);
   else worker<T, NCH, WIDE, CPT>(A, C, dyn);
 }
 
@@ -1608,6 +1980,7 @@ struct AccPlan {
   bool gbits = false;  // bitmap in global memory
   bool wide = false;   // a wave per candidate (accum_kernel<T, 0, true>)
   bool compact = false;  // streaming rows with per-chunk compaction (A.cc)
+  bool dense = false;    // dense resident workers (worker_dense)
   uint32_t mrow = 0;   // member cache entries
   size_t lds = 0;
   uint32_t G = 0;
@@ -1658,8 +2031,24 @@ bool accum_plan(const mc_ctx *c, uint32_t nb, AccPlan *pl) {
   const size_t chunk_bytes = (size_t)nch * NT * 16;
   pl->res = (!wide && !getenv("MC_ACCUM_STREAM") && wfix + per_w * chunk_bytes <= cap) ? (int)per_w : 0;
   if (wfix >= cap) return false;
+  size_t wfix_dense = 0;
+  // dense resident workers: DT-position tiles round-robin, at most NT entries per worker
+  if (!wide && nch <= DMAXCH && !getenv("MC_ACCUM_NO_DENSE") && !getenv("MC_ACCUM_STREAM")) {
+    const uint64_t dchunks = ((c->norder + DT - 1) / DT + W - 1) / W;
+    const uint64_t dper = (dchunks + GW - 1) / GW;
+    const size_t dfix = (size_t)(pl->rec_g + 3) / 4 * 16 + (size_t)nch * NT * 16 + (size_t)NT * 4;
+    if (dper * DT <= (uint64_t)NT && dfix <= cap) {
+      pl->dense = true;
+      pl->res = 0;
+      pl->fcap = dper * DT;
+      wfix_dense = dfix;
+      pl->fn = c->width == 1 ? (nch == 16 ? reinterpret_cast<const void *>(&accum_kernel<uint8_t, 16, false, false, true>)
+                                          : reinterpret_cast<const void *>(&accum_kernel<uint8_t, 0, false, false, true>))
+                             : reinterpret_cast<const void *>(&accum_kernel<uint16_t, 0, false, false, true>);
+    }
+  }
   // streaming rows (config D): compacted per chunk by its worker, the slot list in LDS
-  pl->compact = !wide && nch == 16 && c->width == 1 && pl->res == 0 && per_w <= 64 && !getenv("MC_ACCUM_NO_COMPACT") &&
+  pl->compact = !pl->dense && !wide && nch == 16 && c->width == 1 && pl->res == 0 && per_w <= 64 && !getenv("MC_ACCUM_NO_COMPACT") &&
                 wfix + pl->fcap * 2 <= cap;
   if (pl->compact) pl->fn = reinterpret_cast<const void *>(&accum_kernel<uint8_t, 16, false, true>);
   // controller: mean row, column sums, bvec (+ bitmap unless global), member cache
@@ -1678,7 +2067,8 @@ bool accum_plan(const mc_ctx *c, uint32_t nb, AccPlan *pl) {
     if (m >= 64 || (gb == 1 && m >= 1)) {
       pl->gbits = gb != 0;
       pl->mrow = (uint32_t)m;
-      pl->lds = std::max(f + m * per_entry, wfix + (size_t)pl->res * chunk_bytes + (pl->compact ? pl->fcap * 2 : 0));
+      pl->lds = std::max(f + m * per_entry, pl->dense ? wfix_dense
+                                                      : wfix + (size_t)pl->res * chunk_bytes + (pl->compact ? pl->fcap * 2 : 0));
       return true;
     }
   }
@@ -1715,7 +2105,7 @@ int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, 
   const uint64_t fcap = pl.fcap;
   // s_a: go word + step ring; s_b: partials (+ global bitmap); s_c: flagged positions + kill
   // log; s_h: trace; s_i: member info (MInfo per static position); s_j: row-major static rows
-  const size_t ring_bytes = 256 + (size_t)RING * pl.rec_g * 8;
+  const size_t ring_bytes = 256 + (size_t)RING * pl.rec_g * 8 + (size_t)RING * 16;
   const size_t part_bytes = ((size_t)GW * PART_G * 8 + 255) / 256 * 256;
   const size_t bits_bytes = pl.gbits ? ((c->norder + 31) / 32 * 4 + 255) / 256 * 256 : 0;
   const size_t fpos_bytes = ((size_t)GW * fcap * 4 + 255) / 256 * 256;
@@ -1761,6 +2151,8 @@ int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, 
   A.gbits = d_bits;
   A.go = (uint32_t *)c->s_a.p;
   A.ring = (uint64_t *)((char *)c->s_a.p + 256);
+  A.ringb = A.ring + (size_t)RING * pl.rec_g;
+  A.spec = pl.dense && !getenv("MC_ACCUM_NO_SPEC") ? 1 : 0;
   A.rec_g = pl.rec_g;
   A.partials = (uint64_t *)c->s_b.p;
   char *sc = (char *)c->s_c.p;
@@ -1789,8 +2181,8 @@ int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, 
     A.trace_all = atoi(getenv("MC_ACCUM_PROFILE")) >= 3;
   }
   if (getenv("MC_ACCUM_PROFILE"))
-    fprintf(stderr, "[accum] variant: width %d nch %d wide %d resident chunks/worker %d compact %d global-bitmap %d member-cache %u lds %zu G %u rank %u/%u\n",
-            c->width, nch, (int)pl.wide, pl.res, (int)pl.compact, (int)pl.gbits, pl.mrow, pl.lds, G, A.rank, A.W);
+    fprintf(stderr, "[accum] variant: width %d nch %d wide %d dense %d resident chunks/worker %d compact %d global-bitmap %d member-cache %u lds %zu G %u rank %u/%u\n",
+            c->width, nch, (int)pl.wide, (int)pl.dense, pl.res, (int)pl.compact, (int)pl.gbits, pl.mrow, pl.lds, G, A.rank, A.W);
   DevClassifier cls = c->cls;
   void *args[] = {&A, &cls};
   timed_begin(c);
