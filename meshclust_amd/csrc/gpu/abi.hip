@@ -948,6 +948,47 @@ int mc_accumulate(mc_ctx *c, const uint32_t *bin_lo, const uint64_t *bounds, uin
     if (out[17])  // the controller's shader-clock ticks over its 100 MHz real-time ticks
       fprintf(stderr, "[accum] controller shader clock %.0f MHz over %.3f ms\n", (double)out[16] / ((double)out[17] / 100.0),
               out[17] / 1e5);
+    if (atoi(getenv("MC_ACCUM_PROFILE")) >= 4 && c->s_h.p) {
+      // dense workers, per step < 256: distribution of the active workers' times after the
+      // record (exact window) was published -- seen, scores done, partial stored -- and the
+      // controller's all-partials time
+      const int TW = 20, S2 = 256, G2 = 256, T2 = 6;  // accum.hip TRACE_W, TRACE2_STEPS, GMAX, T2W
+      std::vector<uint64_t> tr(4096 * TW), t2((size_t)S2 * G2 * T2);
+      MCG_CHECK(hipMemcpy(tr.data(), c->s_h.p, tr.size() * 8, hipMemcpyDeviceToHost));
+      MCG_CHECK(hipMemcpy(t2.data(), (char *)c->s_h.p + tr.size() * 8, t2.size() * 8, hipMemcpyDeviceToHost));
+      // columns: seen, scores (wave 0), part B (wave 0), after the B barrier, after the reduce
+      // barrier, partial stored
+      const int col[6] = {0, 1, 3, 4, 5, 2};
+      double acc[6][3] = {{0}}, all = 0, nw = 0;
+      uint64_t ns = 0;
+      for (int st = 2; st < S2; st++) {
+        const uint64_t t0 = tr[(size_t)st * TW], ta = tr[(size_t)st * TW + 7];
+        if (!t0 || !ta) continue;
+        std::vector<double> v[6];
+        for (int w = 0; w < G2; w++) {
+          const uint64_t *x = &t2[((size_t)st * G2 + w) * T2];
+          if (!x[2]) continue;
+          for (int i = 0; i < 6; i++) v[i].push_back(x[col[i]] ? (double)(int64_t)(x[col[i]] - t0) / 100 : 0.0);
+        }
+        if (v[5].empty()) continue;
+        for (int i = 0; i < 6; i++) {
+          std::sort(v[i].begin(), v[i].end());
+          acc[i][0] += v[i][0];
+          acc[i][1] += v[i][v[i].size() / 2];
+          acc[i][2] += v[i].back();
+        }
+        all += (double)(int64_t)(ta - t0) / 100;
+        nw += (double)v[5].size();
+        ns++;
+      }
+      if (ns) {
+        const char *nm[6] = {"seen", "scores", "partB", "last-wave-scores", "reduced", "partial"};
+        fprintf(stderr, "[accum trace4] %llu steps, %.1f workers, us after the exact window's publish (min/med/max):",
+                (unsigned long long)ns, nw / ns);
+        for (int i = 0; i < 6; i++) fprintf(stderr, " %s %.2f/%.2f/%.2f", nm[i], acc[i][0] / ns, acc[i][1] / ns, acc[i][2] / ns);
+        fprintf(stderr, "; controller all-seen %.2f\n", all / ns);
+      }
+    }
     if (atoi(getenv("MC_ACCUM_PROFILE")) >= 2 && c->s_h.p) {
       // per step (first 4096; accum.hip trace_mark): record published -> first / last active
       // worker saw it -> first / last scan done -> first / last partial stored -> controller

@@ -53,6 +53,8 @@ constexpr uint64_t NONE64 = ~0ull;
 constexpr uint32_t RING = 64;          // step records kept for workgroups that read them late
 constexpr uint32_t TRACE_STEPS = 4096;
 constexpr int TRACE_W = 20;            // trace words per step (MC_ACCUM_PROFILE=2), see trace_mark
+constexpr uint32_t TRACE2_STEPS = 256;
+constexpr int T2W = 6;  // trace2 words per worker and step
 constexpr int KINL = 4;                // kill-log entries carried inline in a step record
 constexpr int REC_HDR = 14;            // centre, S, E, kn, KINL kills, mag / sumsq / len (2 each)
 constexpr int PART_G = 8;              // granules per partial
@@ -109,6 +111,7 @@ struct AccArgs {
   uint64_t *ring;  // RING records of rec_g granules
   uint64_t *ringb;  // spec: RING x 2 granules, the exact window {S, E} of step s (NONE: no scan)
   int spec;         // the record carries a superset of the window; the exact one follows (dense)
+  int poll1;        // the controller polls a partial's tag granule before loading it whole
   uint32_t rec_g;
   uint64_t *klog;      // static positions killed by the controller (pop / erase), append-only,
                        // entry e a granule tagged e + 1 (a reader checks the tag: no drain
@@ -130,6 +133,8 @@ struct AccArgs {
   int prof;             // controller phase timers (MC_ACCUM_PROFILE)
   uint64_t *trace;      // MC_ACCUM_PROFILE>=2: per-step timestamps, TRACE_STEPS x TRACE_W
   int trace_all;        // MC_ACCUM_PROFILE=3: every active worker marks min/max (atomics)
+  uint64_t *trace2;     // MC_ACCUM_PROFILE=4 (dense form): per step < TRACE2_STEPS and worker,
+                        // {record seen, scores done, partial stored} (plain stores, no contention)
   // ranks: this one's tiles are t = lt * W + rank; mbox (host memory, device-mapped) non-null
   // when the ranks' kernels exchange every step, slot_g granules per rank slot
   uint32_t W, rank;
@@ -923,9 +928,10 @@ template <typename T, int NCH>
 __device__ __forceinline__ void worker_dense(const AccArgs &A, const DevClassifier &C, uint4 *dyn) {
   __shared__ double s_bv[NW];
   __shared__ uint64_t s_bp[NW];
-  __shared__ uint32_t s_nfl, s_nscan, s_go, s_inl[INL], s_wc[NW];
+  __shared__ uint32_t s_nfl, s_go, s_inl[INL], s_wc[NW];
   __shared__ int s_abort;
   __shared__ uint64_t s_b[2];  // spec: part B of the step, {tag << 32 | S}, {tag << 32 | E}
+  __shared__ uint64_t s_tw[NW];  // MC_ACCUM_PROFILE=4: each wave's scores-done time
   constexpr int NC = NCH > 0 ? NCH : DMAXCH;
   const uint32_t GW = gridDim.x - 1, w = blockIdx.x - 1;
   const Div32 dgw(GW);
@@ -1024,7 +1030,6 @@ __device__ __forceinline__ void worker_dense(const AccArgs &A, const DevClassifi
         if (state == 2) s_abort = 1;
         s_go = got;
         s_nfl = 0;
-        s_nscan = 0;
       }
     }
     __syncthreads();
@@ -1096,61 +1101,62 @@ __device__ __forceinline__ void worker_dense(const AccArgs &A, const DevClassifi
                      : classify_cand<T>(acc, pi_t, pc, A.B, C, &cv_t);
     }
     if (A.trace && t == 0) t_scanned = now();
+    if (A.trace2 && lane == 0) s_tw[wv] = now();
     uint64_t W_S = P_S, W_E = P_E;  // the exact window
     bool abandon = false;
+    uint64_t t_bgot = 0, t_red = 0;
     if (A.spec) {
-      // part B: from the LDS copy once a wave has it, else polled by this wave's lanes 0 / 1
+      // part B: from the LDS copy once a wave has it, else polled by this wave's lanes 0 / 1.
+      // (A wave that gives up marks the abort and takes the step as abandoned, so every wave
+      // still reaches the one barrier below.)
       const uint64_t *rb = A.ringb + (uint64_t)(seen % RING) * 2;
       const uint64_t t0 = now();
+      uint64_t b0 = 0, b1 = 0;
       for (uint32_t it = 1;; it++) {
-        const uint64_t b0 = __hip_atomic_load(&s_b[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        const uint64_t b1 = __hip_atomic_load(&s_b[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        b0 = __hip_atomic_load(&s_b[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        b1 = __hip_atomic_load(&s_b[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         if ((uint32_t)(b0 >> 32) == seen && (uint32_t)(b1 >> 32) == seen) break;
         const uint64_t g = lane < 2 ? ld64(rb + lane) : 0;
-        const uint64_t g0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(g >> 32), 0) << 32) |
-                            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)g, 0);
-        const uint64_t g1 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(g >> 32), 1) << 32) |
-                            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)g, 1);
-        if ((uint32_t)(g0 >> 32) == seen && (uint32_t)(g1 >> 32) == seen) {
+        b0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(g >> 32), 0) << 32) |
+             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)g, 0);
+        b1 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(g >> 32), 1) << 32) |
+             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)g, 1);
+        if ((uint32_t)(b0 >> 32) == seen && (uint32_t)(b1 >> 32) == seen) {
           if (lane == 0) {
-            __hip_atomic_store(&s_b[0], g0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            __hip_atomic_store(&s_b[1], g1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_store(&s_b[0], b0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_store(&s_b[1], b1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           }
           break;
         }
         if ((it & 255) == 0 && timed_out(A, t0)) {
           if (lane == 0) s_abort = 1;
+          b0 = b1 = NONE;
           break;
         }
         __builtin_amdgcn_s_sleep(1);
       }
-      __syncthreads();
-      if (s_abort) {
-        if (t == 0) atomicMax((unsigned long long *)&A.out[3], 99ull);
-        return;
-      }
-      W_S = (uint32_t)s_b[0];
-      W_E = (uint32_t)s_b[1];
+      if (A.trace2 && t == 0) t_bgot = now();
+      W_S = (uint32_t)b0;
+      W_E = (uint32_t)b1;
       abandon = (uint32_t)W_S == NONE;
     }
     uint64_t c0 = 0, c1 = 0;
     const bool any_tile = !abandon && rank_tiles(W_S / DT, W_E / DT, A.W, A.rank, &c0, &c1);
     const uint32_t nact = any_tile ? (uint32_t)(c1 - c0 + 1 < (uint64_t)GW ? c1 - c0 + 1 : (uint64_t)GW) : 0u;
     const uint32_t mine = any_tile ? dgw.mod(w + GW - dgw.mod((uint32_t)c0)) : 0u;
-    const bool active = any_tile && mine < nact;
+    const bool active = any_tile && mine < nact;  // (uniform: every wave has the same part B)
     bool died = false;
     if (active) {
       double best_v = -1.0;
       uint64_t best_p = NONE64;
       uint32_t nscan = 0;
-      const uint64_t base = (uint64_t)w * A.fcap;
       if (comp && pos_t >= W_S && pos_t <= W_E) {
         nscan = 1;
         if (d_t) {
           al_t = false;
           const uint32_t idx = atomicAdd(&s_nfl, 1u);
           if (idx < (uint32_t)INL) s_inl[idx] = pos_t;
-          else st32(A.fpos + base + idx, pos_t);
+          else st32(A.fpos + (uint64_t)w * A.fcap + idx, pos_t);
         }
         if (cv_t > -1.0) {
           best_v = cv_t;
@@ -1162,42 +1168,68 @@ __device__ __forceinline__ void worker_dense(const AccArgs &A, const DevClassifi
       if (lane == 0) {
         s_bv[wv] = best_v;
         s_bp[wv] = best_p;
-        if (nscan) atomicAdd(&s_nscan, nscan);
+        s_wc[wv] = nscan;
       }
       drain();  // this wave's flagged-list stores are complete before the partial announces them
-      __syncthreads();
-      if (t < PART_G) {
-        double v = s_bv[0];
-        uint64_t p = s_bp[0];
-        for (int i = 1; i < NW; i++)
-          if (better(s_bv[i], s_bp[i], v, p)) {
-            v = s_bv[i];
-            p = s_bp[i];
-          }
-        const uint64_t vb = (uint64_t)__double_as_longlong(v);
-        const int j = (int)t;
-        const uint32_t nfl = s_nfl;
-        const uint32_t data = j == 0   ? (uint32_t)(vb >> 32)
-                              : j == 1 ? (uint32_t)vb
-                              : j == 2 ? (p == NONE64 ? NONE : (uint32_t)p)
-                              : j == 3 ? nfl
-                              : j == 4 ? s_nscan
-                                       : ((uint32_t)(j - 5) < nfl ? s_inl[j - 5] : NONE);
-        st64(A.partials + (uint64_t)w * PART_G + j, gran(seen, data));
-        if (A.trace && !A.trace_all && j == 0 && mine == nact / 2 && seen < TRACE_STEPS) {
-          uint64_t *tr = A.trace + (uint64_t)seen * TRACE_W;
-          tr[10] = t_seen;
-          tr[11] = t_klog;
-          tr[12] = t_scanned;
-          tr[13] = t_scanned;
-          tr[14] = now();
+    }
+    __syncthreads();  // the one barrier between the scores and the partial
+    if (A.trace2 && t == 0) t_red = now();
+    if (s_abort) {
+      if (t == 0) atomicMax((unsigned long long *)&A.out[3], 99ull);
+      return;
+    }
+    if (active && t < PART_G) {
+      double vv[NW];
+      uint64_t pp[NW];
+      uint32_t ns = 0;
+#pragma unroll
+      for (int i = 0; i < NW; i++) {
+        vv[i] = s_bv[i];
+        pp[i] = s_bp[i];
+        ns += s_wc[i];
+      }
+      double v = vv[0];
+      uint64_t p = pp[0];
+#pragma unroll
+      for (int i = 1; i < NW; i++)
+        if (better(vv[i], pp[i], v, p)) {
+          v = vv[i];
+          p = pp[i];
         }
-        if (A.trace && A.trace_all && j == 0) {
-          const uint64_t tn = now();
-          trace_mark(A, seen, 1, t_seen);
-          trace_mark(A, seen, 3, t_scanned);
-          trace_mark(A, seen, 5, tn);
-        }
+      const uint64_t vb = (uint64_t)__double_as_longlong(v);
+      const int j = (int)t;
+      const uint32_t nfl = s_nfl;
+      const uint32_t data = j == 0   ? (uint32_t)(vb >> 32)
+                            : j == 1 ? (uint32_t)vb
+                            : j == 2 ? (p == NONE64 ? NONE : (uint32_t)p)
+                            : j == 3 ? nfl
+                            : j == 4 ? ns
+                                     : ((uint32_t)(j - 5) < nfl ? s_inl[j - 5] : NONE);
+      st64(A.partials + (uint64_t)w * PART_G + j, gran(seen, data));
+      if (A.trace && !A.trace_all && j == 0 && mine == nact / 2 && seen < TRACE_STEPS) {
+        uint64_t *tr = A.trace + (uint64_t)seen * TRACE_W;
+        tr[10] = t_seen;
+        tr[11] = t_klog;
+        tr[12] = t_scanned;
+        tr[13] = t_scanned;
+        tr[14] = now();
+      }
+      if (A.trace && A.trace_all && j == 0) {
+        const uint64_t tn = now();
+        trace_mark(A, seen, 1, t_seen);
+        trace_mark(A, seen, 3, t_scanned);
+        trace_mark(A, seen, 5, tn);
+      }
+      if (A.trace2 && j == 0 && seen < TRACE2_STEPS) {
+        uint64_t *tr = A.trace2 + ((uint64_t)seen * GMAX + w) * T2W;
+        tr[0] = t_seen;
+        tr[1] = t_scanned;
+        tr[2] = now();
+        uint64_t tw = 0;
+        for (int i = 0; i < NW; i++) tw = s_tw[i] > tw ? s_tw[i] : tw;
+        tr[3] = t_bgot;
+        tr[4] = tw;
+        tr[5] = t_red;
       }
     }
     // ---- compaction (off the critical path: the controller is collecting) ----------------
@@ -1569,15 +1601,23 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
       const uint64_t t0 = now();
       uint64_t g8[PART_G];
       for (uint32_t it = 1;; it++) {
-        // one granule per poll (less traffic in the CU's memory queue); all of them, each
-        // checked, once that one carries the step
-        bool ok = (uint32_t)(ld64(q + 4 + INL) >> 32) == step;
-        if (ok) {
+        // the whole partial per poll: one round trip once it has landed (A.poll1: the tag
+        // granule first, then all of them)
+        bool ok = true;
+        if (A.poll1) {
+          ok = (uint32_t)(ld64(q + 4 + INL) >> 32) == step;
+          if (ok) {
 #pragma unroll
-          for (int j = 0; j < 5 + INL; j++) {
-            g8[j] = ld64(q + j);
-            ok &= (uint32_t)(g8[j] >> 32) == step;
+            for (int j = 0; j < 5 + INL; j++) {
+              g8[j] = ld64(q + j);
+              ok &= (uint32_t)(g8[j] >> 32) == step;
+            }
           }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 5 + INL; j++) g8[j] = ld64(q + j);
+#pragma unroll
+          for (int j = 0; j < 5 + INL; j++) ok &= (uint32_t)(g8[j] >> 32) == step;
         }
         if (ok) break;
         if ((it & 255) == 0 && timed_out(A, t0)) {
@@ -1591,10 +1631,11 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
         bp_ = (uint32_t)g8[2] == NONE ? NONE64 : (uint64_t)(uint32_t)g8[2];
         cnt_w = (uint32_t)g8[3];
         scan_w = (uint32_t)g8[4];
-        // this worker's flagged positions into the step's list (a slot per position)
+        // this worker's flagged positions into the step's list: cnt_w slots reserved at once
+        const uint32_t slot0 = cnt_w ? atomicAdd(&s_new, cnt_w) : 0u;
         for (uint32_t j = 0; j < cnt_w; j++) {
           const uint32_t p = j < (uint32_t)INL ? (uint32_t)g8[5 + j] : ld32(A.fpos + (uint64_t)wk * A.fcap + j);
-          const uint32_t slot = atomicAdd(&s_new, 1u);
+          const uint32_t slot = slot0 + j;
           if (mslot) {  // (several ranks: every rank takes the union, below)
             st64x(mslot + (slot < (uint32_t)MBOX_INL ? 5 + slot : MBOX_HDR - MBOX_INL + slot), gran(step, p));
           } else if (slot < PLIST) {
@@ -2153,6 +2194,7 @@ int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, 
   A.ring = (uint64_t *)((char *)c->s_a.p + 256);
   A.ringb = A.ring + (size_t)RING * pl.rec_g;
   A.spec = pl.dense && !getenv("MC_ACCUM_NO_SPEC") ? 1 : 0;
+  A.poll1 = getenv("MC_ACCUM_POLL1") ? 1 : 0;
   A.rec_g = pl.rec_g;
   A.partials = (uint64_t *)c->s_b.p;
   char *sc = (char *)c->s_c.p;
@@ -2175,10 +2217,12 @@ int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, 
   A.prof = getenv("MC_ACCUM_PROFILE") ? 1 : 0;
   A.trace = nullptr;
   if (getenv("MC_ACCUM_PROFILE") && atoi(getenv("MC_ACCUM_PROFILE")) >= 2) {
-    if (ensure(c->s_h, TRACE_STEPS * TRACE_W * 8)) return MC_ERR_OOM;
-    MCG_CHECK(hipMemsetAsync(c->s_h.p, 0, TRACE_STEPS * TRACE_W * 8, c->stream));
+    const size_t tb = TRACE_STEPS * TRACE_W * 8, tb2 = (size_t)TRACE2_STEPS * GMAX * T2W * 8;
+    if (ensure(c->s_h, tb + tb2)) return MC_ERR_OOM;
+    MCG_CHECK(hipMemsetAsync(c->s_h.p, 0, tb + tb2, c->stream));
     A.trace = (uint64_t *)c->s_h.p;
-    A.trace_all = atoi(getenv("MC_ACCUM_PROFILE")) >= 3;
+    A.trace_all = atoi(getenv("MC_ACCUM_PROFILE")) == 3;
+    A.trace2 = atoi(getenv("MC_ACCUM_PROFILE")) >= 4 ? (uint64_t *)((char *)c->s_h.p + tb) : nullptr;
   }
   if (getenv("MC_ACCUM_PROFILE"))
     fprintf(stderr, "[accum] variant: width %d nch %d wide %d dense %d resident chunks/worker %d compact %d global-bitmap %d member-cache %u lds %zu G %u rank %u/%u\n",
