@@ -141,6 +141,25 @@ int mc_distance_keys(mc_ctx *ctx, const uint32_t *pivots, uint32_t npiv, const u
                      uint64_t m, uint16_t *keys);
 
 /*
+ * Trainer::split's per-pivot sorts on the device (Trainer.cpp:691-701: std::sort of the
+ * points by distance to each pivot, then reads of ~35 positions of each sorted array by the
+ * alignment binary search, :703-721, and the sampler, :732-755).
+ *   mc_split_begin: for pivot p, the array std::sort is called on is (key << 32 | id) over
+ *     `order` (keys as mc_distance_keys); it stays in HBM.
+ *   mc_split_select: ids[i] = the id std::sort (libstdc++ introsort, ties included) puts at
+ *     position pos[i] of pivot arr[i]'s array; only the ranges holding the queried positions
+ *     are partitioned, and the partitions persist for later calls.
+ *   mc_split_begin_words / mc_split_select_words: the same on arbitrary word arrays compared
+ *     by their upper 32 bits (depth < 0: std::sort's 2 floor(log2 n) limit), returning words.
+ *   mc_split_end: frees the arrays.
+ */
+int mc_split_begin(mc_ctx *ctx, const uint32_t *pivots, uint32_t npiv, const uint32_t *order, uint64_t n);
+int mc_split_begin_words(mc_ctx *ctx, const uint64_t *words, uint32_t narr, uint64_t n, int depth);
+int mc_split_select(mc_ctx *ctx, uint64_t nq, const uint32_t *arr, const uint64_t *pos, uint32_t *ids);
+int mc_split_select_words(mc_ctx *ctx, uint64_t nq, const uint32_t *arr, const uint64_t *pos, uint64_t *words);
+int mc_split_end(mc_ctx *ctx);
+
+/*
  * raw[i * nflag + f] = Feature<T>::raw(flags[f], *points[a[i]], *points[b[i]])
  * (Feature.cpp:117-160) for the k-mer features LD/MANHATTAN/INTERSECTION/PEARSON/
  * KULCZYNSKI2.  Used by Feature::normalize (Feature.cpp:86-114).

@@ -200,7 +200,8 @@ int mc_ctx_destroy(mc_ctx *c) {
   for (Buf *b : {&c->codes, &c->seq_off, &c->seg, &c->seg_off, &c->packed, &c->pk_off, &c->impure, &c->hist, &c->mag, &c->sumsq, &c->len, &c->order,
                  &c->alive, &c->members, &c->member_keys, &c->partials, &c->scan_dev, &c->flags_out, &c->s_a, &c->s_b,
                  &c->s_c, &c->s_d, &c->s_e, &c->s_f, &c->s_g, &c->s_h, &c->s_i, &c->s_j, &c->s_k, &c->hs, &c->mag_s, &c->sumsq_s, &c->len_s, &c->ticket,
-                 &c->msum, &c->ident_s, &c->al_a, &c->al_b, &c->al_out, &c->acc_out})
+                 &c->msum, &c->ident_s, &c->al_a, &c->al_b, &c->al_out, &c->acc_out, &c->sp_words, &c->sp_keys,
+                 &c->sp_scr, &c->sp_nodes, &c->sp_nn, &c->sp_q, &c->sp_err})
     release(*b);
   if (c->h_scan) (void)hipHostFree(c->h_scan);
   if (c->h_stage) (void)hipHostFree(c->h_stage);
@@ -377,6 +378,130 @@ int mc_distance_keys(mc_ctx *c, const uint32_t *pivots, uint32_t npiv, const uin
   TRY(download(keys, c->s_c.p, (size_t)npiv * m, c->stream));
   MCG_CHECK(hipStreamSynchronize(c->stream));
   flush_timers(c);
+  return MC_OK;
+}
+
+// ---- Trainer::split's sorts (split.hip) -----------------------------------------------------
+static int split_reset(mc_ctx *c, uint32_t narr, uint64_t n, int depth) {
+  if (n >= (1ull << 32)) {
+    set_error("mc_split: arrays of 2^32 elements or more");
+    return MC_ERR_ARG;
+  }
+  TRY(ensure(c->sp_scr, (size_t)narr * 2 * n * 4 + 16));
+  TRY(ensure(c->sp_nodes, (size_t)narr * SPLIT_MAXNODE * sizeof(SplitNode)));
+  TRY(ensure(c->sp_nn, (size_t)narr * 4 + 16));
+  TRY(ensure(c->sp_err, 16));
+  MCG_CHECK(hipMemsetAsync(c->sp_nn.p, 0, (size_t)narr * 4, c->stream));
+  MCG_CHECK(hipMemsetAsync(c->sp_err.p, 0, 16, c->stream));
+  int lg = 0;
+  while (n >> (lg + 1)) lg++;
+  c->sp_n = n;
+  c->sp_narr = narr;
+  c->sp_depth0 = depth >= 0 ? depth : 2 * lg;
+  return MC_OK;
+}
+
+int mc_split_begin(mc_ctx *c, const uint32_t *pivots, uint32_t npiv, const uint32_t *order, uint64_t n) {
+  if (!c || c->k == 0) return MC_ERR_STATE;
+  if (!npiv || !n) return MC_ERR_ARG;
+  MCG_CHECK(hipSetDevice(c->device));
+  TRY(check_ids(c, pivots, npiv));
+  TRY(check_ids(c, order, n));
+  TRY(upload(c, c->s_a, pivots, npiv, c->stream));
+  TRY(upload(c, c->s_b, order, n, c->stream));
+  TRY(ensure(c->sp_keys, (size_t)npiv * n * 2 + 16));
+  TRY(ensure(c->sp_words, (size_t)npiv * n * 8 + 16));
+  TRY(split_reset(c, npiv, n, -1));
+  TRY(launch_distance_keys(c, (uint32_t *)c->s_a.p, npiv, (uint32_t *)c->s_b.p, n, (uint16_t *)c->sp_keys.p));
+  TRY(split_build_words(c, (uint32_t *)c->s_b.p, n, npiv, (uint16_t *)c->sp_keys.p, (uint64_t *)c->sp_words.p));
+  MCG_CHECK(hipStreamSynchronize(c->stream));
+  flush_timers(c);
+  return MC_OK;
+}
+
+int mc_split_begin_words(mc_ctx *c, const uint64_t *words, uint32_t narr, uint64_t n, int depth) {
+  if (!c || !words || !narr || !n) return MC_ERR_ARG;
+  MCG_CHECK(hipSetDevice(c->device));
+  TRY(ensure(c->sp_words, (size_t)narr * n * 8 + 16));
+  MCG_CHECK(hipMemcpyAsync(c->sp_words.p, words, (size_t)narr * n * 8, hipMemcpyHostToDevice, c->stream));
+  TRY(split_reset(c, narr, n, depth));
+  MCG_CHECK(hipStreamSynchronize(c->stream));
+  return MC_OK;
+}
+
+int mc_split_select_words(mc_ctx *c, uint64_t nq, const uint32_t *arr, const uint64_t *pos, uint64_t *out) {
+  if (!c) return MC_ERR_ARG;
+  if (!c->sp_narr) return MC_ERR_STATE;
+  if (!nq) return MC_OK;
+  for (uint64_t i = 0; i < nq; i++)
+    if (arr[i] >= c->sp_narr || pos[i] >= c->sp_n) {
+      set_error("mc_split_select: array index or position out of range");
+      return MC_ERR_ARG;
+    }
+  MCG_CHECK(hipSetDevice(c->device));
+  // queries grouped by array (counting sort; one workgroup per array with queries)
+  std::vector<uint64_t> cnt(c->sp_narr + 1, 0);
+  for (uint64_t i = 0; i < nq; i++) cnt[arr[i] + 1]++;
+  for (uint32_t a = 0; a < c->sp_narr; a++) cnt[a + 1] += cnt[a];
+  std::vector<uint64_t> qpos(nq), slot(nq);
+  {
+    std::vector<uint64_t> fill(cnt.begin(), cnt.end() - 1);
+    for (uint64_t i = 0; i < nq; i++) {
+      const uint64_t j = fill[arr[i]]++;
+      qpos[j] = pos[i];
+      slot[i] = j;
+    }
+  }
+  std::vector<uint32_t> qarr;
+  std::vector<uint64_t> qoff;
+  for (uint32_t a = 0; a < c->sp_narr; a++)
+    if (cnt[a + 1] > cnt[a]) {
+      qarr.push_back(a);
+      qoff.push_back(cnt[a]);
+    }
+  qoff.push_back(nq);
+  const uint32_t ng = (uint32_t)qarr.size();
+  // one buffer: qarr | qoff | qpos | qout
+  const size_t o_off = ((size_t)ng * 4 + 15) / 16 * 16, o_pos = o_off + (size_t)(ng + 1) * 8, o_out = o_pos + nq * 8;
+  TRY(ensure(c->sp_q, o_out + nq * 8 + 16));
+  std::vector<uint8_t> hq(o_out);
+  memcpy(hq.data(), qarr.data(), (size_t)ng * 4);
+  memcpy(hq.data() + o_off, qoff.data(), (size_t)(ng + 1) * 8);
+  memcpy(hq.data() + o_pos, qpos.data(), nq * 8);
+  uint8_t *dq = (uint8_t *)c->sp_q.p;
+  TRY(upload(c, c->sp_q, hq.data(), hq.size(), c->stream));
+  timed_begin(c);
+  TRY(launch_select(c, (uint64_t *)c->sp_words.p, c->sp_n, (uint32_t *)c->sp_scr.p, (SplitNode *)c->sp_nodes.p,
+                    (int32_t *)c->sp_nn.p, SPLIT_MAXNODE, c->sp_depth0, ng, (const uint32_t *)dq,
+                    (const uint64_t *)(dq + o_off), (const uint64_t *)(dq + o_pos), (uint64_t *)(dq + o_out),
+                    (int *)c->sp_err.p));
+  timed_end(c, F_KEYS);
+  std::vector<uint64_t> qout(nq);
+  int err = 0;
+  MCG_CHECK(hipMemcpyAsync(qout.data(), dq + o_out, nq * 8, hipMemcpyDeviceToHost, c->stream));
+  MCG_CHECK(hipMemcpyAsync(&err, c->sp_err.p, 4, hipMemcpyDeviceToHost, c->stream));
+  MCG_CHECK(hipStreamSynchronize(c->stream));
+  flush_timers(c);
+  if (err) {
+    set_error("mc_split_select: more partitioned ranges than the device tree holds");
+    return MC_ERR_UNSUPPORTED;
+  }
+  for (uint64_t i = 0; i < nq; i++) out[i] = qout[slot[i]];
+  return MC_OK;
+}
+
+int mc_split_select(mc_ctx *c, uint64_t nq, const uint32_t *arr, const uint64_t *pos, uint32_t *ids) {
+  std::vector<uint64_t> w(nq);
+  TRY(mc_split_select_words(c, nq, arr, pos, w.data()));
+  for (uint64_t i = 0; i < nq; i++) ids[i] = (uint32_t)w[i];
+  return MC_OK;
+}
+
+int mc_split_end(mc_ctx *c) {
+  if (!c) return MC_ERR_ARG;
+  for (Buf *b : {&c->sp_words, &c->sp_keys, &c->sp_scr, &c->sp_nodes, &c->sp_nn, &c->sp_q}) release(*b);
+  c->sp_narr = 0;
+  c->sp_n = 0;
   return MC_OK;
 }
 

@@ -70,6 +70,13 @@ struct Buf {
   size_t bytes = 0;
 };
 
+// A range of one array of the device lazy introsort (split.hip): partitioned (left >= 0:
+// children left, left + 1, cut between them) or finished (fin: a sorted leaf).
+struct SplitNode {
+  int64_t lo, hi, cut;
+  int32_t depth, left, fin, pad;
+};
+
 // Pinned, device-mapped record the fused scan publishes (zero-copy; seq written last).
 struct HostScan {
   mc_scan_result r;
@@ -120,6 +127,11 @@ struct mc_ctx {
   std::vector<uint8_t> h_alive;
   mcg::Buf ident_s, al_a, al_b, al_out;
   mcg::Buf acc_out;  // device-resident accumulation: counters / error word
+  // Trainer::split's sorted arrays (mc_split_*): words, stopper scratch, range trees, queries
+  mcg::Buf sp_words, sp_keys, sp_scr, sp_nodes, sp_nn, sp_q, sp_err;
+  uint64_t sp_n = 0;
+  uint32_t sp_narr = 0;
+  int sp_depth0 = 0;
   // several ranks sharing one accumulation (mc_set_mailbox): host-memory mailbox, mapped
   void *mb_host = nullptr, *mb_dev = nullptr;
   uint64_t mb_bytes = 0;
@@ -153,6 +165,13 @@ int launch_pack(mc_ctx *c);
 int launch_kmer(mc_ctx *c, int k, int width, bool write, uint64_t *d_max, int *d_err);
 int launch_distance_keys(mc_ctx *c, const uint32_t *d_piv, uint32_t npiv, const uint32_t *d_ids, uint64_t m,
                          uint16_t *d_keys);
+// split.hip: words[p * n + t] = keys[p * n + t] << 32 | order[t]; the lazy introsort's queries
+constexpr int32_t SPLIT_MAXNODE = 32768;
+int split_build_words(mc_ctx *c, const uint32_t *d_order, uint64_t n, uint32_t npiv, const uint16_t *d_keys,
+                      uint64_t *d_words);
+int launch_select(mc_ctx *c, uint64_t *d_words, uint64_t n, uint32_t *d_scr, SplitNode *d_nodes, int32_t *d_nnodes,
+                  int32_t maxnode, int32_t depth0, uint32_t ngroups, const uint32_t *d_qarr, const uint64_t *d_qoff,
+                  const uint64_t *d_qpos, uint64_t *d_qout, int *d_err);
 int launch_pairs(mc_ctx *c, const uint32_t *d_a, const uint32_t *d_b, uint64_t m, const uint16_t *flags, int nflag,
                  double *d_raw, uint8_t *d_sim, double *d_c0, double *d_sum, bool classify);
 int launch_scan(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, const double *d_ident, int *nblocks);

@@ -1,0 +1,380 @@
+// split.hip -- Trainer::split's per-pivot std::sort (Trainer.cpp:691-701), evaluated on the
+// device at exactly the positions the trainer reads.
+//
+// The trainer sorts all N points by their distance key to each of ~150 pivots with std::sort
+// (an unstable introsort: among equal keys -- keys are integers <= 10000, ties are everywhere --
+// the order is defined only by that algorithm) and then reads ~35 positions of each sorted
+// array (the alignment binary search, Trainer.cpp:703-721, and the sampler, :732-755).  The
+// host's mc::LazyIntroSort (csrc/host/lazysort.hpp) reproduces libstdc++'s result at a queried
+// position by partitioning only the ranges that hold it; this file is the same algorithm with
+// each pivot's array resident in HBM and its partitions done by one workgroup:
+//   * std::__introsort_loop: median of (first+1, mid, last-1) moved to first, then the
+//     unguarded Hoare partition of [first+1, last) around it; depth limit 2 floor(log2 n)
+//     with std::make_heap + std::sort_heap below it; ranges of <= 16 elements are leaves,
+//     finished by a stable insertion sort (what __final_insertion_sort does to them).
+//   * The Hoare partition as data-parallel passes: the left scan stops at keys >= pivot
+//     (positions l_1 < l_2 < ...), the right scan at keys <= pivot (r_1 > r_2 > ...); the k-th
+//     swap exchanges l_k and r_k of the array as it was before the partition for every k <= K,
+//     K the last k with l_k < r_k (no scan reads a position an earlier swap wrote before the
+//     scans cross, so all K swaps are independent), and the cut is min(l_{K+1}, r_K).  A
+//     workgroup counts the stoppers of its threads' segments, writes their positions in order
+//     (exclusive scan), finds K by a two-round parallel bisection and does the K swaps at once.
+// Elements are 64-bit words (key << 32 | id) compared by the key alone.  Each pivot's tree of
+// partitioned ranges persists across calls (the trainer's rounds query deeper positions of
+// the same arrays).
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+
+#include "mcgpu.hpp"
+
+namespace mcg {
+
+namespace {
+
+constexpr int ST = 1024;  // threads per workgroup
+constexpr int SW = ST / 64;
+// A range of at most LMAX words still to be partitioned is copied into LDS and its query's
+// walk finishes there (every level a few LDS passes instead of global round trips); the range
+// is written back at the end.  LDS: LMAX words | left / right stopper positions (u16)
+constexpr int64_t LMAX = 8192;
+constexpr size_t SEL_LDS = (size_t)LMAX * 8 + 2 * (size_t)LMAX * 2;
+
+__device__ __forceinline__ bool kless(uint64_t x, uint64_t y) { return (x >> 32) < (y >> 32); }
+
+__device__ void insertion_sort_1(uint64_t *f, int64_t n) {  // std::__insertion_sort (stable)
+  for (int64_t i = 1; i < n; i++) {
+    const uint64_t v = f[i];
+    int64_t j = i;
+    while (j > 0 && kless(v, f[j - 1])) {
+      f[j] = f[j - 1];
+      j--;
+    }
+    f[j] = v;
+  }
+}
+
+// libstdc++'s std::__adjust_heap / std::__push_heap with the key comparator
+__device__ void adjust_heap_1(uint64_t *f, int64_t hole, int64_t len, uint64_t v) {
+  const int64_t top = hole;
+  int64_t child = hole;
+  while (child < (len - 1) / 2) {
+    child = 2 * (child + 1);
+    if (kless(f[child], f[child - 1])) child--;
+    f[hole] = f[child];
+    hole = child;
+  }
+  if ((len & 1) == 0 && child == (len - 2) / 2) {
+    child = 2 * (child + 1);
+    f[hole] = f[child - 1];
+    hole = child - 1;
+  }
+  int64_t parent = (hole - 1) / 2;
+  while (hole > top && kless(f[parent], v)) {
+    f[hole] = f[parent];
+    hole = parent;
+    parent = (hole - 1) / 2;
+  }
+  f[hole] = v;
+}
+
+// std::__partial_sort(first, last, last) = std::__make_heap + std::__sort_heap (one thread:
+// reached only below the depth limit, i.e. on degenerate partitions)
+__device__ void heap_sort_1(uint64_t *f, int64_t n) {
+  if (n < 2) return;
+  for (int64_t parent = (n - 2) / 2;; parent--) {
+    adjust_heap_1(f, parent, n, f[parent]);
+    if (parent == 0) break;
+  }
+  for (int64_t last = n; last > 1;) {
+    last--;
+    const uint64_t v = f[last];
+    f[last] = f[0];
+    adjust_heap_1(f, 0, last, v);
+  }
+}
+
+struct SelArgs {
+  uint64_t *words;   // narr arrays of n words
+  uint64_t n;
+  uint32_t *scr;     // narr x 2n: left stoppers | right stoppers (positions, ascending)
+  SplitNode *nodes;  // narr x maxnode
+  int32_t *nnodes;   // narr
+  int32_t maxnode;
+  int32_t depth0;    // the root's depth limit (2 floor(log2 n), or a test override)
+  const uint32_t *qarr;  // per workgroup: its array
+  const uint64_t *qoff;  // per workgroup: its queries [qoff[b], qoff[b + 1])
+  const uint64_t *qpos;  // query positions
+  uint64_t *qout;        // the word std::sort puts at each queried position
+  int *err;
+  unsigned long long *prof;  // MC_SPLIT_PROFILE: thread 0's realtime ticks per phase (8 counters)
+};
+
+// Workgroup-wide exclusive scan of two counters (every thread gets its offsets and the totals).
+__device__ __forceinline__ void block_scan2(uint32_t a, uint32_t b, uint32_t *ea, uint32_t *eb, uint32_t *ta,
+                                            uint32_t *tb, uint32_t *s) {
+  const int lane = threadIdx.x & 63, wv = wave_id();
+  uint32_t ia = a, ib = b;  // inclusive scans within the wave
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t ua = (uint32_t)__shfl_up((int)ia, o, 64), ub = (uint32_t)__shfl_up((int)ib, o, 64);
+    if (lane >= o) {
+      ia += ua;
+      ib += ub;
+    }
+  }
+  if (lane == 63) {
+    s[wv] = ia;
+    s[SW + wv] = ib;
+  }
+  __syncthreads();
+  uint32_t pa = 0, pb = 0, sa = 0, sb = 0;
+  for (int i = 0; i < SW; i++) {
+    if (i < wv) {
+      pa += s[i];
+      pb += s[SW + i];
+    }
+    sa += s[i];
+    sb += s[SW + i];
+  }
+  *ea = pa + ia - a;
+  *eb = pb + ib - b;
+  *ta = sa;
+  *tb = sb;
+  __syncthreads();  // s is reused by the caller's next scan
+}
+
+// One workgroup partitions f[0, n) (n > 16) exactly as std::__unguarded_partition_pivot;
+// returns the cut.  L / R: scratch for n positions each (global u32, or LDS u16 when f is the
+// LDS copy of a range of at most LMAX words).
+template <typename PT>
+__device__ int64_t partition_wg(uint64_t *f, int64_t n, PT *L, PT *R, uint32_t *s32, uint64_t *s64) {
+  const int t = threadIdx.x;
+  if (t == 0) {  // std::__move_median_to_first(first, first + 1, mid, last - 1)
+    const uint64_t a = f[1], b = f[n / 2], c = f[n - 1];
+    int64_t m;
+    if (kless(a, b)) m = kless(b, c) ? n / 2 : kless(a, c) ? n - 1 : 1;
+    else m = kless(a, c) ? 1 : kless(b, c) ? n - 1 : n / 2;
+    const uint64_t x = f[0];
+    f[0] = f[m];
+    f[m] = x;
+  }
+  __syncthreads();
+  const uint64_t pk = f[0] >> 32;
+  // segments of S consecutive positions per thread
+  const int64_t S = (n + ST - 1) / ST;
+  const int64_t i0 = (int64_t)t * S < n ? (int64_t)t * S : n, i1 = i0 + S < n ? i0 + S : n;
+  uint32_t cg = 0, cl = 0;
+  for (int64_t i = i0; i < i1; i++) {
+    const uint64_t k = f[i] >> 32;
+    cg += (i >= 1 && k >= pk) ? 1u : 0u;
+    cl += k <= pk ? 1u : 0u;
+  }
+  uint32_t og, ol, CL, TL;
+  block_scan2(cg, cl, &og, &ol, &CL, &TL, s32);
+  for (int64_t i = i0; i < i1; i++) {
+    const uint64_t k = f[i] >> 32;
+    if (i >= 1 && k >= pk) L[og++] = (PT)i;
+    if (k <= pk) R[ol++] = (PT)i;
+  }
+  __syncthreads();
+  // K = the last k with l_k < r_k (l_k = L[k - 1], r_k = R[TL - k]); monotone in k: bisection
+  // over (lo, hi) with P(lo) true, P(hi) false, ST probes per round
+  const int64_t m = CL < TL ? CL : TL;
+  int64_t lo = 0, hi = m + 1;
+  while (hi - lo > 1) {
+    const int64_t span = hi - lo;
+    const int64_t k = lo + 1 + ((span - 1) * (int64_t)t) / ST;  // in (lo, hi), nondecreasing in t
+    const bool p = L[k - 1] < R[TL - k];
+    const uint64_t bal = __ballot(p);
+    if ((t & 63) == 0) s32[wave_id()] = (uint32_t)__popcll(bal);
+    __syncthreads();
+    uint32_t c = 0;
+    for (int i = 0; i < SW; i++) c += s32[i];
+    // the probes with P true are a prefix (threads 0 .. c - 1): the new bracket is between the
+    // last true probe and the first false one
+    if (t == (int)c - 1) s64[0] = (uint64_t)k;
+    if (t == (int)c) s64[1] = (uint64_t)k;
+    __syncthreads();
+    const int64_t nlo = c > 0 ? (int64_t)s64[0] : lo, nhi = c < (uint32_t)ST ? (int64_t)s64[1] : hi;
+    __syncthreads();
+    lo = nlo;
+    hi = nhi;
+  }
+  const int64_t K = lo;
+  for (int64_t k = 1 + t; k <= K; k += ST) {
+    const uint32_t a = (uint32_t)L[k - 1], b = (uint32_t)R[TL - k];
+    const uint64_t x = f[a];
+    f[a] = f[b];
+    f[b] = x;
+  }
+  const int64_t lk1 = K < (int64_t)CL ? (int64_t)L[K] : n, rK = K >= 1 ? (int64_t)R[TL - K] : n;
+  __syncthreads();
+  return lk1 < rK ? lk1 : rK;
+}
+
+__global__ __launch_bounds__(ST) void select_kernel(SelArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t s_dyn[];
+  __shared__ uint32_t s32[2 * SW];
+  __shared__ uint64_t s64[2];
+  __shared__ SplitNode s_nd;
+  __shared__ int32_t s_nn, s_idx;
+  uint64_t *LW = s_dyn;                                       // LMAX words
+  uint16_t *LL = reinterpret_cast<uint16_t *>(s_dyn + LMAX);  // LMAX + LMAX stopper positions
+  uint16_t *LR = LL + LMAX;
+  const int t = threadIdx.x;
+  const uint32_t arr = a.qarr[blockIdx.x];
+  uint64_t *W = a.words + (uint64_t)arr * a.n;
+  uint32_t *L = a.scr + (uint64_t)arr * 2 * a.n, *R = L + a.n;
+  SplitNode *nd = a.nodes + (uint64_t)arr * a.maxnode;
+  if (t == 0) {
+    s_nn = a.nnodes[arr];
+    if (s_nn == 0) {  // the root: the whole array
+      nd[0] = SplitNode{0, (int64_t)a.n, 0, a.depth0, -1, 0, 0};
+      s_nn = 1;
+    }
+  }
+  __syncthreads();
+  for (uint64_t q = a.qoff[blockIdx.x]; q < a.qoff[blockIdx.x + 1]; q++) {
+    const int64_t pos = (int64_t)a.qpos[q];
+    int32_t idx = 0;
+    bool in_lds = false;  // the walk continues on the LDS copy of [lbase, lend)
+    int64_t lbase = 0, lend = 0;
+    uint64_t tm = a.prof ? __builtin_amdgcn_s_memrealtime() : 0;
+    auto mark = [&](int ph) {
+      if (a.prof && t == 0) {
+        const uint64_t u = __builtin_amdgcn_s_memrealtime();
+        atomicAdd(&a.prof[ph], (unsigned long long)(u - tm));
+        tm = u;
+      }
+    };
+    if (t == 0) s_nd = nd[0];
+    __syncthreads();
+    mark(0);
+    for (;;) {
+      const SplitNode x = s_nd;
+      __syncthreads();  // (s_nd is rewritten below)
+      if (x.fin) {
+        if (t == 0) a.qout[q] = in_lds ? LW[pos - lbase] : W[pos];
+        break;
+      }
+      if (x.left >= 0) {  // (never in LDS: the nodes visited there are fresh)
+        idx = pos < x.cut ? x.left : x.left + 1;
+        if (t == 0) s_nd = nd[idx];
+        __syncthreads();
+        mark(0);
+        continue;
+      }
+      const int64_t n = x.hi - x.lo;
+      if (!in_lds && n > 16 && n <= LMAX && x.depth > 0) {
+        for (int64_t i = t; i < n; i += ST) LW[i] = W[x.lo + i];
+        in_lds = true;
+        lbase = x.lo;
+        lend = x.hi;
+        __syncthreads();
+        mark(1);
+      }
+      uint64_t *f = in_lds ? LW + (x.lo - lbase) : W + x.lo;
+      if (n <= 16 || x.depth == 0) {  // a leaf, or the heapsort fallback below the depth limit
+        if (t == 0) {
+          if (n <= 16) insertion_sort_1(f, n);
+          else heap_sort_1(f, n);
+          nd[idx].fin = 1;
+          s_nd.fin = 1;
+        }
+        __syncthreads();
+        mark(2);
+        continue;
+      }
+      const int64_t cut = x.lo + (in_lds ? partition_wg<uint16_t>(f, n, LL, LR, s32, s64)
+                                         : partition_wg<uint32_t>(f, n, L + x.lo, R + x.lo, s32, s64));
+      if (t == 0) {
+        if (s_nn + 2 > a.maxnode) {
+          atomicMax(a.err, 1);
+          nd[idx].fin = 1;  // (ends this query's walk; the call reports the error)
+          s_nd.fin = 1;
+          s_idx = idx;
+        } else {
+          const SplitNode lc{x.lo, cut, 0, x.depth - 1, -1, 0, 0}, rc{cut, x.hi, 0, x.depth - 1, -1, 0, 0};
+          nd[s_nn] = lc;
+          nd[s_nn + 1] = rc;
+          nd[idx].left = s_nn;
+          nd[idx].cut = cut;
+          s_idx = pos < cut ? s_nn : s_nn + 1;
+          s_nd = pos < cut ? lc : rc;
+          s_nn += 2;
+        }
+      }
+      __syncthreads();
+      idx = s_idx;
+      mark(in_lds ? 4 : 3);
+      if (a.prof && t == 0) atomicAdd(&a.prof[in_lds ? 7 : 6], 1ull);
+    }
+    if (in_lds) {  // the partitioned range back to the array
+      __syncthreads();
+      for (int64_t i = t; i < lend - lbase; i += ST) W[lbase + i] = LW[i];
+    }
+    __syncthreads();
+    mark(5);
+  }
+  if (t == 0) a.nnodes[arr] = s_nn;
+}
+
+__global__ void split_words_kernel(const uint16_t *__restrict__ keys, const uint32_t *__restrict__ order, uint64_t n,
+                                   uint32_t npiv, uint64_t *__restrict__ words) {
+  const uint64_t total = n * npiv;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x)
+    words[i] = ((uint64_t)keys[i] << 32) | order[i % n];
+}
+
+}  // namespace
+
+int split_build_words(mc_ctx *c, const uint32_t *d_order, uint64_t n, uint32_t npiv, const uint16_t *d_keys,
+                      uint64_t *d_words) {
+  const uint64_t total = n * npiv;
+  const int blocks = (int)std::min<uint64_t>((total + 255) / 256, 8192);
+  split_words_kernel<<<blocks, 256, 0, c->stream>>>(d_keys, d_order, n, npiv, d_words);
+  MCG_CHECK(hipGetLastError());
+  return MC_OK;
+}
+
+int launch_select(mc_ctx *c, uint64_t *d_words, uint64_t n, uint32_t *d_scr, SplitNode *d_nodes, int32_t *d_nnodes,
+                  int32_t maxnode, int32_t depth0, uint32_t ngroups, const uint32_t *d_qarr, const uint64_t *d_qoff,
+                  const uint64_t *d_qpos, uint64_t *d_qout, int *d_err) {
+  if (!ngroups) return MC_OK;
+  static const bool prof = getenv("MC_SPLIT_PROFILE") != nullptr;
+  static unsigned long long *d_prof = nullptr;
+  if (prof && !d_prof) {
+    MCG_CHECK(hipMalloc(&d_prof, 64));
+    MCG_CHECK(hipMemset(d_prof, 0, 64));
+  }
+  SelArgs a;
+  a.words = d_words;
+  a.n = n;
+  a.scr = d_scr;
+  a.nodes = d_nodes;
+  a.nnodes = d_nnodes;
+  a.maxnode = maxnode;
+  a.depth0 = depth0;
+  a.qarr = d_qarr;
+  a.qoff = d_qoff;
+  a.qpos = d_qpos;
+  a.qout = d_qout;
+  a.err = d_err;
+  a.prof = prof ? d_prof : nullptr;
+  MCG_CHECK(hipFuncSetAttribute(reinterpret_cast<const void *>(&select_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)SEL_LDS));
+  select_kernel<<<ngroups, ST, SEL_LDS, c->stream>>>(a);
+  MCG_CHECK(hipGetLastError());
+  if (prof) {  // cumulative over the process, in us summed over workgroups
+    unsigned long long h[8];
+    MCG_CHECK(hipMemcpyAsync(h, d_prof, 64, hipMemcpyDeviceToHost, c->stream));
+    MCG_CHECK(hipStreamSynchronize(c->stream));
+    fprintf(stderr, "[split] ngroups %u  sum over WGs (us): nodes %.0f lds-load %.0f leaf %.0f part-global %.0f (%llu) "
+            "part-lds %.0f (%llu) writeback %.0f\n", ngroups, h[0] / 100.0, h[1] / 100.0, h[2] / 100.0, h[3] / 100.0,
+            h[6], h[4] / 100.0, h[7], h[5] / 100.0);
+  }
+  return MC_OK;
+}
+
+}  // namespace mcg

@@ -1,7 +1,7 @@
 // trainer.cpp -- see trainer.hpp.  Compiled with -ffp-contract=off.
 #include "trainer.hpp"
 
-#include "lazysort.hpp"
+#include "lazysort.hpp"  // (the two full sorts; the per-pivot sorts are on the device)
 
 #include <algorithm>
 #include <atomic>
@@ -136,14 +136,12 @@ std::vector<PairId> Trainer::split() {
   // std::sort(pts, by distance to pivot i) is evaluated lazily (lazysort.hpp): only the
   // positions the binary search and the sampler read are resolved, with std::sort's exact
   // tie order.
-  std::vector<uint16_t> keys(P * N);
-  std::vector<LazyIntroSort> sorted;
-  sorted.reserve(P);
-  for (size_t i = 0; i < P; i++) sorted.emplace_back(std::vector<uint64_t>{});  // filled below
-  auto pt_at = [&](size_t i, size_t pos) { return (uint32_t)sorted[i].at((int64_t)pos); };
+  // Each pivot's std::sort(points, by distance to pivot i) (Trainer.cpp:691-701) is evaluated
+  // on the device (mc_split_*, split.hip): the (key << 32 | id) arrays stay in HBM and only
+  // the positions the binary search and the sampler read are resolved, with std::sort's exact
+  // tie order.
   // Two levels per round measured fastest at config B (9 rounds of 450 pairs in the latency
-  // form: 8.3 ms of NW, training 21.8 ms vs 25.1 ms with one level; three levels are 1,050-pair
-  // rounds whose extra pairs cost more than the rounds they save); MC_NW_LOOKAHEAD = 1..4.
+  // form instead of 16 of 150); MC_NW_LOOKAHEAD = 1..4.
   const int look = [] {
     const char *e = getenv("MC_NW_LOOKAHEAD");
     const int v = e ? atoi(e) : 2;
@@ -170,49 +168,18 @@ std::vector<PairId> Trainer::split() {
     }
   };
   {
-    // Pipelined over chunks of pivots: a host thread drives the GPU (keys of chunk c + 1 and
-    // their copy home) while the OpenMP team builds chunk c's (key << 32 | id) words and lazy
-    // sorts and resolves the positions of the first round's decision tree (every chain starts
-    // at the same state, so the same positions).
     Scope s(timer_, "train.sort_keys");
     Scope s3(timer_, "train.sort_keys.pivots");
-    std::vector<size_t> pos0;
-    std::vector<char> live0;
-    tree(2 * (N / 4), N / 4, look, pos0, live0);
-    const size_t Q = std::max<size_t>(1, (P + 3) / 4);  // pivots per chunk
-    const size_t nchunk = (P + Q - 1) / Q;
-    std::atomic<size_t> ready{0};
-    std::exception_ptr key_err;
-    std::thread gpu([&]() {
-      try {
-        for (size_t c = 0; c < nchunk; c++) {
-          const size_t c0 = c * Q, n = std::min(Q, P - c0);
-          check(mc_distance_keys(ctx_, indices.data() + c0, (uint32_t)n, all_ids.data(), N, keys.data() + c0 * N),
-                "mc_distance_keys");
-          ready.store(c + 1, std::memory_order_release);
-        }
-      } catch (...) {
-        key_err = std::current_exception();
-        ready.store(nchunk + 1, std::memory_order_release);  // (wakes the consumer)
-      }
-    });
-    for (size_t c = 0; c < nchunk; c++) {
-      while (ready.load(std::memory_order_acquire) <= c) std::this_thread::yield();
-      if (ready.load(std::memory_order_acquire) > nchunk) break;  // the GPU thread failed
-      const size_t c0 = c * Q, c1 = std::min(P, c0 + Q);
-#pragma omp parallel for schedule(dynamic) num_threads(cfg_.threads)
-      for (size_t i = c0; i < c1; i++) {
-        const uint16_t *kk = &keys[i * N];
-        std::vector<uint64_t> w(N);
-        for (size_t t = 0; t < N; t++) w[t] = ((uint64_t)kk[points[t]] << 32) | points[t];
-        sorted[i] = LazyIntroSort(std::move(w));
-        for (size_t n = 0; n < pos0.size(); n++)
-          if (live0[n] && pos0[n] < N) pt_at(i, pos0[n]);
-      }
-    }
-    gpu.join();
-    if (key_err) std::rethrow_exception(key_err);
+    check(mc_split_begin(ctx_, indices.data(), (uint32_t)P, points.data(), N), "mc_split_begin");
   }
+  // ids at sorted positions of the pivots' arrays
+  std::vector<uint32_t> q_arr, q_ids;
+  std::vector<uint64_t> q_pos;
+  auto select = [&]() {
+    q_ids.resize(q_arr.size());
+    if (!q_arr.empty())
+      check(mc_split_select(ctx_, q_arr.size(), q_arr.data(), q_pos.data(), q_ids.data()), "mc_split_select");
+  };
   // binary search with alignment (:703-721): the 150 dependent chains advance together.  Each
   // round aligns, for every active chain, the next `look` levels of its decision tree at once
   // (the current pivot, both positions the next comparison can move to, ...: 2^look - 1 pairs
@@ -222,8 +189,8 @@ std::vector<PairId> Trainer::split() {
   std::vector<size_t> offset(P, N / 4), pivot(P, 2 * (N / 4));
   std::vector<char> active(P, 1);
   // Sampler positions of the current pivot estimate (the loops of :732-755 below).
-  auto sample_positions = [&](size_t i, size_t pv, std::vector<size_t> &out) {
-    const size_t npts = sorted[i].size();
+  auto sample_positions = [&](size_t pv, std::vector<size_t> &out) {
+    const size_t npts = N;
     double before_inc = (double)pv / to_add_each, after_inc = ((double)(npts - pv)) / to_add_each;
     double bs = 0, as = (double)pv;
     for (int t = 0; t < (int)to_add_each; t++, bs += before_inc) out.push_back((size_t)(int)std::round(bs));
@@ -236,101 +203,37 @@ std::vector<PairId> Trainer::split() {
     std::vector<size_t> who, first;  // chain of each batch entry's tree; first entry of each chain
     std::vector<std::vector<size_t>> tpos(P);
     std::vector<std::vector<char>> tlive(P);
-    auto gather = [&]() {
+    for (;;) {
       who.clear();
       for (size_t i = 0; i < P; i++) {
         if (active[i] && offset[i] == 0) active[i] = 0;
         if (active[i]) who.push_back(i);
       }
-    };
-    auto build_batch = [&](bool parallel) {
-      first.assign(who.size() + 1, 0);
-      for (size_t t = 0; t < who.size(); t++) {
-        tree(pivot[who[t]], offset[who[t]], look, tpos[who[t]], tlive[who[t]]);
-        size_t m = 0;
-        for (char l : tlive[who[t]]) m += l != 0;
-        first[t + 1] = first[t] + m;
-      }
-      batch.resize(first[who.size()]);
-      auto fill = [&](size_t t) {
-        const size_t i = who[t];
-        size_t q = first[t];
-        for (size_t n = 0; n < tpos[i].size(); n++)
-          if (tlive[i][n]) batch[q++] = PairId(indices[i], pt_at(i, tpos[i][n]));
-      };
-      if (parallel) {
-#pragma omp parallel for schedule(dynamic) num_threads(cfg_.threads)
-        for (size_t t = 0; t < who.size(); t++) fill(t);
-      } else {
-        for (size_t t = 0; t < who.size(); t++) fill(t);
-      }
-    };
-    gather();
-    {
-      Scope s2(timer_, "train.nw_search.resolve");
-      build_batch(true);
-    }
-    while (!batch.empty()) {
-      // The GPU aligns this round's trees while the host resolves, in every chain, the positions
-      // of every tree the next round can start from (or, for a chain that ends within this
-      // round, the sampler's positions around each pivot it can end on): the lazy sorts'
-      // partitions are then ready when the identities come back.  Each LazyIntroSort is touched
-      // by one host thread only.
-      std::vector<double> al;
-      // An error of the GPU thread (mc::Error from check()) must not escape the std::thread
-      // (std::terminate would end the host process): it is carried out and rethrown here.
-      std::exception_ptr gpu_err;
-      std::thread gpu([&]() {
-        try {
-          nw_batch(batch, al);
-        } catch (...) {
-          gpu_err = std::current_exception();
-        }
-      });
-      std::exception_ptr spec_err;
-      try {
-        Scope s2(timer_, "train.nw_search.speculate");  // one core left to the thread driving the GPU
-#pragma omp parallel for schedule(dynamic) num_threads(std::max(1, cfg_.threads - 1))
+      {
+        Scope s2(timer_, "train.nw_search.resolve");
+        first.assign(who.size() + 1, 0);
+        q_arr.clear();
+        q_pos.clear();
         for (size_t t = 0; t < who.size(); t++) {
           const size_t i = who[t];
-          // the states the walk can end in: below the live nodes of the last level (or where
-          // a node's offset reaches 0), each the root of the next round's tree
-          std::vector<size_t> pos, tp;
-          std::vector<char> tl;
-          const std::vector<size_t> &np = tpos[i];
-          const std::vector<char> &nl = tlive[i];
-          const size_t nn = np.size(), inner = nn / 2;  // nodes of the last level: inner .. nn-1
-          for (size_t n = 0; n < nn; n++) {
-            if (!nl[n]) continue;
-            const bool last_level = n >= inner || !nl[2 * n + 1];
-            if (!last_level) continue;
-            // offset of node n: o >> depth(n)
-            size_t depth = 0;
-            for (size_t x = n; x > 0; x = (x - 1) / 2) depth++;
-            const size_t on = offset[i] >> depth, oc = on / 2;
-            for (int side = 0; side < 2; side++) {
-              const size_t pc = side ? np[n] + on : np[n] - on;
-              if (oc > 0) {
-                tree(pc, oc, look, tp, tl);
-                for (size_t m = 0; m < tp.size(); m++)
-                  if (tl[m]) pos.push_back(tp[m]);
-              } else {
-                sample_positions(i, pc, pos);
-              }
+          tree(pivot[i], offset[i], look, tpos[i], tlive[i]);
+          for (size_t n = 0; n < tpos[i].size(); n++)
+            if (tlive[i][n]) {
+              q_arr.push_back((uint32_t)i);
+              q_pos.push_back(tpos[i][n]);
             }
-          }
-          for (size_t q : pos)
-            if (q < sorted[i].size()) pt_at(i, q);
+          first[t + 1] = q_arr.size();
         }
-      } catch (...) {
-        spec_err = std::current_exception();
+        select();
+        batch.resize(q_arr.size());
+        for (size_t q = 0; q < q_arr.size(); q++) batch[q] = PairId(indices[q_arr[q]], q_ids[q]);
       }
+      if (batch.empty()) break;
+      std::vector<double> al;
       {
         Scope s3(timer_, "train.nw_search.align");
-        gpu.join();
+        nw_batch(batch, al);
       }
-      if (gpu_err) std::rethrow_exception(gpu_err);
-      if (spec_err) std::rethrow_exception(spec_err);
       for (size_t t = 0; t < who.size(); t++) {
         const size_t i = who[t];
         // the aligned nodes of this chain's tree, in batch order
@@ -351,42 +254,36 @@ std::vector<PairId> Trainer::split() {
             break;
           }
           offset[i] /= 2;
-          if (offset[i] == 0) break;  // (gather drops the chain)
+          if (offset[i] == 0) break;  // (the next round's gather drops the chain)
         }
       }
-      gather();
-      // The new trees were resolved by the speculation above: plain lookups.
-      Scope s2(timer_, "train.nw_search.resolve");
-      build_batch(false);
     }
   }
   int aerr = 0;
   std::vector<std::vector<PairId>> bufs(P);
-  Scope sb(timer_, "train.sample");
-#pragma omp parallel for schedule(dynamic) num_threads(cfg_.threads)
-  for (size_t i = 0; i < P; i++) {
-    const size_t npts = sorted[i].size();
-    const uint32_t p = indices[i];
-    double before_inc = (double)pivot[i] / to_add_each;
-    double after_inc = ((double)(npts - pivot[i])) / to_add_each;
-    double before_start = 0, after_start = (double)pivot[i];
-    std::vector<PairId> &buf = bufs[i];
-    for (int t = 0; t < (int)to_add_each; t++) {
-      int idx = (int)std::round(before_start);
-      uint32_t q = pt_at(i, (size_t)idx);
-      buf.push_back(hdr_less(p, q) ? PairId(p, q) : PairId(q, p));
-      before_start += before_inc;
+  {
+    Scope sb(timer_, "train.sample");
+    q_arr.clear();
+    q_pos.clear();
+    std::vector<size_t> sp;
+    for (size_t i = 0; i < P; i++) {
+      sp.clear();
+      sample_positions(pivot[i], sp);
+      for (size_t x : sp) {
+        q_arr.push_back((uint32_t)i);
+        q_pos.push_back(x);
+      }
     }
-    for (int t = 0; t < (int)to_add_each && std::round(after_start) < (double)npts; t++) {
-      int idx = (int)std::round(after_start);
-      uint32_t q = pt_at(i, (size_t)idx);
-      buf.push_back(hdr_less(p, q) ? PairId(p, q) : PairId(q, p));
-      after_start += after_inc;
+    select();
+    for (size_t q = 0; q < q_arr.size(); q++) {
+      const uint32_t p = indices[q_arr[q]], x = q_ids[q];
+      bufs[q_arr[q]].push_back(hdr_less(p, x) ? PairId(p, x) : PairId(x, p));
     }
+    check(mc_split_end(ctx_), "mc_split_end");
   }
   for (size_t i = 0; i < P; i++) {  // the warning flag keeps the serial loop's last writer
     double before_inc = (double)pivot[i] / to_add_each;
-    double after_inc = ((double)(sorted[i].size() - pivot[i])) / to_add_each;
+    double after_inc = ((double)(N - pivot[i])) / to_add_each;
     if (before_inc < 1) aerr = 1;
     else if (after_inc < 1) aerr = -1;
     pairs.insert(bufs[i].begin(), bufs[i].end());

@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "mc_oracle.h"
+#include "../meshclust_amd/csrc/host/lazysort.hpp"
 
 struct mc_ctx {
   std::vector<uint8_t> codes;
@@ -29,6 +30,7 @@ struct mc_ctx {
   std::vector<uint32_t> order;
   std::vector<uint8_t> alive;
   std::vector<uint32_t> members;  // current cluster, in `current` order
+  std::vector<mc::LazyIntroSort> split;  // mc_split_*: the host's lazy introsort
 };
 
 static thread_local std::string g_err;
@@ -135,6 +137,52 @@ int mc_distance_keys(mc_ctx *c, const uint32_t *piv, uint32_t np, const uint32_t
     for (uint64_t i = 0; i < m; i++)
       keys[p * m + i] = (uint16_t)mco_distance(row(c, ids[i]), row(c, piv[p]), c->width, c->B, c->mags[ids[i]],
                                                c->mags[piv[p]]);
+  return MC_OK;
+}
+
+int mc_split_begin(mc_ctx *c, const uint32_t *piv, uint32_t np, const uint32_t *order, uint64_t n) {
+  std::vector<uint16_t> keys((size_t)np * n);
+  int rc = mc_distance_keys(c, piv, np, order, n, keys.data());
+  if (rc) return rc;
+  c->split.clear();
+  c->split.reserve(np);
+  for (uint32_t p = 0; p < np; p++) {
+    std::vector<uint64_t> w(n);
+    for (uint64_t t = 0; t < n; t++) w[t] = ((uint64_t)keys[(size_t)p * n + t] << 32) | order[t];
+    c->split.emplace_back(std::move(w));
+  }
+  return MC_OK;
+}
+
+int mc_split_begin_words(mc_ctx *c, const uint64_t *words, uint32_t narr, uint64_t n, int depth) {
+  c->split.clear();
+  for (uint32_t a = 0; a < narr; a++)
+    c->split.emplace_back(std::vector<uint64_t>(words + (size_t)a * n, words + (size_t)(a + 1) * n), depth);
+  return MC_OK;
+}
+
+int mc_split_select_words(mc_ctx *c, uint64_t nq, const uint32_t *arr, const uint64_t *pos, uint64_t *out) {
+  for (uint64_t i = 0; i < nq; i++)
+    if (arr[i] >= c->split.size() || pos[i] >= c->split[arr[i]].size()) return fail(MC_ERR_ARG, "split query out of range");
+  // one thread per array (a LazyIntroSort is not shared between threads)
+  std::vector<std::vector<uint64_t>> by(c->split.size());
+  for (uint64_t i = 0; i < nq; i++) by[arr[i]].push_back(i);
+#pragma omp parallel for schedule(dynamic)
+  for (size_t a = 0; a < by.size(); a++)
+    for (uint64_t i : by[a]) out[i] = c->split[a].at((int64_t)pos[i]);
+  return MC_OK;
+}
+
+int mc_split_select(mc_ctx *c, uint64_t nq, const uint32_t *arr, const uint64_t *pos, uint32_t *ids) {
+  std::vector<uint64_t> w(nq);
+  int rc = mc_split_select_words(c, nq, arr, pos, w.data());
+  if (rc) return rc;
+  for (uint64_t i = 0; i < nq; i++) ids[i] = (uint32_t)w[i];
+  return MC_OK;
+}
+
+int mc_split_end(mc_ctx *c) {
+  c->split.clear();
   return MC_OK;
 }
 
