@@ -151,7 +151,7 @@ int mc_distance_keys(mc_ctx *ctx, const uint32_t *pivots, uint32_t npiv, const u
  *     are partitioned, and the partitions persist for later calls.
  *   mc_split_begin_words / mc_split_select_words: the same on arbitrary word arrays compared
  *     by their upper 32 bits (depth < 0: std::sort's 2 floor(log2 n) limit), returning words.
- *   mc_split_end: frees the arrays.
+ *   mc_split_end: ends the queries (the device buffers stay with the context for reuse).
  */
 int mc_split_begin(mc_ctx *ctx, const uint32_t *pivots, uint32_t npiv, const uint32_t *order, uint64_t n);
 int mc_split_begin_words(mc_ctx *ctx, const uint64_t *words, uint32_t narr, uint64_t n, int depth);

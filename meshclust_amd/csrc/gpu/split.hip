@@ -161,21 +161,55 @@ __device__ int64_t partition_wg(uint64_t *f, int64_t n, PT *L, PT *R, uint32_t *
   }
   __syncthreads();
   const uint64_t pk = f[0] >> 32;
-  // segments of S consecutive positions per thread
-  const int64_t S = (n + ST - 1) / ST;
-  const int64_t i0 = (int64_t)t * S < n ? (int64_t)t * S : n, i1 = i0 + S < n ? i0 + S : n;
-  uint32_t cg = 0, cl = 0;
-  for (int64_t i = i0; i < i1; i++) {
-    const uint64_t k = f[i] >> 32;
-    cg += (i >= 1 && k >= pk) ? 1u : 0u;
-    cl += k <= pk ? 1u : 0u;
-  }
-  uint32_t og, ol, CL, TL;
-  block_scan2(cg, cl, &og, &ol, &CL, &TL, s32);
-  for (int64_t i = i0; i < i1; i++) {
-    const uint64_t k = f[i] >> 32;
-    if (i >= 1 && k >= pk) L[og++] = (PT)i;
-    if (k <= pk) R[ol++] = (PT)i;
+  uint32_t CL, TL;
+  if constexpr (sizeof(PT) == 2) {
+    // LDS copy: segments of S consecutive positions per thread, counted, scanned, written
+    const int64_t S = (n + ST - 1) / ST;
+    const int64_t i0 = (int64_t)t * S < n ? (int64_t)t * S : n, i1 = i0 + S < n ? i0 + S : n;
+    uint32_t cg = 0, cl = 0;
+    for (int64_t i = i0; i < i1; i++) {
+      const uint64_t k = f[i] >> 32;
+      cg += (i >= 1 && k >= pk) ? 1u : 0u;
+      cl += k <= pk ? 1u : 0u;
+    }
+    uint32_t og, ol;
+    block_scan2(cg, cl, &og, &ol, &CL, &TL, s32);
+    for (int64_t i = i0; i < i1; i++) {
+      const uint64_t k = f[i] >> 32;
+      if (i >= 1 && k >= pk) L[og++] = (PT)i;
+      if (k <= pk) R[ol++] = (PT)i;
+    }
+  } else {
+    // global range: chunks of CPT words per thread, every load of a chunk in flight at once,
+    // stopper positions written chunk after chunk (so in order)
+    constexpr int CPT = 8;
+    uint32_t bg = 0, bl = 0;  // stoppers before this chunk
+    for (int64_t c0 = 0; c0 < n; c0 += (int64_t)ST * CPT) {
+      const int64_t i0 = c0 + (int64_t)t * CPT;
+      uint32_t kk[CPT];
+#pragma unroll
+      for (int e = 0; e < CPT; e++) kk[e] = i0 + e < n ? (uint32_t)(f[i0 + e] >> 32) : 0u;
+      uint32_t mg = 0, ml = 0;
+#pragma unroll
+      for (int e = 0; e < CPT; e++)
+        if (i0 + e < n) {
+          mg |= (i0 + e >= 1 && kk[e] >= pk) ? 1u << e : 0u;
+          ml |= kk[e] <= pk ? 1u << e : 0u;
+        }
+      uint32_t og, ol, tg, tl;
+      block_scan2((uint32_t)__popc(mg), (uint32_t)__popc(ml), &og, &ol, &tg, &tl, s32);
+      og += bg;
+      ol += bl;
+#pragma unroll
+      for (int e = 0; e < CPT; e++) {
+        if (mg >> e & 1) L[og++] = (PT)(i0 + e);
+        if (ml >> e & 1) R[ol++] = (PT)(i0 + e);
+      }
+      bg += tg;
+      bl += tl;
+    }
+    CL = bg;
+    TL = bl;
   }
   __syncthreads();
   // K = the last k with l_k < r_k (l_k = L[k - 1], r_k = R[TL - k]); monotone in k: bisection
@@ -202,11 +236,28 @@ __device__ int64_t partition_wg(uint64_t *f, int64_t n, PT *L, PT *R, uint32_t *
     hi = nhi;
   }
   const int64_t K = lo;
-  for (int64_t k = 1 + t; k <= K; k += ST) {
-    const uint32_t a = (uint32_t)L[k - 1], b = (uint32_t)R[TL - k];
-    const uint64_t x = f[a];
-    f[a] = f[b];
-    f[b] = x;
+  // the K independent swaps, four per thread in flight
+  for (int64_t k0 = 1 + t; k0 <= K; k0 += 4 * ST) {
+    uint32_t a[4], b[4];
+    uint64_t x[4], y[4];
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+      const int64_t k = k0 + (int64_t)e * ST;
+      a[e] = k <= K ? (uint32_t)L[k - 1] : 0u;
+      b[e] = k <= K ? (uint32_t)R[TL - k] : 0u;
+    }
+#pragma unroll
+    for (int e = 0; e < 4; e++)
+      if (k0 + (int64_t)e * ST <= K) {
+        x[e] = f[a[e]];
+        y[e] = f[b[e]];
+      }
+#pragma unroll
+    for (int e = 0; e < 4; e++)
+      if (k0 + (int64_t)e * ST <= K) {
+        f[a[e]] = y[e];
+        f[b[e]] = x[e];
+      }
   }
   const int64_t lk1 = K < (int64_t)CL ? (int64_t)L[K] : n, rK = K >= 1 ? (int64_t)R[TL - K] : n;
   __syncthreads();
@@ -366,9 +417,10 @@ int launch_select(mc_ctx *c, uint64_t *d_words, uint64_t n, uint32_t *d_scr, Spl
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)SEL_LDS));
   select_kernel<<<ngroups, ST, SEL_LDS, c->stream>>>(a);
   MCG_CHECK(hipGetLastError());
-  if (prof) {  // cumulative over the process, in us summed over workgroups
+  if (prof) {  // this call, in us summed over workgroups
     unsigned long long h[8];
     MCG_CHECK(hipMemcpyAsync(h, d_prof, 64, hipMemcpyDeviceToHost, c->stream));
+    MCG_CHECK(hipMemsetAsync(d_prof, 0, 64, c->stream));
     MCG_CHECK(hipStreamSynchronize(c->stream));
     fprintf(stderr, "[split] ngroups %u  sum over WGs (us): nodes %.0f lds-load %.0f leaf %.0f part-global %.0f (%llu) "
             "part-lds %.0f (%llu) writeback %.0f\n", ngroups, h[0] / 100.0, h[1] / 100.0, h[2] / 100.0, h[3] / 100.0,

@@ -8,6 +8,7 @@
 // links only libmcgpu; this file is never part of the product.
 #include <cfloat>
 #include <cstdint>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -149,6 +150,13 @@ int mc_split_begin(mc_ctx *c, const uint32_t *piv, uint32_t np, const uint32_t *
   for (uint32_t p = 0; p < np; p++) {
     std::vector<uint64_t> w(n);
     for (uint64_t t = 0; t < n; t++) w[t] = ((uint64_t)keys[(size_t)p * n + t] << 32) | order[t];
+    if (p == 0 && getenv("MC_DUMP_SPLIT")) {  // (diagnostics: the first pivot's array)
+      FILE *fd = fopen(getenv("MC_DUMP_SPLIT"), "wb");
+      if (fd) {
+        fwrite(w.data(), 8, n, fd);
+        fclose(fd);
+      }
+    }
     c->split.emplace_back(std::move(w));
   }
   return MC_OK;
