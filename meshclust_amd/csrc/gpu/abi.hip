@@ -1085,7 +1085,7 @@ int mc_accumulate(mc_ctx *c, const uint32_t *bin_lo, const uint64_t *bounds, uin
       // columns: seen, scores (wave 0), part B (wave 0), after the B barrier, after the reduce
       // barrier, partial stored
       const int col[6] = {0, 1, 3, 4, 5, 2};
-      double acc[6][3] = {{0}}, all = 0, nw = 0;
+      double acc[6][3] = {{0}}, all = 0, nw = 0, apub = 0;
       uint64_t ns = 0;
       for (int st = 2; st < S2; st++) {
         const uint64_t t0 = tr[(size_t)st * TW], ta = tr[(size_t)st * TW + 7];
@@ -1104,6 +1104,7 @@ int mc_accumulate(mc_ctx *c, const uint32_t *bin_lo, const uint64_t *bounds, uin
           acc[i][2] += v[i].back();
         }
         all += (double)(int64_t)(ta - t0) / 100;
+        apub += tr[(size_t)st * TW + 6] ? (double)(int64_t)(tr[(size_t)st * TW + 6] - t0) / 100 : 0.0;
         nw += (double)v[5].size();
         ns++;
       }
@@ -1112,7 +1113,7 @@ int mc_accumulate(mc_ctx *c, const uint32_t *bin_lo, const uint64_t *bounds, uin
         fprintf(stderr, "[accum trace4] %llu steps, %.1f workers, us after the exact window's publish (min/med/max):",
                 (unsigned long long)ns, nw / ns);
         for (int i = 0; i < 6; i++) fprintf(stderr, " %s %.2f/%.2f/%.2f", nm[i], acc[i][0] / ns, acc[i][1] / ns, acc[i][2] / ns);
-        fprintf(stderr, "; controller all-seen %.2f\n", all / ns);
+        fprintf(stderr, "; controller all-seen %.2f; record (centre) published %.2f\n", all / ns, apub / ns);
       }
     }
     if (atoi(getenv("MC_ACCUM_PROFILE")) >= 2 && c->s_h.p) {

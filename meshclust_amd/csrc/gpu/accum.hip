@@ -932,6 +932,7 @@ __device__ __forceinline__ void worker_dense(const AccArgs &A, const DevClassifi
   __shared__ int s_abort;
   __shared__ uint64_t s_b[2];  // spec: part B of the step, {tag << 32 | S}, {tag << 32 | E}
   __shared__ uint64_t s_tw[NW];  // MC_ACCUM_PROFILE=4: each wave's scores-done time
+  __shared__ uint32_t s_arr;     // waves that have reduced this step's scores
   constexpr int NC = NCH > 0 ? NCH : DMAXCH;
   const uint32_t GW = gridDim.x - 1, w = blockIdx.x - 1;
   const Div32 dgw(GW);
@@ -966,6 +967,7 @@ __device__ __forceinline__ void worker_dense(const AccArgs &A, const DevClassifi
   if (t == 0) {
     s_abort = 0;
     s_b[0] = s_b[1] = 0;
+    s_arr = 0;
   }
   __syncthreads();
   uint32_t kcur = 0, seen = 0;
@@ -1150,91 +1152,106 @@ __device__ __forceinline__ void worker_dense(const AccArgs &A, const DevClassifi
       double best_v = -1.0;
       uint64_t best_p = NONE64;
       uint32_t nscan = 0;
+      bool listed = false;  // a flagged position went to this worker's list in global memory
       if (comp && pos_t >= W_S && pos_t <= W_E) {
         nscan = 1;
         if (d_t) {
           al_t = false;
           const uint32_t idx = atomicAdd(&s_nfl, 1u);
           if (idx < (uint32_t)INL) s_inl[idx] = pos_t;
-          else st32(A.fpos + (uint64_t)w * A.fcap + idx, pos_t);
+          else {
+            st32(A.fpos + (uint64_t)w * A.fcap + idx, pos_t);
+            listed = true;
+          }
         }
         if (cv_t > -1.0) {
           best_v = cv_t;
           best_p = pos_t;
         }
       }
-      wave_best_all(best_v, best_p, better);
-      nscan = wave_sum32(nscan);
+      const uint64_t scanned = __ballot(nscan != 0);
+      if (__ballot(best_p != NONE64)) wave_best_all(best_v, best_p, better);  // (waves with no candidate skip it)
       if (lane == 0) {
         s_bv[wv] = best_v;
         s_bp[wv] = best_p;
-        s_wc[wv] = nscan;
+        s_wc[wv] = (uint32_t)__popcll(scanned);
       }
-      drain();  // this wave's flagged-list stores are complete before the partial announces them
-    }
-    __syncthreads();  // the one barrier between the scores and the partial
-    if (A.trace2 && t == 0) t_red = now();
-    if (s_abort) {
-      if (t == 0) atomicMax((unsigned long long *)&A.out[3], 99ull);
-      return;
-    }
-    if (active && t < PART_G) {
-      double vv[NW];
-      uint64_t pp[NW];
-      uint32_t ns = 0;
+      // this wave's flagged-list stores are complete before the partial announces them
+      if (__ballot(listed)) drain();
+      // arrival: the wave that completes the workgroup's scores combines the eight waves'
+      // results and publishes the partial (no workgroup barrier on the path)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      uint32_t arr = 0;
+      if (lane == 0) arr = atomicAdd(&s_arr, 1u);
+      arr = (uint32_t)__builtin_amdgcn_readfirstlane((int)arr);
+      if (arr == (uint32_t)NW - 1) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        if (A.trace2 && lane == 0) t_red = now();
+        if (lane < PART_G) {
+          double vv[NW];
+          uint64_t pp[NW];
+          uint32_t ns = 0;
 #pragma unroll
-      for (int i = 0; i < NW; i++) {
-        vv[i] = s_bv[i];
-        pp[i] = s_bp[i];
-        ns += s_wc[i];
-      }
-      double v = vv[0];
-      uint64_t p = pp[0];
+          for (int i = 0; i < NW; i++) {
+            vv[i] = s_bv[i];
+            pp[i] = s_bp[i];
+            ns += s_wc[i];
+          }
+          double v = vv[0];
+          uint64_t p = pp[0];
 #pragma unroll
-      for (int i = 1; i < NW; i++)
-        if (better(vv[i], pp[i], v, p)) {
-          v = vv[i];
-          p = pp[i];
+          for (int i = 1; i < NW; i++)
+            if (better(vv[i], pp[i], v, p)) {
+              v = vv[i];
+              p = pp[i];
+            }
+          const uint64_t vb = (uint64_t)__double_as_longlong(v);
+          const int j = lane;
+          const uint32_t nfl = s_nfl;
+          const uint32_t data = j == 0   ? (uint32_t)(vb >> 32)
+                                : j == 1 ? (uint32_t)vb
+                                : j == 2 ? (p == NONE64 ? NONE : (uint32_t)p)
+                                : j == 3 ? nfl
+                                : j == 4 ? ns
+                                         : ((uint32_t)(j - 5) < nfl ? s_inl[j - 5] : NONE);
+          st64(A.partials + (uint64_t)w * PART_G + j, gran(seen, data));
+          if (j == 0) s_arr = 0;  // (the next step's arrivals come after the next record)
+          if (A.trace && !A.trace_all && j == 0 && mine == nact / 2 && seen < TRACE_STEPS) {
+            uint64_t *tr = A.trace + (uint64_t)seen * TRACE_W;
+            tr[10] = t_seen;
+            tr[11] = t_klog;
+            tr[12] = t_scanned;
+            tr[13] = t_scanned;
+            tr[14] = now();
+          }
+          if (A.trace && A.trace_all && j == 0) {
+            const uint64_t tn = now();
+            trace_mark(A, seen, 1, t_seen);
+            trace_mark(A, seen, 3, t_scanned);
+            trace_mark(A, seen, 5, tn);
+          }
+          if (A.trace2 && j == 0 && seen < TRACE2_STEPS) {
+            uint64_t *tr = A.trace2 + ((uint64_t)seen * GMAX + w) * T2W;
+            tr[0] = t_seen;
+            tr[1] = t_scanned;
+            tr[2] = now();
+            uint64_t tw = 0;
+            for (int i = 0; i < NW; i++) tw = s_tw[i] > tw ? s_tw[i] : tw;
+            tr[3] = t_bgot;
+            tr[4] = tw;
+            tr[5] = t_red;
+          }
         }
-      const uint64_t vb = (uint64_t)__double_as_longlong(v);
-      const int j = (int)t;
-      const uint32_t nfl = s_nfl;
-      const uint32_t data = j == 0   ? (uint32_t)(vb >> 32)
-                            : j == 1 ? (uint32_t)vb
-                            : j == 2 ? (p == NONE64 ? NONE : (uint32_t)p)
-                            : j == 3 ? nfl
-                            : j == 4 ? ns
-                                     : ((uint32_t)(j - 5) < nfl ? s_inl[j - 5] : NONE);
-      st64(A.partials + (uint64_t)w * PART_G + j, gran(seen, data));
-      if (A.trace && !A.trace_all && j == 0 && mine == nact / 2 && seen < TRACE_STEPS) {
-        uint64_t *tr = A.trace + (uint64_t)seen * TRACE_W;
-        tr[10] = t_seen;
-        tr[11] = t_klog;
-        tr[12] = t_scanned;
-        tr[13] = t_scanned;
-        tr[14] = now();
-      }
-      if (A.trace && A.trace_all && j == 0) {
-        const uint64_t tn = now();
-        trace_mark(A, seen, 1, t_seen);
-        trace_mark(A, seen, 3, t_scanned);
-        trace_mark(A, seen, 5, tn);
-      }
-      if (A.trace2 && j == 0 && seen < TRACE2_STEPS) {
-        uint64_t *tr = A.trace2 + ((uint64_t)seen * GMAX + w) * T2W;
-        tr[0] = t_seen;
-        tr[1] = t_scanned;
-        tr[2] = now();
-        uint64_t tw = 0;
-        for (int i = 0; i < NW; i++) tw = s_tw[i] > tw ? s_tw[i] : tw;
-        tr[3] = t_bgot;
-        tr[4] = tw;
-        tr[5] = t_red;
       }
     }
     // ---- compaction (off the critical path: the controller is collecting) ----------------
     died = t < n_ent && !al_t;
-    if (__syncthreads_or(died)) {
+    const int any_died = __syncthreads_or(died);
+    if (s_abort) {
+      if (t == 0) atomicMax((unsigned long long *)&A.out[3], 99ull);
+      return;
+    }
+    if (any_died) {
       const bool keep = t < n_ent && al_t;
       const uint64_t bal = __ballot(keep);
       if (lane == 0) s_wc[wv] = (uint32_t)__popcll(bal);
@@ -1301,6 +1318,7 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
   __shared__ uint64_t s_bp[NW];
   __shared__ uint32_t s_new;  // members taken into the cluster this step
   __shared__ uint32_t s_plist[PLIST];  // ... their positions
+  __shared__ uint32_t s_pbin[PLIST];   // ... their bvec bins (kills deferred to the next window)
   __shared__ uint64_t s_q[4];
   __shared__ uint32_t s_klast[KINL];
   __shared__ int s_abort;
@@ -1342,6 +1360,9 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
   }
   uint64_t lg = 1;
   while (lg * 2 <= A.nb) lg *= 2;
+  // the workers' partials as a buffer resource (16-byte sc1 polls, aux 16 = sc1)
+  const __amdgpu_buffer_rsrc_t prs =
+      __builtin_amdgcn_make_buffer_rsrc(A.partials, 0, (int)(GW * PART_G * 8), 0x00020000);
   DevBvec bv{A.gbits ? A.gbits : lbits, A.gbits != nullptr, cnt, fw, lo, bnd, A.len_s, A.nb, lg};
   uint32_t last = NONE;   // current centre (static position)
   uint32_t last_q = 0;    // its member index in the current cluster
@@ -1351,6 +1372,7 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
   uint32_t step = 0;
   uint64_t err = 0;
   uint32_t kn = 0;      // kill-log length
+  uint32_t npend = 0;   // new members s_plist[0, npend) whose bvec kills are still to be done
   uint64_t t_wait = 0, t_coll = 0, t_mark = 0;
   const uint64_t clk0 = A.prof ? __builtin_amdgcn_s_memtime() : 0, rt0 = A.prof ? now() : 0;
   uint64_t t_sub[4] = {0, 0, 0, 0};  // collect: reduce (stragglers), column sums, mean, closest
@@ -1445,7 +1467,8 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
   // data from the read-only static arrays) or column sums past the cache, and the bvec kill
   // (wide rows: the row stays in `hr`; its column sums are added here only for a member past
   // the step's list, `sums`, the others by the column-sum pass over the list)
-  auto take = [&](uint64_t qm, uint32_t p, bool sums) {
+  // (defer >= 0: the bvec kill is left to the next window -- the bin goes to s_pbin[defer])
+  auto take = [&](uint64_t qm, uint32_t p, bool sums, int64_t defer = -1) {
     const uint64_t key = ((uint64_t)step << 32) | p;
     st32(A.mem_pos + cl_start + qm, p);
     st64(A.mkeys + cl_start + qm, key);
@@ -1471,7 +1494,8 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
           if (pv[e]) atomicAdd((unsigned long long *)&msum[k * per + e], (unsigned long long)pv[e]);
       }
     }
-    bv.kill_in(p, mi.bin);
+    if (defer >= 0) s_pbin[defer] = (uint32_t)mi.bin;
+    else bv.kill_in(p, mi.bin);
   };
 
   // bvec after insert_finalize: every static position alive
@@ -1514,14 +1538,23 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
         t_ws[0] += t - t_mark;
         t_mark = t;
       }
-      const bool fast = wt.fb < A.nb && wt.bb < A.nb && cnt[wt.fb] > 0 && cnt[wt.bb] > 0;
       if (A.spec) {
         // publish the centre now, with a superset of its window: the fast form's window lies in
         // the two edge bins' span [lo[fb], lo[bb + 1]) (bv_fast_window), the general one anywhere.
-        // The workers score that span while the exact window is computed (part B, below).
+        // The workers score that span while the exact window is computed (part B, below).  (The
+        // step's new members are not killed in the bvec yet: an edge bin with more alive
+        // entries than that is nonempty after the kills.)
+        const bool fast_after = wt.fb < A.nb && wt.bb < A.nb && cnt[wt.fb] > npend && cnt[wt.bb] > npend;
         step++;
-        if (wv == 0) publish(fast ? lo[wt.fb] : 0, fast ? lo[wt.bb + 1] - 1 : A.N - 1, true);
+        if (wv == 0) publish(fast_after ? lo[wt.fb] : 0, fast_after ? lo[wt.bb + 1] - 1 : A.N - 1, true);
+        if (A.trace2 && threadIdx.x == 0 && step < TRACE_STEPS) A.trace[(uint64_t)step * TRACE_W + 6] = now();
       }
+      if (npend) {  // the last step's bvec kills, after the record is out
+        for (uint32_t i = threadIdx.x; i < npend; i += NT) bv.kill_in(s_plist[i], s_pbin[i]);
+        npend = 0;
+        __syncthreads();
+      }
+      const bool fast = wt.fb < A.nb && wt.bb < A.nb && cnt[wt.fb] > 0 && cnt[wt.bb] > 0;
       int64_t count = 0;
       if (fast) {
         // nearest-alive form (bv_fast_window): four one-wave queries side by side
@@ -1598,6 +1631,7 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
     if (threadIdx.x < nact) {  // (nact <= G - 1 < NT)
       const uint32_t wk = Div32(GW).mod((uint32_t)c0 + threadIdx.x);
       const uint64_t *q = A.partials + (uint64_t)wk * PART_G;
+      const uint32_t poff = wk * PART_G * 8;
       const uint64_t t0 = now();
       uint64_t g8[PART_G];
       for (uint32_t it = 1;; it++) {
@@ -1614,8 +1648,14 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
             }
           }
         } else {
+          // 16-byte sc1 loads of granule pairs (half the requests of 8-byte loads; each 8-byte
+          // granule still carries its own tag)
 #pragma unroll
-          for (int j = 0; j < 5 + INL; j++) g8[j] = ld64(q + j);
+          for (int j = 0; j < PART_G / 2; j++) {
+            const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(prs, (int)(poff + 16 * j), 0, 16);
+            g8[2 * j] = ((uint64_t)v.y << 32) | v.x;
+            g8[2 * j + 1] = ((uint64_t)v.w << 32) | v.z;
+          }
 #pragma unroll
           for (int j = 0; j < 5 + INL; j++) ok &= (uint32_t)(g8[j] >> 32) == step;
         }
@@ -1780,7 +1820,9 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
       // remove_available: the new members, one thread each, all their loads in flight at once
       // (member i on thread i + 64: wave 0, which publishes the next record, keeps no
       // outstanding stores for that record's drain to wait on)
-      for (uint64_t i = (threadIdx.x + NT - 64) % NT; i < nflag && i < PLIST; i += NT) take(M + i, s_plist[i], false);
+      for (uint64_t i = (threadIdx.x + NT - 64) % NT; i < nflag && i < PLIST; i += NT)
+        take(M + i, s_plist[i], false, (int64_t)i);
+      npend = nflag < PLIST ? (uint32_t)nflag : PLIST;
       if (M + nflag > A.mrow) drain();  // members past the cache are read back from mem_pos / mkeys
       __syncthreads();
       if (A.prof && threadIdx.x == 0) t_ws[3] += now() - tq;  // (the takes, inside "column sums")
@@ -2065,7 +2107,7 @@ bool accum_plan(const mc_ctx *c, uint32_t nb, AccPlan *pl) {
        : c->width == 1 ? (nch == 16 ? reinterpret_cast<const void *>(&accum_kernel<uint8_t, 16>)
                                     : reinterpret_cast<const void *>(&accum_kernel<uint8_t, 0>))
                        : reinterpret_cast<const void *>(&accum_kernel<uint16_t, 0>);
-  const size_t static_lds = 12 * 1024;  // both roles' __shared__ words, with margin
+  const size_t static_lds = 16 * 1024;  // both roles' __shared__ words (13.1 KB), with margin
   const size_t cap = 160 * 1024 - static_lds;
   // worker: record words, centre row (wide), alive flags, resident rows (not wide)
   const size_t wfix = (size_t)(pl->rec_g + 3) / 4 * 16 + (wide ? (size_t)nch * 16 : 0) + (pl->fcap + 15) / 16 * 16;
@@ -2136,6 +2178,15 @@ int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, 
   }
   const uint32_t G = pl.G, GW = G - 1;
   const int nch = (int)((c->B * c->width + 15) / 16);
+  {
+    hipFuncAttributes fa;
+    MCG_CHECK(hipFuncGetAttributes(&fa, pl.fn));
+    if (fa.sharedSizeBytes + pl.lds > 160 * 1024) {  // (accum_plan's static_lds margin is too small)
+      set_error("accumulation kernel: static + dynamic LDS exceed 160 KB (" + std::to_string(fa.sharedSizeBytes) +
+                " + " + std::to_string(pl.lds) + ")");
+      return MC_ERR_HIP;
+    }
+  }
   MCG_CHECK(hipFuncSetAttribute(pl.fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pl.lds));
   int per_cu = 0;
   MCG_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pl.fn, NT, pl.lds));

@@ -23,11 +23,6 @@ struct Center {
 // step of the accumulation is split over the ranks by record (static bvec blocks), each
 // mean-shift iteration by centre; the ranks exchange partial step results and new centres with
 // `allgather` (equal blocks of `bytes`, rank order into `out`; returns 0 on success).
-struct ShardComm {
-  int rank = 0, world = 1;
-  int (*allgather)(void *user, const void *in, uint64_t bytes, void *out) = nullptr;
-  void *user = nullptr;
-};
 
 // Fault injection for the multi-rank tests: MC_FAULT=<rank>:<stage> makes that rank throw at
 // that stage ("upload", "train", "accumulate", "update"), so the tests can check that every

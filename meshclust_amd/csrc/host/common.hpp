@@ -20,6 +20,15 @@ struct Error : std::runtime_error {
 };
 // A rank stopping because another rank reported a failure (or an exchange was aborted): the
 // multi-rank driver reports the failing rank's own error in preference to these.
+// Several ranks (GPUs) sharing one clustering: rank r of `world`, and an all-gather of a fixed
+// number of bytes per rank (RCCL between processes, a shared buffer between the threads of
+// one process, gloo in the CPU tests).
+struct ShardComm {
+  int rank = 0, world = 1;
+  int (*allgather)(void *user, const void *in, uint64_t bytes, void *out) = nullptr;
+  void *user = nullptr;
+};
+
 struct PeerError : Error {
   explicit PeerError(const std::string &m) : Error(m, 1) {}
 };

@@ -180,6 +180,7 @@ RunResult run_pipeline(const Dataset &ds, mc_ctx *ctx, Options opt, bool upload,
   tc.k = opt.align ? 0 : opt.k;
   tc.threads = threads;
   tc.verbose = verbose;
+  tc.comm = comm;
   Trainer tr(ds, ctx, tc, rr.timer);
   // The bvec (Runner.cpp:345-350: insert every point, insert_finalize) depends only on the
   // lengths, so a host thread builds it while the trainer runs, with a quarter of the

@@ -7,6 +7,7 @@
 #include <atomic>
 #include <cmath>
 #include <cstdio>
+#include <cstring>
 #include <exception>
 #include <set>
 #include <thread>
@@ -67,6 +68,15 @@ std::pair<std::vector<PairId>, std::vector<PairId>> bin_data(const std::vector<L
 }  // namespace
 
 bool Trainer::hdr_less(uint32_t a, uint32_t b) const { return ds_.headers[a].compare(ds_.headers[b]) < 0; }
+
+bool Trainer::gather(const std::vector<uint64_t> &mine, std::vector<uint64_t> &all) const {
+  const ShardComm *cm = cfg_.comm;
+  if (!cm || cm->world <= 1) return false;
+  all.assign(mine.size() * (size_t)cm->world, 0);
+  if (cm->allgather(cm->user, mine.data(), mine.size() * 8, all.data()) != 0)
+    throw PeerError("training all-gather across ranks failed");
+  return true;
+}
 
 void Trainer::nw_batch(const std::vector<PairId> &pairs, std::vector<double> &ident) {
   std::vector<uint32_t> a(pairs.size()), b(pairs.size());
@@ -167,18 +177,29 @@ std::vector<PairId> Trainer::split() {
       live[2 * n + 1] = live[2 * n + 2] = oc > 0;
     }
   };
+  // Several ranks: rank r runs the chains (binary searches and samples) of its block of pivots
+  // [i0, i1) -- each chain needs only its own pivot's sorted array -- and the sampled pairs are
+  // all-gathered at the end (one exchange; the pairs go into a header-ordered set, so the
+  // union is the same whatever rank found them).
+  const int W = cfg_.comm && cfg_.comm->world > 1 ? cfg_.comm->world : 1;
+  const size_t per = (P + (size_t)W - 1) / (size_t)W;
+  const size_t i0 = std::min(P, per * (size_t)(W > 1 ? cfg_.comm->rank : 0)), i1 = std::min(P, i0 + per);
+  const uint64_t nw_pairs0 = nw_pairs, nw_cells0 = nw_cells;
   {
     Scope s(timer_, "train.sort_keys");
     Scope s3(timer_, "train.sort_keys.pivots");
-    check(mc_split_begin(ctx_, indices.data(), (uint32_t)P, points.data(), N), "mc_split_begin");
+    if (i1 > i0) check(mc_split_begin(ctx_, indices.data() + i0, (uint32_t)(i1 - i0), points.data(), N), "mc_split_begin");
   }
   // ids at sorted positions of the pivots' arrays
   std::vector<uint32_t> q_arr, q_ids;
   std::vector<uint64_t> q_pos;
   auto select = [&]() {
     q_ids.resize(q_arr.size());
-    if (!q_arr.empty())
-      check(mc_split_select(ctx_, q_arr.size(), q_arr.data(), q_pos.data(), q_ids.data()), "mc_split_select");
+    if (!q_arr.empty()) {  // (arrays are numbered from this rank's first pivot)
+      std::vector<uint32_t> la(q_arr.size());
+      for (size_t q = 0; q < q_arr.size(); q++) la[q] = q_arr[q] - (uint32_t)i0;
+      check(mc_split_select(ctx_, q_arr.size(), la.data(), q_pos.data(), q_ids.data()), "mc_split_select");
+    }
   };
   // binary search with alignment (:703-721): the 150 dependent chains advance together.  Each
   // round aligns, for every active chain, the next `look` levels of its decision tree at once
@@ -205,7 +226,7 @@ std::vector<PairId> Trainer::split() {
     std::vector<std::vector<char>> tlive(P);
     for (;;) {
       who.clear();
-      for (size_t i = 0; i < P; i++) {
+      for (size_t i = i0; i < i1; i++) {
         if (active[i] && offset[i] == 0) active[i] = 0;
         if (active[i]) who.push_back(i);
       }
@@ -266,7 +287,7 @@ std::vector<PairId> Trainer::split() {
     q_arr.clear();
     q_pos.clear();
     std::vector<size_t> sp;
-    for (size_t i = 0; i < P; i++) {
+    for (size_t i = i0; i < i1; i++) {
       sp.clear();
       sample_positions(pivot[i], sp);
       for (size_t x : sp) {
@@ -279,7 +300,36 @@ std::vector<PairId> Trainer::split() {
       const uint32_t p = indices[q_arr[q]], x = q_ids[q];
       bufs[q_arr[q]].push_back(hdr_less(p, x) ? PairId(p, x) : PairId(x, p));
     }
-    check(mc_split_end(ctx_), "mc_split_end");
+    if (i1 > i0) check(mc_split_end(ctx_), "mc_split_end");
+    // the ranks' pivots and samples: [nw pairs, nw cells, pairs, pivot[i0..i1), pairs (a << 32 | b)]
+    const size_t cap = per * (2 * to_add_each);
+    std::vector<uint64_t> mine(3 + per + cap, 0), all;
+    mine[0] = nw_pairs - nw_pairs0;
+    mine[1] = nw_cells - nw_cells0;
+    size_t np = 0;
+    for (size_t i = i0; i < i1; i++) {
+      mine[3 + (i - i0)] = pivot[i];
+      for (const PairId &pr : bufs[i]) mine[3 + per + np++] = ((uint64_t)pr.first << 32) | pr.second;
+    }
+    mine[2] = np;
+    if (gather(mine, all)) {
+      nw_pairs = nw_pairs0;
+      nw_cells = nw_cells0;
+      for (int r = 0; r < W; r++) {
+        const uint64_t *b = all.data() + (size_t)r * mine.size();
+        const size_t r0 = std::min(P, per * (size_t)r), r1 = std::min(P, r0 + per);
+        nw_pairs += b[0];
+        nw_cells += b[1];
+        for (size_t i = r0; i < r1; i++) {
+          pivot[i] = b[3 + (i - r0)];
+          if (r != cfg_.comm->rank) bufs[i].clear();
+        }
+        if (r == cfg_.comm->rank) continue;
+        // (another rank's pairs go to the first pivot of its block: only the union matters)
+        for (uint64_t q = 0; q < b[2] && r1 > r0; q++)
+          bufs[r0].push_back(PairId((uint32_t)(b[3 + per + q] >> 32), (uint32_t)b[3 + per + q]));
+      }
+    }
   }
   for (size_t i = 0; i < P; i++) {  // the warning flag keeps the serial loop's last writer
     double before_inc = (double)pivot[i] / to_add_each;
@@ -303,7 +353,32 @@ void Trainer::get_labels(const std::vector<PairId> &vec, std::vector<Labeled> &b
   std::vector<double> al;
   {
     Scope s(timer_, "train.nw_labels");
-    nw_batch(vec, al);
+    const int W = cfg_.comm && cfg_.comm->world > 1 ? cfg_.comm->world : 1;
+    if (W == 1) {
+      nw_batch(vec, al);
+    } else {
+      // rank r aligns pairs [r * per, (r + 1) * per); the identities are all-gathered
+      const size_t m = vec.size(), per = (m + (size_t)W - 1) / (size_t)W;
+      const size_t j0 = std::min(m, per * (size_t)cfg_.comm->rank), j1 = std::min(m, j0 + per);
+      const uint64_t p0 = nw_pairs, c0 = nw_cells;
+      std::vector<double> part;
+      nw_batch(std::vector<PairId>(vec.begin() + j0, vec.begin() + j1), part);
+      std::vector<uint64_t> mine(2 + per, 0), all;
+      mine[0] = nw_pairs - p0;
+      mine[1] = nw_cells - c0;
+      for (size_t j = j0; j < j1; j++) memcpy(&mine[2 + (j - j0)], &part[j - j0], 8);
+      gather(mine, all);
+      nw_pairs = p0;
+      nw_cells = c0;
+      al.assign(m, 0.0);
+      for (int r = 0; r < W; r++) {
+        const uint64_t *b = all.data() + (size_t)r * mine.size();
+        const size_t r0 = std::min(m, per * (size_t)r), r1 = std::min(m, r0 + per);
+        nw_pairs += b[0];
+        nw_cells += b[1];
+        for (size_t j = r0; j < r1; j++) memcpy(&al[j], &b[2 + (j - r0)], 8);
+      }
+    }
   }
   std::set<Labeled, decltype(hcmp)> buf_pos(hcmp), buf_neg(hcmp);
   for (size_t i = 0; i < vec.size(); i++) {

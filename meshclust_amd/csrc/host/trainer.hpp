@@ -25,6 +25,9 @@ struct TrainerConfig {
   int k = 4;                     // 0 => alignment mode (Runner.cpp:332)
   int threads = 1;
   bool verbose = true;
+  // several ranks: each runs the sampler's binary searches of its block of pivots and its
+  // share of the label alignments; the results are all-gathered (null / world 1: one rank)
+  const ShardComm *comm = nullptr;
 };
 
 class Trainer {
@@ -48,6 +51,8 @@ class Trainer {
   Matrix feat_matrix(const std::vector<PairId> &pos, const std::vector<PairId> &neg, int ncols,
                      Matrix &labels);
   void nw_batch(const std::vector<PairId> &pairs, std::vector<double> &ident);
+  // all-gather of `words` u64 per rank (every rank the same count); false: one rank
+  bool gather(const std::vector<uint64_t> &mine, std::vector<uint64_t> &all) const;
   bool hdr_less(uint32_t a, uint32_t b) const;
 
   const Dataset &ds_;
