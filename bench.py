@@ -76,8 +76,8 @@ def cpu_baseline(fasta, args, n_reads, threads, repeats, limit_s=600):
         return None
     walls = []
     with tempfile.TemporaryDirectory() as td:
-        out = os.path.join(td, "o.clstr")
-        for _ in range(repeats):
+        for i in range(repeats):
+            out = os.path.join(td, "o%d.clstr" % i)  # (a new file per run, as the GPU steps)
             t0 = time.perf_counter()
             try:
                 r = subprocess.run([ref, fasta] + args + ["--threads", str(threads), "--output", out],
@@ -157,10 +157,15 @@ def main():
     # GPU made the process fault in the system HSA runtime's exit handler under rocprofv3.
     sync = eng.sync  # hipDeviceSynchronize on this rank's GPU
     out_dir = tempfile.mkdtemp(prefix="mc_bench_out")
-    clstr = os.path.join(out_dir, "bench_rank%d.clstr" % rank)
+    nstep = [0]
 
     def one_step():
-        """parse -> upload -> GPU pipeline -> .clstr written (the BASELINE metric's work)."""
+        """parse -> upload -> GPU pipeline -> .clstr written (the BASELINE metric's work).
+        Every run writes a new output file, as a clustering run does (rewriting one path would
+        time the kernel freeing the previous run's page-cache pages on O_TRUNC: 2.5 ms for
+        4 MB); the files are removed after the timed region."""
+        nstep[0] += 1
+        clstr = os.path.join(out_dir, "bench_rank%d_%d.clstr" % (rank, nstep[0]))
         t = time.perf_counter()
         ds = M.Dataset([fasta], threads=threads)
         t1 = time.perf_counter()

@@ -378,7 +378,15 @@ __global__ __launch_bounds__(NT) void mean_shift_kernel(HistView H, DevClassifie
                                                         uint32_t jbase) {
   extern __shared__ __attribute__((aligned(16))) uint4 dyn[];
   __shared__ uint32_t cnt;
-  const uint32_t j = jbase + blockIdx.x;
+  // XCD-aware order (speed only: blocks are dealt round-robin over the 8 XCDs): the blocks one
+  // XCD runs take consecutive centres, so the neighbourhoods j - delta .. j + delta they read
+  // overlap in that XCD's L2 instead of being fetched by eight L2s
+  uint32_t jl;
+  {
+    const uint32_t nb = gridDim.x, x = blockIdx.x % 8, k = blockIdx.x / 8, r = nb % 8, qlo = nb / 8;
+    jl = x < r ? x * (qlo + 1) + k : r * (qlo + 1) + (x - r) * qlo + k;
+  }
+  const uint32_t j = jbase + jl;
   const int nch = (int)((H.B * (int)sizeof(T) + 15) / 16);
   uint4 *clds = dyn;
   double *mean = reinterpret_cast<double *>(dyn + nch);

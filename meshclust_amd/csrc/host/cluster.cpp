@@ -585,17 +585,6 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
   return part;
 }
 
-namespace {
-inline void put_uint(std::string &o, unsigned long long v) {
-  char b[24];
-  int n = 0;
-  do {
-    b[n++] = (char)('0' + v % 10);
-    v /= 10;
-  } while (v);
-  while (n) o.push_back(b[--n]);
-}
-}  // namespace
 
 // print_output (ClusterFactory.cpp:495-520): ">Cluster c" for every non-empty cluster, then
 // "i\t{len}nt, {header}... " per member with '*' after the centre.  Clusters are formatted
@@ -612,31 +601,61 @@ void write_clstr(const std::string &path, const Dataset &ds, const std::vector<C
   std::vector<std::string> out(T);
   std::vector<uint64_t> at(T + 1, 0);
   bool ok = true;
+  auto ndig = [](unsigned long long v) {
+    int n = 1;
+    while (v >= 10) {
+      v /= 10;
+      n++;
+    }
+    return n;
+  };
+  auto put = [](char *o, unsigned long long v, int n) {  // n = ndig(v)
+    for (int i = n - 1; i >= 0; i--) {
+      o[i] = (char)('0' + v % 10);
+      v /= 10;
+    }
+    return o + n;
+  };
 #pragma omp parallel num_threads(T)
   {
 #pragma omp for schedule(static, 1)
     for (int t = 0; t < T; t++) {
-      std::string &o = out[t];
+      // exact size first, then every line written into the buffer in place
       const size_t c0 = C * t / T, c1 = C * (t + 1) / T;
-      size_t est = 0;
-      for (size_t c = c0; c < c1; c++) est += 24 + part[c].points.size() * 48;
-      o.reserve(est);
+      size_t bytes = 0;
       for (size_t c = c0; c < c1; c++) {
         const auto &cen = part[c];
         if (cen.points.empty()) continue;
-        o += ">Cluster ";
-        put_uint(o, (unsigned long long)label[c]);
-        o += '\n';
+        bytes += 10 + (size_t)ndig((unsigned long long)label[c]);
+        unsigned long long pt = 0;
+        for (uint32_t p : cen.points)
+          bytes += (size_t)ndig(pt++) + 1 + (size_t)ndig(ds.lengths[p]) + 4 + ds.headers[p].size() + 4 +
+                   (p == cen.centre ? 1 : 0) + 1;
+      }
+      std::string &o = out[t];
+      o.resize(bytes);
+      char *w = &o[0];
+      for (size_t c = c0; c < c1; c++) {
+        const auto &cen = part[c];
+        if (cen.points.empty()) continue;
+        memcpy(w, ">Cluster ", 9);
+        w = put(w + 9, (unsigned long long)label[c], ndig((unsigned long long)label[c]));
+        *w++ = '\n';
         unsigned long long pt = 0;
         for (uint32_t p : cen.points) {
-          put_uint(o, pt++);
-          o += '\t';
-          put_uint(o, (unsigned long long)ds.lengths[p]);
-          o += "nt, ";
-          o += ds.headers[p];
-          o += "... ";
-          if (p == cen.centre) o += '*';
-          o += '\n';
+          w = put(w, pt, ndig(pt));
+          pt++;
+          *w++ = '\t';
+          w = put(w, ds.lengths[p], ndig(ds.lengths[p]));
+          memcpy(w, "nt, ", 4);
+          w += 4;
+          const auto h = ds.headers[p];
+          memcpy(w, h.data(), h.size());
+          w += h.size();
+          memcpy(w, "... ", 4);
+          w += 4;
+          if (p == cen.centre) *w++ = '*';
+          *w++ = '\n';
         }
       }
     }
