@@ -80,248 +80,23 @@ struct NWPairs {
   const uint32_t *out;  // optional result slot per pair (else the pair index)
 };
 
-template <int R, typename P>
-__global__ __launch_bounds__(64) void nw_kernel(NWPairs q) {
-  constexpr int SH = Pack<P>::SH;
-  constexpr P LEN1 = (P)1 << SH;
-  const uint32_t slot = blockIdx.x;
-  if (slot >= q.npairs) return;
-  const uint32_t p = q.pidx[slot];
-  const uint8_t *a = q.A + q.aoff[q.ai[p]];
-  const int la = (int)(q.aoff[q.ai[p] + 1] - q.aoff[q.ai[p]]);
-  const uint8_t *b = q.Bq + q.boff[q.bi[p]];
-  const int lb = (int)(q.boff[q.bi[p] + 1] - q.boff[q.bi[p]]);
-  const int lane = threadIdx.x;
-  const int len1 = la + 1, len2 = lb + 1;
-  const int shorter = (len2 < len1 ? len2 : len1) - 1;
-  const int lenDiff = len2 > len1 ? len2 - len1 : len1 - len2;
-  int maxDiff = 0;
-  if (lenDiff >= 1) maxDiff += -GO - lenDiff * GE;
-  maxDiff += MISMATCH * shorter - 1;
-  const int NINF = maxDiff;
-  int *bnd = q.bnd ? q.bnd + q.bnd_off[slot] : nullptr;  // 6 ints per column, columns 0..lb
-  const int nblk = (la + 64 * R - 1) / (64 * R);
-  int fin_score = 0;
-  P fin_pay = 0;
-  for (int blk = 0; blk < (nblk > 0 ? nblk : 1); blk++) {
-    const int itop = blk * 64 * R + lane * R + 1;  // first row of this lane
-    uint8_t ac[R];
-    int M[R], X[R], Y[R];
-    P MP[R], XP[R], YP[R];
-#pragma unroll
-    for (int r = 0; r < R; r++) {
-      const int i = itop + r;
-      ac[r] = i <= la ? a[i - 1] : (uint8_t)0xFF;
-      // column 0 (GlobAlignE.cpp:140-160): M = Y = -inf, X = -o - i*e, lengths i (T: + i)
-      M[r] = NINF + i;
-      Y[r] = NINF + i;
-      X[r] = -GO - i * GE + i;
-      MP[r] = XP[r] = YP[r] = 0;  // i gap moves, no diagonal
-    }
-    // diagonal input for column 1: row itop-1 at column 0
-    int dM, dX, dY;
-    P dMP, dXP, dYP;
-    {
-      const int i = itop - 1;
-      if (i == 0) {  // matches[0]=0, lowerGap[0]=-inf, upperGapLag at j=1 = -o
-        dM = 0;
-        dX = NINF;
-        dY = -GO;
-        dMP = dXP = dYP = 0;
-      } else {  // (T: + i)
-        dM = NINF + i;
-        dX = -GO - i * GE + i;
-        dY = NINF + i;
-        dMP = dXP = dYP = 0;
-      }
-    }
-    int oM = NINF, oX = NINF, oY = NINF;  // this lane's bottom row, last computed column
-    P oMP = 0, oXP = 0, oYP = 0;
-    uint8_t ob = 0;
-    const int steps = lb + 63;
-    // seq2 codes for lane 0 (column t + 1 at step t): one 64-byte block per 64 steps, lane l
-    // holding byte l, loaded a block ahead and read with a uniform readlane
-    int bcur = 0, bnext = lane < lb ? b[lane] : 0;
-    for (int t = 0; t < steps; t++) {
-      const int j = t - lane + 1;  // column of this lane at this step
-      if ((t & 63) == 0) {
-        bcur = bnext;
-        const int nx = t + 64 + lane;
-        bnext = nx < lb ? b[nx] : 0;
-      }
-      // hand-off from lane-1: its bottom row at column j (computed at step t-1) + seq2 code
-      int uM = dpp_shr1(oM), uX = dpp_shr1(oX), uY = dpp_shr1(oY);
-      P uMP = dshr<P>(oMP), uXP = dshr<P>(oXP), uYP = dshr<P>(oYP);
-      uint8_t bc = (uint8_t)dpp_shr1((int)ob);
-      const int b0 = __builtin_amdgcn_readlane(bcur, t & 63);
-      if (lane == 0) {
-        bc = (j >= 1 && j <= lb) ? (uint8_t)b0 : 0;
-        if (blk == 0) {  // row 0 at column j: M = X = -inf, Y = -o - j*e, lengths j (T: + j)
-          uM = NINF + j;
-          uX = NINF + j;
-          uY = -GO - j * GE + j;
-          uMP = uXP = uYP = 0;
-        } else if (j >= 1 && j <= lb) {
-          const int *s = bnd + 6 * j;
-          uM = s[0];
-          uX = s[1];
-          uY = s[2];
-          uMP = (P)(uint32_t)s[3];
-          uXP = (P)(uint32_t)s[4];
-          uYP = (P)(uint32_t)s[5];
-          if constexpr (sizeof(P) == 8) {
-            // long pairs keep 64-bit payloads in two boundary records
-            const int *s2 = bnd + 6 * (lb + 1) + 6 * j;
-            uMP |= (P)(uint32_t)s2[3] << 32;
-            uXP |= (P)(uint32_t)s2[4] << 32;
-            uYP |= (P)(uint32_t)s2[5] << 32;
-          }
-        }
-      }
-      if (j >= 1 && j <= lb) {
-        // above (row itop-1, column j) = u*, diagonal (row itop-1, column j-1) = d*
-        int aM = uM, aX = uX;
-        P aMP = uMP, aXP = uXP;
-        int gM = dM, gX = dX, gY = dY;
-        P gMP = dMP, gXP = dXP, gYP = dYP;
-#pragma unroll
-        for (int r = 0; r < R; r++) {
-          const int pM = M[r], pX = X[r], pY = Y[r];  // (i, j-1): this row's previous column
-          const P pMP = MP[r], pXP = XP[r], pYP = YP[r];
-          // upperGap (GlobAlignE.cpp:233-251)
-          const int yb = pM - OPEN_T, yc = pY + EXT_T;
-          const bool yFromM = yb >= yc;
-          Y[r] = yFromM ? yb : yc;
-          YP[r] = yFromM ? pMP : pYP;
-          // matches (:255-299)
-          const bool hit = ac[r] == bc;
-          const int s = hit ? MATCH_T : MISMATCH_T;
-          // M on ties, then X, then Y: M iff gM >= max(gX, gY), else X iff gX >= gY
-          const bool xy = gX >= gY;
-          const int mxy = xy ? gX : gY;
-          const P pxy = xy ? gXP : gYP;
-          const bool fromM = gM >= mxy;
-          const int best = fromM ? gM : mxy;
-          const P bestP = fromM ? gMP : pxy;
-          M[r] = best + s;
-          MP[r] = bestP + LEN1 + (hit ? (P)1 : (P)0);
-          // lowerGap (:316-330), from the row above in this column
-          const int xb = aM - OPEN_T, xc = aX + EXT_T;
-          const bool xFromM = xb >= xc;
-          X[r] = xFromM ? xb : xc;
-          XP[r] = xFromM ? aMP : aXP;
-          // next row: above = this row's new values, diagonal = this row's old values
-          aM = M[r];
-          aX = X[r];
-          aMP = MP[r];
-          aXP = XP[r];
-          gM = pM;
-          gX = pX;
-          gY = pY;
-          gMP = pMP;
-          gXP = pXP;
-          gYP = pYP;
-        }
-        dM = uM;
-        dX = uX;
-        dY = uY;
-        dMP = uMP;
-        dXP = uXP;
-        dYP = uYP;
-        oM = M[R - 1];
-        oX = X[R - 1];
-        oY = Y[R - 1];
-        oMP = MP[R - 1];
-        oXP = XP[R - 1];
-        oYP = YP[R - 1];
-        ob = bc;
-        if (lane == 63 && blk + 1 < nblk) {
-          int *s = bnd + 6 * j;
-          s[0] = oM;
-          s[1] = oX;
-          s[2] = oY;
-          s[3] = (int)(uint32_t)oMP;
-          s[4] = (int)(uint32_t)oXP;
-          s[5] = (int)(uint32_t)oYP;
-          if constexpr (sizeof(P) == 8) {
-            int *s2 = bnd + 6 * (lb + 1) + 6 * j;
-            s2[3] = (int)(uint32_t)(oMP >> 32);
-            s2[4] = (int)(uint32_t)(oXP >> 32);
-            s2[5] = (int)(uint32_t)(oYP >> 32);
-          }
-        }
-      } else {
-        ob = bc;
-      }
-    }
-    // the final cell (la, lb) lives in this block's lane/row
-    const int fl = la - blk * 64 * R - 1;
-    if (fl >= 0 && fl < 64 * R && lane == fl / R) {
-      const int r = fl % R;
-      int mM = 0, mX = 0, mY = 0;
-      P pM = 0, pX = 0, pY = 0;
-#pragma unroll
-      for (int rr = 0; rr < R; rr++)
-        if (rr == r) {
-          mM = M[rr];
-          mX = X[rr];
-          mY = Y[rr];
-          pM = MP[rr];
-          pX = XP[rr];
-          pY = YP[rr];
-        }
-      // GlobAlignE.cpp:278-291: M, then lowerGap (X), then upperGap (Y)
-      int sc = mM > mX ? mM : mX;
-      sc = sc > mY ? sc : mY;
-      fin_score = sc - (la + lb);  // (T -> score)
-      fin_pay = sc == mM ? pM : (sc == mX ? pX : pY);
-    }
-    __syncthreads();
-  }
-  const int fl = la - (nblk - 1) * 64 * R - 1;
-  const int owner = la == 0 ? 0 : fl / R;
-  if (lane == owner) {
-    int L, I;
-    if (la == 0) {
-      // no rows (len1 == 1): only cell 0 of each state row exists.  With columns
-      // (lb > 0) every j leaves matches[0] = lowerGap[0] = -inf, matchLen[0] = j and
-      // upperGap[0] = -inf untouched, so the final max picks `matches` (GlobAlignE.cpp:
-      // 244-251, 278-283): score -inf, length lb, 0 identities.  Without columns the
-      // initial state (0, 0, 0) is the answer and the identity is 0/0.
-      L = lb;
-      I = 0;
-      fin_score = lb > 0 ? NINF : 0;
-    } else {
-      L = la + lb - (int)(fin_pay >> SH);
-      I = (int)(fin_pay & (((P)1 << SH) - 1));
-    }
-    const uint32_t o = q.out ? q.out[p] : p;
-    q.ident[o] = (double)I / (double)L;
-    if (q.len) q.len[o] = L;
-    if (q.ids) q.ids[o] = I;
-    if (q.score) q.score[o] = fin_score;
-  }
-}
-
-template <int R, typename P>
-int launch_bucket(mc_ctx *c, NWPairs q) {
-  if (q.npairs == 0) return MC_OK;
-  nw_kernel<R, P><<<q.npairs, 64, 0, c->stream>>>(q);
-  MCG_CHECK(hipGetLastError());
-  return MC_OK;
-}
-
-
 // ---------------------------------------------------------------------------------------
-// Latency form for small batches (the training sampler's dependent alignment rounds): one
-// pair per workgroup of W waves.  Wave w owns rows [w*64*R, (w+1)*64*R) of each row block and
-// runs 64 + KLAG steps behind wave w-1; lane 63 of wave w-1 leaves its bottom row for column
-// j in an LDS ring that lane 0 of wave w reads KLAG + 1 steps later.  A workgroup barrier
-// every KLAG steps orders those writes and reads (a slot is rewritten RING_C columns later,
-// with a barrier in between).  Inside a wave the bottom row moves down by one lane per step
-// with DPP wave_shr:1 (a VALU move, no LDS round trip).
+// One kernel, two launch forms.  A pair per workgroup of W waves: wave w owns rows
+// [w*64*R, (w+1)*64*R) of each row block and runs 64 + KLAG steps behind wave w-1; lane 63 of
+// wave w-1 leaves its bottom row for column j in an LDS ring that lane 0 of wave w reads
+// KLAG + 1 steps later.  A workgroup barrier every KLAG steps orders those writes and reads (a
+// slot is rewritten RING_C columns later, with a barrier in between).  Inside a wave the
+// bottom row moves down by one lane per step with DPP wave_shr:1 (a VALU move, no LDS round
+// trip).
+//  * throughput form (many pairs: the label batch, the --align window scans): W = 1, a wave
+//    per pair, R = 4 / 8 / 16 rows per lane, no LDS;
+//  * latency form (< 1,024 pairs: the sampler's dependent rounds): W = 4 / 8 / 16 waves.
+// The steady-state steps (every lane inside the matrix) run unrolled by two with no per-lane
+// branches, so the state registers of consecutive steps alternate instead of being copied
+// back: 18 VALU instructions per cell at R = 16 against 26.5 for the earlier single-wave
+// kernel, whose loop-carried state cost ~90 v_mov per step.
 constexpr int KLAG = 16, RING_C = 64;
-struct GenStep {  // tags of the latency form's step variants
+struct GenStep {  // tags of the step variants
   static constexpr bool value = true;
 };
 struct SteadyStep {
@@ -390,7 +165,7 @@ __global__ __launch_bounds__(64 * W) void nw_mw_kernel(NWPairs q) {
     int ob = 0;
     const int lagw = w * (64 + KLAG);
     const int steps = lb + 63 + (W - 1) * (64 + KLAG);
-    int bcur = 0, bnext = lane < lb ? b[lane] : 0;  // seq2 blocks for lane 0, as in nw_kernel
+    int bcur = 0, bnext = lane < lb ? b[lane] : 0;  // seq2 codes for lane 0: one 64-byte block per 64 steps, lane l holding byte l, loaded a block ahead and read with a uniform readlane
     // lane 0's hand-in for its next column, loaded one step ahead so the LDS / global latency
     // hides behind a step of cell updates (the slot was written >= KLAG steps earlier, with a
     // barrier in between, see above)
@@ -615,7 +390,11 @@ __global__ __launch_bounds__(64 * W) void nw_mw_kernel(NWPairs q) {
   const int owner = la == 0 ? 0 : fl / R;
   if (gl == owner) {
     int L, I;
-    if (la == 0) {  // see nw_kernel
+    if (la == 0) {
+      // no rows (len1 == 1): only cell 0 of each state row exists.  With columns (lb > 0)
+      // every j leaves matches[0] = lowerGap[0] = -inf, matchLen[0] = j and upperGap[0] = -inf
+      // untouched, so the final max picks `matches` (GlobAlignE.cpp:244-251, 278-283): score
+      // -inf, length lb, 0 identities.  Without columns the initial state is the answer, 0/0.
       L = lb;
       I = 0;
       fin_score = lb > 0 ? NINF : 0;
@@ -643,6 +422,14 @@ inline int mw_waves(uint64_t la) {
     return v == 4 || v == 8 || v == 16 ? v : 0;
   }();
   return forced ? forced : la <= 1024 ? 4 : 8;
+}
+
+template <int R, typename P>
+int launch_bucket(mc_ctx *c, NWPairs q) {
+  if (q.npairs == 0) return MC_OK;
+  nw_mw_kernel<R, P, 1><<<q.npairs, 64, 0, c->stream>>>(q);
+  MCG_CHECK(hipGetLastError());
+  return MC_OK;
 }
 
 template <int R, typename P>
