@@ -283,6 +283,18 @@ int mc_mean_shift(mc_ctx *ctx, const uint32_t *centre_ids, uint32_t C, const uin
                   const uint32_t *members, int delta, uint32_t *new_centre);
 
 /*
+ * One iteration of MS's update loop (ClusterFactory.cpp:740-760) in one device round trip:
+ * mc_mean_shift over all centres, then the classifier pairs of merge (ClusterFactory.cpp:
+ * 427-493, Trainer::merge Trainer.cpp:129-157) over the NEW centres: for i in [0, C) and t in
+ * (i, min(C-1, i+delta)], pair q (i-major, t ascending) = feat->compute(new_centre[t],
+ * new_centre[i]); similar[q] / combo0[q] as mc_classify_pairs.  *npairs receives the pair
+ * count (sum over i of min(delta, C-1-i)); similar and combo0 need room for it.
+ */
+int mc_update_iteration(mc_ctx *ctx, const uint32_t *centre_ids, uint32_t C, const uint64_t *member_off,
+                        const uint32_t *members, int delta, uint32_t *new_centre, uint8_t *similar,
+                        double *combo0, uint64_t *npairs);
+
+/*
  * The same for centres j0 <= j < j1 only (new_centre holds j1 - j0 entries): the per-rank
  * share of one iteration when the update is sharded over GPUs by centre; the ranks then
  * all-gather the new centres (the centre-reassignment exchange).

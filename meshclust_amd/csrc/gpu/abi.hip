@@ -1231,6 +1231,47 @@ int mc_mean_shift(mc_ctx *c, const uint32_t *centre_ids, uint32_t C, const uint6
   return mean_shift_common(c, centre_ids, C, member_off, members, delta, nullptr, new_centre, 0, C);
 }
 
+int mc_update_iteration(mc_ctx *c, const uint32_t *centre_ids, uint32_t C, const uint64_t *member_off,
+                        const uint32_t *members, int delta, uint32_t *new_centre, uint8_t *similar, double *combo0,
+                        uint64_t *npairs) {
+  if (!c || !npairs || !member_off) return MC_ERR_ARG;
+  TRY(no_align(c, "mc_update_iteration"));
+  if (!c->has_cls || c->k == 0 || delta < 0) return MC_ERR_STATE;
+  *npairs = 0;
+  if (C == 0) return MC_OK;
+  MCG_CHECK(hipSetDevice(c->device));
+  TRY(check_ids(c, centre_ids, C));
+  const uint64_t nm = member_off[C];
+  TRY(check_ids(c, members, nm));
+  std::vector<uint64_t> poff(C + 1, 0);
+  for (uint32_t i = 0; i < C; i++) poff[i + 1] = poff[i] + std::min<uint64_t>((uint64_t)delta, C - 1 - i);
+  const uint64_t m = poff[C];
+  TRY(upload(c, c->s_a, centre_ids, C, c->stream));
+  TRY(upload(c, c->s_b, member_off, C + 1, c->stream));
+  TRY(upload(c, c->s_c, members, nm, c->stream));
+  TRY(upload(c, c->s_h, poff.data(), C + 1, c->stream));
+  TRY(ensure(c->flags_out, (size_t)C * 4 + 16));
+  TRY(ensure(c->s_i, m * 8 + 16));
+  TRY(ensure(c->s_j, m * 9 + 64));
+  uint32_t *d_new = (uint32_t *)c->flags_out.p;
+  uint32_t *d_pa = (uint32_t *)c->s_i.p, *d_pb = d_pa + m;
+  double *d_c0 = (double *)c->s_j.p;
+  uint8_t *d_sim = (uint8_t *)(d_c0 + m);
+  TRY(launch_mean_shift(c, (uint32_t *)c->s_a.p, C, (uint64_t *)c->s_b.p, member_off, (uint32_t *)c->s_c.p, delta,
+                        nullptr, d_new, 0, C));
+  if (m) {
+    TRY(launch_merge_pairs(c, d_new, C, (const uint64_t *)c->s_h.p, d_pa, d_pb));
+    TRY(launch_pairs(c, d_pa, d_pb, m, nullptr, 0, nullptr, d_sim, d_c0, nullptr, true));
+    if (similar) TRY(download(similar, d_sim, m, c->stream));
+    if (combo0) TRY(download(combo0, d_c0, m, c->stream));
+  }
+  TRY(download(new_centre, d_new, C, c->stream));
+  MCG_CHECK(hipStreamSynchronize(c->stream));
+  flush_timers(c);
+  *npairs = m;
+  return MC_OK;
+}
+
 int mc_mean_shift_range(mc_ctx *c, const uint32_t *centre_ids, uint32_t C, const uint64_t *member_off,
                         const uint32_t *members, int delta, uint32_t j0, uint32_t j1, uint32_t *new_centre) {
   TRY(no_align(c, "mc_mean_shift_range"));

@@ -514,6 +514,28 @@ int launch_pairs(mc_ctx *c, const uint32_t *d_a, const uint32_t *d_b, uint64_t m
   return MC_OK;
 }
 
+// merge's classifier pairs over the new centres (ClusterFactory.cpp:427-493): centre i's pairs
+// are (new[t], new[i]) for t = i+1 .. i + (poff[i+1] - poff[i]), at poff[i]..
+__global__ __launch_bounds__(256) void merge_pairs_kernel(const uint32_t *__restrict__ d_new, uint32_t C,
+                                                          const uint64_t *__restrict__ poff, uint32_t *pa, uint32_t *pb) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= C) return;
+  const uint64_t q0 = poff[i], n = poff[i + 1] - q0;
+  const uint32_t ci = d_new[i];
+  for (uint64_t d = 0; d < n; d++) {
+    pa[q0 + d] = d_new[i + 1 + d];
+    pb[q0 + d] = ci;
+  }
+}
+
+int launch_merge_pairs(mc_ctx *c, const uint32_t *d_new, uint32_t C, const uint64_t *d_poff, uint32_t *d_a,
+                       uint32_t *d_b) {
+  if (C == 0) return MC_OK;
+  merge_pairs_kernel<<<(C + 255) / 256, 256, 0, c->stream>>>(d_new, C, d_poff, d_a, d_b);
+  MCG_CHECK(hipGetLastError());
+  return MC_OK;
+}
+
 int launch_values(mc_ctx *c, const double *d_raw, uint64_t m, uint8_t *d_sim, double *d_c0, double *d_sum) {
   if (m == 0) return MC_OK;
   const int grid = grid_for(m, NT, 4096);

@@ -175,6 +175,8 @@ int launch_select(mc_ctx *c, uint64_t *d_words, uint64_t n, uint32_t *d_scr, Spl
 int launch_pairs(mc_ctx *c, const uint32_t *d_a, const uint32_t *d_b, uint64_t m, const uint16_t *flags, int nflag,
                  double *d_raw, uint8_t *d_sim, double *d_c0, double *d_sum, bool classify);
 int launch_scan(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, const double *d_ident, int *nblocks);
+int launch_merge_pairs(mc_ctx *c, const uint32_t *d_new, uint32_t C, const uint64_t *d_poff, uint32_t *d_a,
+                       uint32_t *d_b);
 int launch_values(mc_ctx *c, const double *d_raw, uint64_t m, uint8_t *d_sim, double *d_c0, double *d_sum);
 int launch_finalize(mc_ctx *c, int nblocks);
 int launch_mean_shift(mc_ctx *c, const uint32_t *d_cid, uint32_t C, const uint64_t *d_off, const uint64_t *h_off,

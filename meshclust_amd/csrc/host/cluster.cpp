@@ -471,7 +471,11 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
       accumulate(&last, ds, ctx, bv, part, cfg, stats, flag_buf, timer, memo.get(), shard, all_flagged);
   }
   Scope s(timer, "update+merge");
+  std::vector<uint8_t> fused_sim;
+  std::vector<double> fused_c0;
   for (int it = 0; it < cfg.iterations; it++) {
+    bool fused = false;
+    uint64_t fused_np = 0;
     // mean_shift_update for every centre, all reading the same state (ClusterFactory.cpp:744-749)
     const uint32_t C = (uint32_t)part.size();
     std::vector<uint32_t> cids(C), members, newc(C);
@@ -512,8 +516,19 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
         }
       for (uint32_t j = 0; j < C; j++) newc[j] = all[(size_t)(j / per) * blk + 1 + j % per];
     } else if (C && !memo) {
-      Scope sm(timer, "update.mean_shift");
-      check(mc_mean_shift(ctx, cids.data(), C, off.data(), members.data(), cfg.delta, newc.data()), "mc_mean_shift");
+      // mean shift and the merge pass's classifier pairs over the new centres in one device
+      // round trip (the pairs below are exactly these, in this order)
+      Scope sm(timer, "update.mean_shift+merge_pairs");
+      uint64_t np = 0;
+      uint64_t npairs = 0;  // sum over i of min(delta, C - 1 - i)
+      for (uint32_t i = 0; i < C; i++) npairs += std::min<uint64_t>((uint64_t)std::max(cfg.delta, 0), C - 1 - i);
+      fused_sim.resize(npairs);
+      fused_c0.resize(fused_sim.size());
+      check(mc_update_iteration(ctx, cids.data(), C, off.data(), members.data(), cfg.delta, newc.data(),
+                                fused_sim.data(), fused_c0.data(), &np),
+            "mc_update_iteration");
+      fused = true;
+      fused_np = np;
     } else if (C) {
       // Trainer::filter(center clone, good): feat->compute(*member, *clone) (Trainer.cpp:334-349)
       std::vector<uint32_t> fa, fb;
@@ -556,7 +571,11 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
     stats.merge_evals += pa.size();
     std::vector<uint8_t> sim(pa.size(), 0);
     std::vector<double> c0(pa.size(), 0.0);
-    if (!pa.empty() && !memo) {
+    if (fused) {
+      if (fused_np != pa.size()) throw Error("mc_update_iteration: merge pair count mismatch", 1);
+      std::copy(fused_sim.begin(), fused_sim.begin() + pa.size(), sim.begin());
+      std::copy(fused_c0.begin(), fused_c0.begin() + pa.size(), c0.begin());
+    } else if (!pa.empty() && !memo) {
       Scope sm(timer, "update.merge_pairs");
       check(mc_classify_pairs(ctx, pa.data(), pb.data(), pa.size(), sim.data(), c0.data(), nullptr), "mc_classify_pairs");
     } else if (!pa.empty()) {  // both centres are clones: only memoised pairs can be similar

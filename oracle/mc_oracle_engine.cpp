@@ -463,6 +463,22 @@ int mc_mean_shift(mc_ctx *c, const uint32_t *cid, uint32_t C, const uint64_t *of
   return mc_mean_shift_range(c, cid, C, off, members, delta, 0, C, newc);
 }
 
+int mc_update_iteration(mc_ctx *c, const uint32_t *cid, uint32_t C, const uint64_t *off, const uint32_t *members,
+                        int delta, uint32_t *newc, uint8_t *similar, double *combo0, uint64_t *npairs) {
+  if (!npairs || delta < 0) return fail(MC_ERR_ARG, "bad arguments");
+  if (c->align) return fail(MC_ERR_STATE, "mc_update_iteration is not available in alignment mode");
+  *npairs = 0;
+  if (int rc = mc_mean_shift_range(c, cid, C, off, members, delta, 0, C, newc)) return rc;
+  std::vector<uint32_t> pa, pb;
+  for (uint32_t i = 0; i < C; i++)
+    for (uint32_t t = i + 1; t < C && t <= i + (uint32_t)delta; t++) {
+      pa.push_back(newc[t]);
+      pb.push_back(newc[i]);
+    }
+  *npairs = pa.size();
+  return mc_classify_pairs(c, pa.data(), pb.data(), pa.size(), similar, combo0, nullptr);
+}
+
 int mc_accumulate(mc_ctx *, const uint32_t *, const uint64_t *, uint32_t, double, uint32_t *, uint64_t *, uint32_t *,
                   uint64_t *, uint64_t *) {
   return fail(MC_ERR_UNSUPPORTED, "the CPU oracle engine drives accumulation step by step");
