@@ -88,7 +88,7 @@ def gpu_lib():
         for name in ("mc_load_sequences", "mc_load_packed", "mc_kmer_max", "mc_kmer_build", "mc_get_histograms", "mc_distance_keys",
                      "mc_pair_features", "mc_set_classifier", "mc_classify_pairs", "mc_nw_identity",
                      "mc_nw_identity_raw", "mc_set_order", "mc_kill", "mc_cluster_begin", "mc_scan",
-                     "mc_mean_shift", "mc_timers", "mc_classify_values", "mc_mean_shift_select", "mc_accumulate",
+                     "mc_mean_shift", "mc_update_iteration", "mc_timers", "mc_classify_values", "mc_mean_shift_select", "mc_accumulate",
                      "mc_scan_part", "mc_scan_commit", "mc_comm_unique_id", "mc_comm_create", "mc_comm_allgather",
                      "mc_comm_stats", "mc_comm_destroy", "mc_sync"):
             getattr(lib, name).restype = C.c_int
@@ -255,6 +255,31 @@ class Engine:
         _check(self.lib.mc_classify_values(self.ctx, _p(raw), C.c_uint64(m), _p(sim), _p(c0), _p(s)),
                "mc_classify_values")
         return sim, c0, s
+
+    def mean_shift(self, centres, member_off, members, delta):
+        centres = np.ascontiguousarray(centres, np.uint32)
+        member_off = np.ascontiguousarray(member_off, np.uint64)
+        members = np.ascontiguousarray(members, np.uint32)
+        out = np.zeros(len(centres), np.uint32)
+        _check(self.lib.mc_mean_shift(self.ctx, _p(centres), len(centres), _p(member_off), _p(members), delta, _p(out)),
+               "mc_mean_shift")
+        return out
+
+    def update_iteration(self, centres, member_off, members, delta):
+        """mc_update_iteration: (new centres, merge pairs' similar flags, their combo 0 values)."""
+        centres = np.ascontiguousarray(centres, np.uint32)
+        member_off = np.ascontiguousarray(member_off, np.uint64)
+        members = np.ascontiguousarray(members, np.uint32)
+        C_ = len(centres)
+        m = sum(min(delta, C_ - 1 - i) for i in range(C_))
+        out = np.zeros(C_, np.uint32)
+        sim = np.zeros(max(m, 1), np.uint8)
+        c0 = np.zeros(max(m, 1))
+        n = C.c_uint64(0)
+        _check(self.lib.mc_update_iteration(self.ctx, _p(centres), C_, _p(member_off), _p(members), delta, _p(out),
+                                            _p(sim), _p(c0), C.byref(n)), "mc_update_iteration")
+        assert n.value == m
+        return out, sim[:m], c0[:m]
 
     def mean_shift_select(self, centres, member_off, members, delta, keep):
         centres = np.ascontiguousarray(centres, np.uint32)

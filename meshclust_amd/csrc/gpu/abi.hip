@@ -201,7 +201,7 @@ int mc_ctx_destroy(mc_ctx *c) {
                  &c->alive, &c->members, &c->member_keys, &c->partials, &c->scan_dev, &c->flags_out, &c->s_a, &c->s_b,
                  &c->s_c, &c->s_d, &c->s_e, &c->s_f, &c->s_g, &c->s_h, &c->s_i, &c->s_j, &c->s_k, &c->hs, &c->mag_s, &c->sumsq_s, &c->len_s, &c->ticket,
                  &c->msum, &c->ident_s, &c->al_a, &c->al_b, &c->al_out, &c->acc_out, &c->sp_words, &c->sp_keys,
-                 &c->sp_scr, &c->sp_nodes, &c->sp_nn, &c->sp_q, &c->sp_err})
+                 &c->sp_scr, &c->sp_nodes, &c->sp_nn, &c->sp_q, &c->sp_err, &c->u_off, &c->u_mem})
     release(*b);
   if (c->h_scan) (void)hipHostFree(c->h_scan);
   if (c->h_stage) (void)hipHostFree(c->h_stage);
@@ -244,6 +244,10 @@ static int load_common(mc_ctx *c, const uint64_t *seq_off, uint64_t n, const int
 
 int mc_load_sequences(mc_ctx *c, const uint8_t *codes, const uint64_t *seq_off, uint64_t n, const int32_t *seg,
                       const uint64_t *seg_off) {
+  if (c) {
+    c->h_uoff.clear();
+    c->h_umem.clear();
+  }
   if (!c || !seq_off || !seg_off || (n && !codes)) return MC_ERR_ARG;
   std::vector<uint64_t> pk_off;
   TRY(load_common(c, seq_off, n, seg, seg_off, pk_off));
@@ -257,6 +261,10 @@ int mc_load_sequences(mc_ctx *c, const uint8_t *codes, const uint64_t *seq_off, 
 int mc_load_packed(mc_ctx *c, const uint32_t *packed, const uint64_t *pk_off, const uint64_t *seq_off, uint64_t n,
                    const uint64_t *exc_pos, const uint8_t *exc_val, uint64_t nexc, const int32_t *seg,
                    const uint64_t *seg_off) {
+  if (c) {
+    c->h_uoff.clear();
+    c->h_umem.clear();
+  }
   if (!c || !pk_off || !seq_off || !seg_off || (n && !packed) || (nexc && (!exc_pos || !exc_val))) return MC_ERR_ARG;
   for (uint64_t i = 0; i < n; i++)
     if (pk_off[i + 1] - pk_off[i] != (seq_off[i + 1] - seq_off[i] + 15) / 16) {
@@ -559,6 +567,22 @@ int mc_set_classifier(mc_ctx *c, const mc_classifier *cls) {
     if (ok) c->cls.layout = cls->n_single == 4 ? 3 : 4;
   }
   if (getenv("MC_CLASSIFY_GENERIC")) c->cls.layout = 0;  // diagnostics: the generic form only
+  c->fcls.on = c->cls.layout != 0 && !getenv("MC_CLASSIFY_EXACT");
+  for (int i = 0; i < MC_MAX_SINGLE; i++) {
+    c->fcls.rinv[i] = 0.0;
+    c->fcls.noff[i] = 0.0;
+    c->fcls.nsgn[i] = 1.0;
+    if (i >= cls->n_single) continue;
+    if (!cls->is_sim[i]) {
+      c->fcls.noff[i] = 1.0;
+      c->fcls.nsgn[i] = -1.0;
+    }
+    const double r = cls->maxs[i] - cls->mins[i];
+    c->fcls.rinv[i] = 1.0 / r;
+    if (i >= 2 && !(std::isfinite(r) && r != 0.0 && std::isfinite(c->fcls.rinv[i]) && c->fcls.rinv[i] != 0.0 &&
+                    std::isfinite(cls->mins[i])))
+      c->fcls.on = 0;
+  }
   c->has_cls = true;
   return MC_OK;
 }
@@ -1242,13 +1266,22 @@ int mc_update_iteration(mc_ctx *c, const uint32_t *centre_ids, uint32_t C, const
   MCG_CHECK(hipSetDevice(c->device));
   TRY(check_ids(c, centre_ids, C));
   const uint64_t nm = member_off[C];
-  TRY(check_ids(c, members, nm));
   std::vector<uint64_t> poff(C + 1, 0);
   for (uint32_t i = 0; i < C; i++) poff[i + 1] = poff[i] + std::min<uint64_t>((uint64_t)delta, C - 1 - i);
   const uint64_t m = poff[C];
   TRY(upload(c, c->s_a, centre_ids, C, c->stream));
-  TRY(upload(c, c->s_b, member_off, C + 1, c->stream));
-  TRY(upload(c, c->s_c, members, nm, c->stream));
+  const bool same = c->h_uoff.size() == (size_t)C + 1 && c->h_umem.size() == nm &&
+                    std::memcmp(c->h_uoff.data(), member_off, ((size_t)C + 1) * 8) == 0 &&
+                    (nm == 0 || std::memcmp(c->h_umem.data(), members, nm * 4) == 0);
+  if (!same) {
+    TRY(check_ids(c, members, nm));
+    c->h_uoff.clear();
+    c->h_umem.clear();
+    TRY(upload(c, c->u_off, member_off, C + 1, c->stream));
+    TRY(upload(c, c->u_mem, members, nm, c->stream));
+    c->h_uoff.assign(member_off, member_off + C + 1);
+    c->h_umem.assign(members, members + nm);
+  }
   TRY(upload(c, c->s_h, poff.data(), C + 1, c->stream));
   TRY(ensure(c->flags_out, (size_t)C * 4 + 16));
   TRY(ensure(c->s_i, m * 8 + 16));
@@ -1257,7 +1290,7 @@ int mc_update_iteration(mc_ctx *c, const uint32_t *centre_ids, uint32_t C, const
   uint32_t *d_pa = (uint32_t *)c->s_i.p, *d_pb = d_pa + m;
   double *d_c0 = (double *)c->s_j.p;
   uint8_t *d_sim = (uint8_t *)(d_c0 + m);
-  TRY(launch_mean_shift(c, (uint32_t *)c->s_a.p, C, (uint64_t *)c->s_b.p, member_off, (uint32_t *)c->s_c.p, delta,
+  TRY(launch_mean_shift(c, (uint32_t *)c->s_a.p, C, (uint64_t *)c->u_off.p, member_off, (uint32_t *)c->u_mem.p, delta,
                         nullptr, d_new, 0, C));
   if (m) {
     TRY(launch_merge_pairs(c, d_new, C, (const uint64_t *)c->s_h.p, d_pa, d_pb));

@@ -92,8 +92,28 @@ struct MInfo {
   uint64_t mag, sumsq, len, bin;  // bin: the bvec bin holding this static position
   WinTab wt;
 };
+static_assert(sizeof(MInfo) % 8 == 0, "MInfo is loaded as 8-byte words");
+constexpr int MINFO_W = (int)(sizeof(MInfo) / 8);
+
+// A position's MInfo as independent 8-byte loads (issue them all, then `minfo_take`): a struct
+// copy is split into field loads that the compiler places next to each use, one memory round
+// trip at a time when LDS stores (generic pointers) sit in between.
+__device__ __forceinline__ void minfo_issue(const MInfo *m, uint2 (&w)[MINFO_W]) {
+  const uint2 *s = reinterpret_cast<const uint2 *>(m);
+#pragma unroll
+  for (int k = 0; k < MINFO_W; k++) w[k] = s[k];
+}
+__device__ __forceinline__ MInfo minfo_take(uint2 (&w)[MINFO_W]) {
+#pragma unroll
+  for (int k = 0; k < MINFO_W; k++) asm volatile("" : "+v"(w[k].x), "+v"(w[k].y));
+  MInfo r;
+  __builtin_memcpy(&r, w, sizeof(MInfo));
+  return r;
+}
 
 struct AccArgs {
+  int dbg;     // MC_ACCUM_DBG bits (bisection aid): 1 per-member kills, 2 thread-per-member closest
+  FastCls fc;  // the workers' division-light decision (features.hpp classify_fast)
   // chunk-major static layout (scan.hip build_static)
   const uint4 *hs;
   uint64_t npad;
@@ -370,8 +390,25 @@ struct DevBvec {
   __device__ __forceinline__ void kill_one(uint64_t p) { kill_in(p, bin_of(p)); }
   __device__ __forceinline__ void kill_in(uint64_t p, uint64_t b) {  // ... when its bin b is known
     atomicAnd(&bits[p >> 5], ~(1u << (p & 31)));
-    atomicSub(&cn[b], 1u);
-    for (uint64_t i = b + 1; i <= nb; i += i & (~i + 1)) atomicSub(&fw[i], 1u);
+    count_sub(b, 1u);
+  }
+  __device__ __forceinline__ void count_sub(uint64_t b, uint32_t n) {  // n kills in bin b: counts only
+    atomicSub(&cn[b], n);
+    for (uint64_t i = b + 1; i <= nb; i += i & (~i + 1)) atomicSub(&fw[i], n);
+  }
+  // kills of a list (every thread of the workgroup; p / b valid where `act`): the bits one
+  // atomic each, the counts once per distinct bin of each wave (a step's new members share a
+  // few bins: per-member Fenwick walks were same-address LDS atomics in series)
+  __device__ __forceinline__ void kill_list(bool act, uint64_t p, uint64_t b) {
+    if (act) atomicAnd(&bits[p >> 5], ~(1u << (p & 31)));
+    uint64_t pending = __ballot(act);
+    while (pending) {
+      const int L = __builtin_ctzll(pending);
+      const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, L);
+      const uint64_t same = __ballot(act && (uint32_t)b == b0) & pending;
+      if ((int)(threadIdx.x & 63) == L) count_sub(b0, (uint32_t)__popcll(same));
+      pending &= ~same;
+    }
   }
 };
 
@@ -1099,8 +1136,9 @@ __device__ __forceinline__ void worker_dense(const AccArgs &A, const DevClassifi
       } else {
         for (int k = 0; k < nch; k++) acc.add(rr[(uint64_t)k * NT], clds[k]);
       }
-      d_t = C.layout ? classify_std(C, acc.finish(pi_t.mag, pc.mag), pi_t, pt_t, pc, tq, A.B, &cv_t)
-                     : classify_cand<T>(acc, pi_t, pc, A.B, C, &cv_t);
+      d_t = A.fc.on    ? classify_fast(C, A.fc, acc.finish(pi_t.mag, pc.mag), pi_t, pt_t, pc, tq, A.B, &cv_t)
+            : C.layout ? classify_std(C, acc.finish(pi_t.mag, pc.mag), pi_t, pt_t, pc, tq, A.B, &cv_t)
+                       : classify_cand<T>(acc, pi_t, pc, A.B, C, &cv_t);
     }
     if (A.trace && t == 0) t_scanned = now();
     if (A.trace2 && lane == 0) s_tw[wv] = now();
@@ -1393,7 +1431,9 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
       st32(A.mem_pos + cl_start, (uint32_t)pos);
       st64(A.mkeys + cl_start, 0);
       if (A.mrow) {
-        const MInfo mi = A.minfo[pos];
+        uint2 w[MINFO_W];
+        minfo_issue(A.minfo + pos, w);
+        const MInfo mi = minfo_take(w);
         mc.pos[0] = (uint32_t)pos;
         mc.key[0] = 0;
         mc.info[0] = mi.mag;
@@ -1470,19 +1510,37 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
   // (defer >= 0: the bvec kill is left to the next window -- the bin goes to s_pbin[defer])
   auto take = [&](uint64_t qm, uint32_t p, bool sums, int64_t defer = -1) {
     const uint64_t key = ((uint64_t)step << 32) | p;
+    const uint4 *hrow = A.hr + (uint64_t)p * nch;
+    // every load of the member is issued before the first store: LDS stores go through generic
+    // pointers, which the compiler does not move loads past (a load -> wait -> store per 16
+    // bytes was 21 dependent memory round trips per member, ≈2.9 us of a config-B step)
+    const bool cached = qm < A.mrow;
+    uint2 w[MINFO_W];
+    minfo_issue(A.minfo + p, w);
+    if constexpr (!WIDE && NCH > 0) {
+      if (cached) {
+        uint4 rv[NC];
+#pragma unroll
+        for (int k = 0; k < NC; k++) rv[k] = hrow[k];
+        // (the scheduler would otherwise sink each load to its store: hold them all here)
+#pragma unroll
+        for (int k = 0; k < NC; k++) asm volatile("" : "+v"(rv[k].x), "+v"(rv[k].y), "+v"(rv[k].z), "+v"(rv[k].w));
+#pragma unroll
+        for (int k = 0; k < NC; k++) mc.row[qm * mc.rp + k] = rv[k];
+      }
+    } else if (!WIDE && cached) {
+      for (int k = 0; k < nch; k++) mc.row[qm * mc.rp + k] = hrow[k];
+    }
+    const MInfo mi = minfo_take(w);
     st32(A.mem_pos + cl_start + qm, p);
     st64(A.mkeys + cl_start + qm, key);
-    const uint4 *hrow = A.hr + (uint64_t)p * nch;
-    const MInfo mi = A.minfo[p];
-    if (qm < A.mrow) {
+    if (cached) {
       mc.pos[qm] = p;
       mc.key[qm] = key;
       mc.info[qm * 3 + 0] = mi.mag;
       mc.info[qm * 3 + 1] = mi.sumsq;
       mc.info[qm * 3 + 2] = mi.len;
       mc.wt[qm] = mi.wt;
-      if (!WIDE)
-        for (int k = 0; k < nch; k++) mc.row[qm * mc.rp + k] = hrow[k];
     }
     if (WIDE ? sums : qm >= A.mrow) {
       constexpr int per = 16 / (int)sizeof(T);
@@ -1550,7 +1608,14 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
         if (A.trace2 && threadIdx.x == 0 && step < TRACE_STEPS) A.trace[(uint64_t)step * TRACE_W + 6] = now();
       }
       if (npend) {  // the last step's bvec kills, after the record is out
-        for (uint32_t i = threadIdx.x; i < npend; i += NT) bv.kill_in(s_plist[i], s_pbin[i]);
+        if (A.dbg & 1) {
+          for (uint32_t i = threadIdx.x; i < npend; i += NT) bv.kill_in(s_plist[i], s_pbin[i]);
+        } else
+        for (uint32_t i0 = 0; i0 < npend; i0 += NT) {
+          const uint32_t i = i0 + threadIdx.x;
+          const bool act = i < npend;
+          bv.kill_list(act, act ? s_plist[i] : 0, act ? s_pbin[i] : 0);
+        }
         npend = 0;
         __syncthreads();
       }
@@ -1927,6 +1992,57 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
             bq = q;
           }
         }
+      } else if (NCH > 0 && NC % 4 == 0 && sizeof(T) == 1 && !(A.dbg & 2)) {
+        // a quad of lanes per member, a quarter of the row each, SAD only (distance_d needs
+        // sum |p - F| and the magnitudes): a quarter of the dependent LDS reads per lane
+        constexpr int CPL = NC >= 4 ? NC / 4 : 1;
+        const int sub = threadIdx.x & 3;
+        for (uint64_t q = threadIdx.x >> 2; q < M; q += NT / 4) {
+          uint32_t s4[CPL];
+          if (q < A.mrow) {
+            const uint4 *row = mc.row + q * mc.rp + sub * CPL;
+            uint4 rv[CPL], fv[CPL];
+#pragma unroll
+            for (int k = 0; k < CPL; k++) {
+              rv[k] = row[k];
+              fv[k] = F4[sub * CPL + k];
+            }
+#pragma unroll
+            for (int k = 0; k < CPL; k++) {
+              s4[k] = __builtin_amdgcn_sad_u8(rv[k].x, fv[k].x, 0u);
+              s4[k] = __builtin_amdgcn_sad_u8(rv[k].y, fv[k].y, s4[k]);
+              s4[k] = __builtin_amdgcn_sad_u8(rv[k].z, fv[k].z, s4[k]);
+              s4[k] = __builtin_amdgcn_sad_u8(rv[k].w, fv[k].w, s4[k]);
+            }
+          } else {
+            const uint64_t r = ld32(A.mem_pos + cl_start + q);
+#pragma unroll
+            for (int k = 0; k < CPL; k++) {
+              const uint4 a = A.hr[r * nch + sub * CPL + k], f = F4[sub * CPL + k];
+              s4[k] = __builtin_amdgcn_sad_u8(a.x, f.x, 0u);
+              s4[k] = __builtin_amdgcn_sad_u8(a.y, f.y, s4[k]);
+              s4[k] = __builtin_amdgcn_sad_u8(a.z, f.z, s4[k]);
+              s4[k] = __builtin_amdgcn_sad_u8(a.w, f.w, s4[k]);
+            }
+          }
+          uint32_t sad = 0;
+#pragma unroll
+          for (int k = 0; k < CPL; k++) sad += s4[k];
+          sad += dpp_mv<0xB1>(0u, sad);  // quad_perm [1,0,3,2]
+          sad += dpp_mv<0x4E>(0u, sad);  // quad_perm [2,3,0,1]: every lane of the quad has the sum
+          if (sub == 0) {
+            const uint64_t mp = q < A.mrow ? mc.info[q * 3] : A.mag_s[ld32(A.mem_pos + cl_start + q)];
+            const uint64_t key = q < A.mrow ? mc.key[q] : ld64(A.mkeys + cl_start + q);
+            const uint64_t smin = (mp + sumF - sad) >> 1;
+            const double frac = (double)(2 * smin) / (double)(mp + sumF);
+            const double d = __builtin_fma(-frac, frac, 1.0) * 10000.0;
+            if (d < bd || (d == bd && key < bk)) {
+              bd = d;
+              bk = key;
+              bq = q;
+            }
+          }
+        }
       } else
       for (uint64_t q = threadIdx.x; q < M; q += NT) {
         Acc<T> acc;
@@ -2260,6 +2376,8 @@ int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, 
   A.cl_centre = d_cl_centre;
   A.cl_off = d_cl_off;
   A.out = d_out;
+  A.fc = c->fcls;
+  A.dbg = getenv("MC_ACCUM_DBG") ? atoi(getenv("MC_ACCUM_DBG")) : 0;
   A.budget = 20ull * 100000000ull;  // a single hand-off never takes 20 s: give up, report error 99
   A.W = c->mb_world > 0 ? (uint32_t)c->mb_world : 1u;
   A.rank = c->mb_world > 0 ? (uint32_t)c->mb_rank : 0u;

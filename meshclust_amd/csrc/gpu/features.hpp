@@ -342,6 +342,87 @@ __device__ __forceinline__ int classify_std(const DevClassifier &C, const PS &s,
   return sum >= C.thr;
 }
 
+// Division-light decision for the accumulation workers (the same decision and combo 0 as
+// classify_std, bit for bit).  Combo 0 (LD x INTERSECTION) is computed exactly: the first
+// maximum of get_close compares its values.  The other GLM terms are evaluated with
+// reciprocals (two Newton steps: a few ulps) and normalised by the host's RN(1/range); the
+// decision is taken from that sum only when it clears the threshold by a margin that bounds
+// the difference to the exact sum many times over (every approximate quotient is within
+// 2^-48 relative of the exact one; the margin allows 2^-40 on every term).  Otherwise, or for
+// any non-finite value, classify_std decides.
+// (two Newton steps: from any hardware estimate within 2^-14 to a few ulps)
+__device__ __forceinline__ double rcp_nr(double b) {
+  double y = __builtin_amdgcn_rcp(b);
+  y = __builtin_fma(y, __builtin_fma(-b, y, 1.0), y);
+  return __builtin_fma(y, __builtin_fma(-b, y, 1.0), y);
+}
+__device__ __forceinline__ double rsq_nr(double a) {
+  double y = __builtin_amdgcn_rsq(a);
+  const double h = 0.5 * a;
+  y = y * __builtin_fma(-h * y, y, 1.5);
+  return y * __builtin_fma(-h * y, y, 1.5);
+}
+__device__ __forceinline__ int classify_fast(const DevClassifier &C, const FastCls &F, const PS &s, const PInfo &p,
+                                             const PTerms &tp, const PInfo &q, const PTerms &tq, int B, double *c0) {
+  const mc_classifier &c = C.c;
+  const bool kul = C.layout == 4;
+  // exact: LD and INTERSECTION, normalised, and combo 0
+  double v0 = (double)(p.len > q.len ? p.len - q.len : q.len - p.len);
+  double v1 = (double)(s.smin * 2) / (double)(p.mag + q.mag);
+  {
+    const double n0 = (v0 - c.mins[0]) / (c.maxs[0] - c.mins[0]), n1 = (v1 - c.mins[1]) / (c.maxs[1] - c.mins[1]);
+    v0 = c.is_sim[0] ? n0 : 1 - n0;
+    v1 = c.is_sim[1] ? n1 : 1 - n1;
+  }
+  const double a0 = v0 * v1;
+  *c0 = a0;
+  // approximate: MANHATTAN, PEARSON (, KULCZYNSKI2)
+  double r[5], e[5], v[5];
+  r[2] = (double)(int32_t)(uint32_t)s.sabs;
+  {
+    const int64_t dot = (int64_t)s.sdot - tq.ap * (int64_t)p.mag - tp.ap * (int64_t)q.mag + (int64_t)B * tp.ap * tq.ap;
+    const double prod = (double)(int64_t)((uint64_t)tp.np * (uint64_t)tq.np);
+    const double pr = 0.5 < prod ? prod : 0.5;
+    r[3] = (double)dot * rsq_nr(pr);
+  }
+  r[4] = kul ? ((double)B * (tp.da + tq.da)) * rcp_nr((2.0 * tp.da) * tq.da) * (double)s.smin : 0.0;
+  const int nf = kul ? 5 : 4;
+#pragma unroll
+  for (int i = 2; i < 5; i++) {
+    if (i >= nf) {
+      v[i] = e[i] = 0.0;
+      continue;
+    }
+    const double n = (r[i] - c.mins[i]) * F.rinv[i];
+    v[i] = F.noff[i] + F.nsgn[i] * n;
+    // |approximate - exact| of v[i]: 2^-40 of (|raw| + |min|) / |range| + 2^-40 (|v| + 1)
+    e[i] = 0x1p-40 * ((__builtin_fabs(r[i]) + __builtin_fabs(c.mins[i])) * __builtin_fabs(F.rinv[i]) +
+                      __builtin_fabs(v[i]) + 1.0);
+  }
+  const double q00 = v0 * v0;
+  const double a1 = q00 * (v[2] * v[2]);
+  const double a2 = v[3];
+  const double a3 = q00 * (v[4] * v[4]);
+  double sum = c.weights[0];
+  sum = __builtin_fma(c.weights[1], a0, sum);
+  sum = __builtin_fma(c.weights[2], a1, sum);
+  sum = __builtin_fma(c.weights[3], a2, sum);
+  if (kul) sum = __builtin_fma(c.weights[4], a3, sum);
+  const double d1 = q00 * (2.0 * __builtin_fabs(v[2]) + e[2]) * e[2] + 0x1p-40 * __builtin_fabs(a1);
+  const double d3 = q00 * (2.0 * __builtin_fabs(v[4]) + e[4]) * e[4] + 0x1p-40 * __builtin_fabs(a3);
+  const double mag = __builtin_fabs(c.weights[0]) + __builtin_fabs(c.weights[1] * a0) + __builtin_fabs(c.weights[2] * a1) +
+                     __builtin_fabs(c.weights[3] * a2) + (kul ? __builtin_fabs(c.weights[4] * a3) : 0.0);
+  const double margin = 2.0 * (__builtin_fabs(c.weights[2]) * d1 + __builtin_fabs(c.weights[3]) * e[3] +
+                               (kul ? __builtin_fabs(c.weights[4]) * d3 : 0.0)) +
+                        0x1p-40 * mag;
+  if (__builtin_isfinite(sum) && __builtin_isfinite(margin) && __builtin_isfinite(a0)) {
+    if (sum - margin >= C.thr) return 1;
+    if (sum + margin < C.thr) return 0;
+  }
+  double cx;
+  return classify_std(C, s, p, tp, q, tq, B, &cx);
+}
+
 template <typename T>
 __device__ __forceinline__ uint4 ld16(const uint8_t *row, int ch) {
   return reinterpret_cast<const uint4 *>(row)[ch];

@@ -40,6 +40,15 @@ struct DevClassifier {
   int layout;
 };
 
+// The accumulation workers' division-light decision (features.hpp classify_fast), passed to
+// the accumulation kernel only: rinv[i] = RN(1 / (maxs[i] - mins[i])) on the host, and
+// is_sim ? n : 1 - n == noff + nsgn * n; on = 1 when the classifier has the trainer's layout
+// and every range of features 2..4 is finite and nonzero.
+struct FastCls {
+  double rinv[MC_MAX_SINGLE], noff[MC_MAX_SINGLE], nsgn[MC_MAX_SINGLE];
+  int on;
+};
+
 // Read-only view of the device histogram matrix passed to kernels by value.
 struct HistView {
   const uint8_t *hist;
@@ -104,6 +113,7 @@ struct mc_ctx {
   mcg::Buf hist, mag, sumsq, len;
   // classifier
   mcg::DevClassifier cls{};
+  mcg::FastCls fcls{};
   bool has_cls = false;
   // accumulation state
   uint64_t norder = 0;
@@ -138,6 +148,11 @@ struct mc_ctx {
   int mb_rank = 0, mb_world = 0, mb_share = 1;
   // scratch
   mcg::Buf s_a, s_b, s_c, s_d, s_e, s_f, s_g, s_h, s_i, s_j, s_k;
+  // mc_update_iteration's member lists on the device and their host shadow: re-uploaded only
+  // when a merge changed them (cleared when sequences are loaded: the ids were checked against n)
+  mcg::Buf u_off, u_mem;
+  std::vector<uint64_t> h_uoff;
+  std::vector<uint32_t> h_umem;
   std::vector<void *> pinned;
   // timers: event pairs recorded around kernels, resolved lazily after the next stream sync
   hipEvent_t ev0 = nullptr, ev1 = nullptr;

@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 if [ -z "${SKIP_PARITY:-}" ]; then
   timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_configs.py tests/test_gpu_edges.py -m gpu -x -q \
-    -k "e2e or device_accumulate or B100k or member_cache" --timeout 300 --timeout-method thread -p no:cacheprovider \
+    -k "e2e or device_accumulate or B100k or member_cache or update_iteration" --timeout 300 --timeout-method thread -p no:cacheprovider \
     > gpurun_out/accum_parity.log 2>&1 || { echo "parity rc=$?"; tail -n 30 gpurun_out/accum_parity.log; exit 1; }
   tail -n 1 gpurun_out/accum_parity.log
 fi

@@ -340,6 +340,33 @@ def test_mean_shift_select_vs_oracle(eng, a1k):
     assert list(got) == want
 
 
+def test_update_iteration_equals_separate_calls(eng, a1k):
+    """mc_update_iteration (mean shift + merge pairs in one round trip) == mc_mean_shift followed
+    by mc_classify_pairs on the new centres (ClusterFactory.cpp:740-760); twice with the same
+    member lists (the device copy is reused) and once after they change."""
+    g, recs = a1k
+    eng.set_classifier(O.classifier_from_golden(g))
+    rng = np.random.default_rng(11)
+    for it, delta in enumerate([3, 3, 2]):
+        C = 20
+        sizes = rng.integers(1, 40, size=C)
+        if it == 1:
+            sizes = prev_sizes
+        members = prev_members if it == 1 else rng.choice(len(recs), size=int(sizes.sum()), replace=False).astype(np.uint32)
+        off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
+        centres = members[off[:-1].astype(np.int64)]
+        if it == 1:
+            centres = centres[::-1].copy()
+        prev_sizes, prev_members = sizes, members
+        newc, sim, c0 = eng.update_iteration(centres, off, members, delta)
+        want = eng.mean_shift(centres, off, members, delta)
+        assert np.array_equal(newc, want)
+        pa = [want[t] for i in range(C) for t in range(i + 1, min(C - 1, i + delta) + 1)]
+        pb = [want[i] for i in range(C) for t in range(i + 1, min(C - 1, i + delta) + 1)]
+        s2, c2, _ = eng.classify_pairs(np.array(pa), np.array(pb))
+        assert np.array_equal(sim, s2) and np.array_equal(c0, c2)
+
+
 # ---------------------------------------------------------------- device-resident accumulation
 ACC_CASES = {
     "b20k": ((20000, 1000, 200, 0.03, 71), ["--id", "0.90"]),
