@@ -112,7 +112,8 @@ __device__ __forceinline__ MInfo minfo_take(uint2 (&w)[MINFO_W]) {
 }
 
 struct AccArgs {
-  int dbg;     // MC_ACCUM_DBG bits (bisection aid): 1 per-member kills, 2 thread-per-member closest
+  int dbg;     // MC_ACCUM_DBG bits (opt-in variants, both measured slower at config B): 1 per-bin
+               // aggregated bvec kills (window 3.9 -> 20.2 ms), 2 quad-per-member closest search
   FastCls fc;  // the workers' division-light decision (features.hpp classify_fast)
   // chunk-major static layout (scan.hip build_static)
   const uint4 *hs;
@@ -1608,7 +1609,7 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
         if (A.trace2 && threadIdx.x == 0 && step < TRACE_STEPS) A.trace[(uint64_t)step * TRACE_W + 6] = now();
       }
       if (npend) {  // the last step's bvec kills, after the record is out
-        if (A.dbg & 1) {
+        if (!(A.dbg & 1)) {
           for (uint32_t i = threadIdx.x; i < npend; i += NT) bv.kill_in(s_plist[i], s_pbin[i]);
         } else
         for (uint32_t i0 = 0; i0 < npend; i0 += NT) {
@@ -1992,7 +1993,7 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
             bq = q;
           }
         }
-      } else if (NCH > 0 && NC % 4 == 0 && sizeof(T) == 1 && !(A.dbg & 2)) {
+      } else if (NCH > 0 && NC % 4 == 0 && sizeof(T) == 1 && (A.dbg & 2)) {
         // a quad of lanes per member, a quarter of the row each, SAD only (distance_d needs
         // sum |p - F| and the magnitudes): a quarter of the dependent LDS reads per lane
         constexpr int CPL = NC >= 4 ? NC / 4 : 1;

@@ -108,6 +108,16 @@ def test_config_B100k_global_bitmap_equals_reference(product):
     assert st["accum_path"] == "device"
 
 
+@pytest.mark.parametrize("env,tag", [({"MC_ACCUM_DBG": "3"}, ".dbg3"), ({"MC_CLASSIFY_EXACT": "1"}, ".exact")])
+def test_config_B100k_accum_variants_equal_reference(product, env, tag):
+    """The accumulation kernel's opt-in forms (per-bin aggregated bvec kills and the
+    quad-per-member closest search, MC_ACCUM_DBG=3) and the workers' exact classifier
+    (MC_CLASSIFY_EXACT: classify_std everywhere, no division-light decision) at config B, against
+    the reference's partition."""
+    st = _big("B100k", product, 300, env=env, tag=tag)
+    assert st["accum_path"] == "device"
+
+
 @pytest.mark.parametrize("env", [{}, {"MC_ACCUM_STEPS": "1"}])
 def test_config_D100k_partition_equals_reference(product, env):
     """Config D's shape (10 reads per template, 10,000 clusters) at 100k reads: the device loop
