@@ -2247,8 +2247,9 @@ bool accum_plan(const mc_ctx *c, uint32_t nb, AccPlan *pl) {
                              : reinterpret_cast<const void *>(&accum_kernel<uint16_t, 0, false, false, true>);
     }
   }
-  // streaming rows (config D): compacted per chunk by its worker, the slot list in LDS
-  pl->compact = !pl->dense && !wide && nch == 16 && c->width == 1 && pl->res == 0 && per_w <= 64 && !getenv("MC_ACCUM_NO_COMPACT") &&
+  // streaming rows (config D): compacted per chunk by its worker, the slot list in LDS -- opt in
+  // (MC_ACCUM_COMPACT): measured slower at D1M, accumulation 1060 -> 1424 ms (profiles/r03_v10)
+  pl->compact = !pl->dense && !wide && nch == 16 && c->width == 1 && pl->res == 0 && per_w <= 64 && getenv("MC_ACCUM_COMPACT") &&
                 wfix + pl->fcap * 2 <= cap;
   if (pl->compact) pl->fn = reinterpret_cast<const void *>(&accum_kernel<uint8_t, 16, false, true>);
   // controller: mean row, column sums, bvec (+ bitmap unless global), member cache

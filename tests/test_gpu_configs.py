@@ -158,3 +158,9 @@ def test_config_D1M_properties():
     st2 = _run(fa, flags, out_steps, 900, env={"MC_ACCUM_STEPS": "1"})
     got2, _ = _partition(out_steps)
     assert BG.canonical_digest(got2) == BG.canonical_digest(got)
+    # the streaming form's opt-in per-chunk compaction of alive rows (MC_ACCUM_COMPACT)
+    out_cmp = fa[:-3] + ".compact.clstr"
+    st3 = _run(fa, flags, out_cmp, 600, env={"MC_ACCUM_COMPACT": "1"})
+    assert st3["accum_path"] == "device", st3["accum_path"]
+    got3, _ = _partition(out_cmp)
+    assert BG.canonical_digest(got3) == BG.canonical_digest(got)
