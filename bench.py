@@ -1,31 +1,38 @@
 #!/usr/bin/env python3
 """bench.py -- sequences clustered per second on MI355X (BASELINE.json metric).
 
-Workload (BASELINE.json configs[1]): 100,000 synthetic 1 kb
-reads, 1,000 templates, 3% per-base mutation, seed 41, --id 0.90 (auto k = 4, 8-bit
-histograms).  One "step" = one end-to-end run of meshclust on that FASTA, the BASELINE
-metric's unit of work (N / wall from parse to .clstr written): parse +
-encode + 2-bit pack on the host, upload, K1 histograms -> training (split sort keys, NW
-labels, GLM) -> accumulation -> 15 mean-shift + merge iterations on the GPU, .clstr written.
-The FASTA is read from the page cache (the file is generated before the timed region).  The
-rate on sequences already resident in HBM (no parse / upload / write) is reported in
-"extra" as resident_sequences_per_s.
+Workloads (synthetic reads from meshclust_amd.synth, generated before the
+timed region and read from the page cache):
 
-With --gpus N > 1 (torch.distributed, one rank per GPU) the ranks share ONE clustering of
-BASELINE.json configs[3] (config D: 1,000,000 reads x 1 kb, 10,000 templates, seed 51,
---id 0.90), sharded by record (strong scaling): every rank's persistent accumulation kernel
-scans only its interleaved tiles of each get_close window and the kernels exchange each step's
-{first maximum, flagged reads} through a host-memory mailbox they all map (no host round trip
-per step); every mean-shift iteration is split by centre and the new centres all-gathered over
-RCCL.  --mode replicas instead gives every rank its own config-B batch (seed 41 + rank: weak
-scaling, no collective on the data path); --mode shard at N = 1 runs the sharded code path on
-one rank.
+* ``--workload B`` (default; BASELINE.json configs[1]): 100,000 reads x 1 kb, 1,000
+  templates, 3% per-base mutation, seed 41, ``--id 0.90`` (auto k = 4, 8-bit histograms);
+* ``--workload D`` (configs[3]): 1,000,000 reads x 1 kb, 10,000 templates, seed 51.
+
+One "step" = one end-to-end run of meshclust on that FASTA (N / wall from
+parse to .clstr written): parse + encode + 2-bit pack on the host, upload, K1 histograms ->
+training (split sort keys, NW labels, GLM) -> accumulation -> 15 mean-shift + merge
+iterations on the GPU, .clstr written.  The rate on sequences already resident in HBM (no
+parse / upload / write) is reported in "extra" as resident_sequences_per_s.
+
+GPUs.  ``--gpus N`` runs N ranks, one process per GPU: launched by the driver through
+torch.distributed.run, or -- when WORLD_SIZE is not set -- spawned here as N child processes
+(torch.distributed.run, 127.0.0.1) before anything touches a GPU; rank 0 prints the line.
+The N ranks share ONE clustering of the same workload at every N, sharded by record (strong
+scaling): every rank's persistent accumulation kernel scans its interleaved tiles of each
+get_close window and the kernels exchange each step's {first maximum, flagged reads} through a
+host-memory mailbox they all map (no host round trip per step); the training's pivots and label
+alignments and every mean-shift iteration are split over the ranks and all-gathered (RCCL, the
+centre reassignment).  ``--mode replicas`` instead gives every rank its own batch (seed +
+rank: weak scaling, no collective on the data path); ``--mode shard`` at N = 1 runs the
+sharded code path on one rank.  MC_BENCH_ONE_GPU=1 (rehearsal on a one-GPU box): every rank
+on GPU 0, each kernel on its share of the CUs, gloo for the host-side all-gathers.
 
 Prints ONE JSON line on rank 0.
 """
 import argparse
 import json
 import os
+import socket
 import subprocess
 import sys
 import tempfile
@@ -35,6 +42,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+WORKLOADS = {  # reads, templates, seed (length 1 kb, mutation 0.03)
+    "B": (100000, 1000, 41),
+    "D": (1000000, 10000, 51),
+}
 
 
 def ensure_fasta(n, length, templates, mut, seed):
@@ -96,13 +107,37 @@ def cpu_baseline(fasta, args, n_reads, threads, repeats, limit_s=600):
             "cpu_model": cpu_model(), "host_cpus": os.cpu_count(), "threads": threads}
 
 
+def spawn_ranks(n):
+    """--gpus N without a launcher: N child processes through torch.distributed.run (each
+    child sees WORLD_SIZE and runs one rank); this process never touches a GPU and exits with
+    the launcher's status."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
+
+
+def kernel_pmc(kname):
+    """The FETCH_SIZE / WRITE_SIZE passes of a kernel (rocprofv3 --pmc, separate passes,
+    scripts/pmc_summary.py): HBM bytes per launch, FETCH doubled per the gfx950 note."""
+    pmc = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    if not os.path.exists(pmc):
+        return None
+    e = next((v for k, v in sorted(json.load(open(pmc)).items()) if k.startswith(kname)), None)
+    return round(e["hbm_bytes_per_dispatch"]) if e and "hbm_bytes_per_dispatch" in e else None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="B",
+                    help="B: 100k x 1 kb (BASELINE configs[1]); D: 1M x 1 kb (configs[3])")
     ap.add_argument("--mode", choices=["auto", "shard", "replicas"], default="auto",
-                    help="auto: one GPU -> config B, several -> config D shared by the ranks")
+                    help="auto: one clustering (sharded by record over the ranks when N > 1)")
     ap.add_argument("--n", type=int, default=None)
     ap.add_argument("--len", type=int, default=1000)
     ap.add_argument("--templates", type=int, default=None)
@@ -112,16 +147,20 @@ def main():
     ap.add_argument("--cpu-repeats", type=int, default=3, help="reference runs (median)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--stats-out", default=None)
+    ap.add_argument("--keep-clstr", default=None, help="rank 0 keeps the last timed step's .clstr here")
     a = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(spawn_ranks(a.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    shard = a.mode == "shard" or (a.mode == "auto" and world > 1)
-    cfg_d = shard and a.n is None  # the sharded workload: config D unless a size is given
-    a.n = a.n if a.n is not None else (1000000 if cfg_d else 100000)
-    a.templates = a.templates if a.templates is not None else (10000 if cfg_d else 1000)
-    a.seed = a.seed if a.seed is not None else (51 if cfg_d else 41)
+    mode = "replicas" if a.mode == "replicas" else "shard" if (a.mode == "shard" or world > 1) else "single"
+    shard = mode == "shard"
+    n0, t0_, s0_ = WORKLOADS[a.workload]
+    a.n = a.n if a.n is not None else n0
+    a.templates = a.templates if a.templates is not None else t0_
+    a.seed = a.seed if a.seed is not None else s0_
     dist = None
     if world > 1 or shard:
         import torch.distributed as dist  # noqa: F811
@@ -135,14 +174,13 @@ def main():
     M.tune_host_heap()  # this process runs many clusterings: keep large freed blocks
     if shard and world == 1:
         os.environ["MC_SHARD_FORCE"] = "1"  # the sharded code path with one rank
-    if shard and rank == 0:  # one shared input: rank 0 writes it, the others wait
+    replicas = mode == "replicas"
+    if rank == 0:  # one shared input (rank 0 writes it, the others wait), or rank 0's replica
         ensure_fasta(a.n, a.len, a.templates, a.mut, a.seed)
     if dist:
         dist.barrier()
-    fasta = ensure_fasta(a.n, a.len, a.templates, a.mut, a.seed + (0 if shard else rank))
+    fasta = ensure_fasta(a.n, a.len, a.templates, a.mut, a.seed + (rank if replicas else 0))
     threads = min(16, host_threads())
-    # MC_BENCH_ONE_GPU=1 (rehearsal on a one-GPU box): every rank on GPU 0, the ranks' kernels
-    # splitting its CUs, gloo for the host-side all-gathers (RCCL takes one rank per GPU)
     one_gpu = os.environ.get("MC_BENCH_ONE_GPU") == "1"
     if one_gpu:
         local = 0
@@ -158,6 +196,7 @@ def main():
     sync = eng.sync  # hipDeviceSynchronize on this rank's GPU
     out_dir = tempfile.mkdtemp(prefix="mc_bench_out")
     nstep = [0]
+    last_clstr = [None]
 
     def one_step():
         """parse -> upload -> GPU pipeline -> .clstr written (the BASELINE metric's work).
@@ -166,6 +205,7 @@ def main():
         4 MB); the files are removed after the timed region."""
         nstep[0] += 1
         clstr = os.path.join(out_dir, "bench_rank%d_%d.clstr" % (rank, nstep[0]))
+        last_clstr[0] = clstr
         t = time.perf_counter()
         ds = M.Dataset([fasta], threads=threads)
         t1 = time.perf_counter()
@@ -218,11 +258,11 @@ def main():
             dist.destroy_process_group()
         return
     s0 = stats[-1]
-    n_total = a.n * a.steps * (1 if shard else world)
+    n_total = a.n * a.steps * (world if replicas else 1)
     value = n_total / elapsed
     ms_step = elapsed / a.steps * 1000.0
 
-    # roofline of the dominant kernel family
+    # roofline of the dominant kernel (accumulation), and of the other HBM kernels
     fam_ms = {f: v[0] for f, v in tim.items()}
     fam_n = {f: v[1] for f, v in tim.items()}
     B = 4 ** s0["k"]
@@ -246,30 +286,57 @@ def main():
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
                 "bytes_per_eval": eval_bytes, "evals_per_launch": round(scan_evals / fam_n["scan"], 1),
                 "avg_launch_us": round(avg_s * 1e6, 2),
-                "us_per_step": round(fam_ms["scan"] * 1e3 / sum(s["scan_steps"] for s in stats), 2)}
-        pmc = os.path.join(ROOT, "profiles", "pmc_latest.json")
-        if os.path.exists(pmc) and not shard:  # (counters of the config-B launch)  # rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (scripts/pmc_summary.py)
-            e = next((v for k2, v in sorted(json.load(open(pmc)).items()) if k2.startswith(kname)), None)
-            if e and "hbm_bytes_per_dispatch" in e:
-                roof["traffic"] = round(e["hbm_bytes_per_dispatch"])
+                "us_per_step": round(fam_ms["scan"] * 1e3 / sum(s["scan_steps"] for s in stats), 2),
+                "note": "priced against HBM by algorithmic bytes (SURVEY.md §8(d)); the rows stay in LDS, "
+                        "so the kernel is bound by its dependent step chain, not by HBM (DESIGN.md §3.1)"}
+        if a.workload == "B" and not shard and world == 1:  # (the counters are of the config-B launch)
+            tr = kernel_pmc(kname)
+            if tr is not None:
+                roof["traffic"] = tr
                 roof["traffic_unit"] = "bytes/launch (FETCH_SIZE x2 + WRITE_SIZE, profiles/pmc_latest.json)"
                 roof["algorithmic_bytes_per_launch"] = round(per_launch_bytes)
+    # K1 and the mean-shift update, the other two HBM-class kernels north_star names
+    # (K1: ceil(L/4) packed bytes in + B*w row + 8 magnitude out per read; mean shift: one read
+    # of each neighbourhood member's row and magnitudes per centre, update_evals of them)
+    others = {}
+    if fam_n["kmer"]:
+        kb = a.n * (a.len / 4.0 + B * width + 8) * a.steps / fam_n["kmer"]
+        ks = fam_ms["kmer"] / fam_n["kmer"] / 1e3
+        others["kmer_kernel"] = {"bound": "hbm", "bytes_per_read": a.len / 4.0 + B * width + 8,
+                                 "algorithmic_bytes_per_launch": round(kb), "avg_launch_us": round(ks * 1e6, 2),
+                                 "achieved": round(kb / ks / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                 "frac": round(kb / ks / 1e9 / HBM_PEAK_GBS, 4),
+                                 "traffic": kernel_pmc("kmer_kernel<unsigned char") if width == 1 else None}
+    if fam_n["mean_shift"]:
+        mb = sum(s["update_evals"] for s in stats) * (B * width + 16) / fam_n["mean_shift"] / (world if shard else 1)
+        ms = fam_ms["mean_shift"] / fam_n["mean_shift"] / 1e3
+        others["mean_shift_kernel"] = {"bound": "hbm", "bytes_per_member": B * width + 16,
+                                       "algorithmic_bytes_per_launch": round(mb), "avg_launch_us": round(ms * 1e6, 2),
+                                       "achieved": round(mb / ms / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                       "frac": round(mb / ms / 1e9 / HBM_PEAK_GBS, 4),
+                                       "traffic": kernel_pmc("mean_shift_kernel<unsigned char") if width == 1 else None}
     nw_cells = sum(s["nw_cells"] for s in stats)
     nw_rate = nw_cells / (fam_ms["nw"] / 1e3) if fam_ms["nw"] else None
-    # NW is VALU-bound: 26.5 VALU instructions per cell in the throughput form;
-    # a wave64 VALU instruction holds its SIMD 4 cycles (MI355X_MICROARCH.md issue costs), so
-    # the int32 issue peak is 256 CU x 4 SIMD x 16 lanes/clk x 2.4 GHz = 39.3e12 lane-ops/s
-    # (SQ_INSTS_VALU agrees: profiles/r03_v4/config_c.json, 0.98 of it in the throughput form)
-    nw_peak = 256 * 4 * 16 * 2.4e9 / 26.5
+    # NW is VALU-bound: the peak is the int32 VALU issue rate (lane-instructions
+    # per second, from the microbenchmark in profiles/) over the VALU instructions per cell that
+    # the SQ_INSTS_VALU counter gives for the current kernels (profiles/nw_counters.json)
+    nwc_path = os.path.join(ROOT, "profiles", "nw_counters.json")
+    nwc = json.load(open(nwc_path)) if os.path.exists(nwc_path) else {}
+    lane_ops = nwc.get("valu_lane_ops_per_s", 256 * 4 * 16 * 2.4e9)
+    ipc = nwc.get("lane_insts_per_cell", 20.0)
+    nw_peak = lane_ops / ipc
     nw_roof = {"bound": "valu", "achieved": nw_rate, "peak": nw_peak, "unit": "cells/s",
                "frac": round(nw_rate / nw_peak, 4) if nw_rate else None,
+               "lane_insts_per_cell": ipc, "valu_lane_ops_per_s": lane_ops,
                "cells_per_step": nw_cells / a.steps, "ms_per_step": round(fam_ms["nw"] / a.steps, 3)}
-    nwc = os.path.join(ROOT, "profiles", "nw_counters.json")
-    if os.path.exists(nwc):  # rocprofv3 SQ counter pass on the NW kernels (scripts/prof_summary.py)
-        nw_roof["counters"] = json.load(open(nwc))
+    if nwc:
+        nw_roof["counters"] = nwc
     cpu = None
-    if not a.no_cpu_baseline and world == 1 and not shard:  # the reference: rank 0 at N = 1 only
+    if not a.no_cpu_baseline and world == 1 and mode == "single" and a.workload == "B":
+        # the reference: rank 0 at N = 1 only, on the full config-B FASTA (~27 s a run)
         cpu = cpu_baseline(fasta, ["--id", a.id], a.n, host_threads(), a.cpu_repeats)
+    wl = "config %s: %dk synthetic 1kb reads (%d templates), --id %s k-mer mean-shift" % (
+        a.workload, a.n // 1000, a.templates, a.id)
     line = {
         "metric": "sequences clustered/sec (+ NW cell-updates/sec) at 1/2/4/8 MI355X",
         "value": round(value, 1),
@@ -279,22 +346,23 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": round(ms_step, 2),
         "higher_is_better": True,
-        "scaling": "strong" if shard else "weak",
+        "scaling": "weak" if replicas else "strong",
         "vs_baseline": None,
-        "dtype": "u8",
+        "dtype": "u8" if width == 1 else "u%d" % (8 * width),
         "data": "synthetic (meshclust_amd.synth: %d reads x %d bp, %d templates, mut %.2f, seed %d%s)"
-                % (a.n, a.len, a.templates, a.mut, a.seed, "" if shard else "+rank"),
-        "config": {"workload": ("config D: %dk synthetic 1kb reads (%d templates), --id %s k-mer mean-shift, "
-                                "one clustering shared by %d GPU(s)" % (a.n // 1000, a.templates, a.id, world)) if shard
-                   else "config B: %dk synthetic 1kb reads, --id %s k-mer mean-shift" % (a.n // 1000, a.id),
-                   "reads": a.n if shard else a.n * world, "read_len": a.len, "k": s0["k"], "histogram_bits": 8 * width,
+                % (a.n, a.len, a.templates, a.mut, a.seed, "+rank" if replicas else ""),
+        "config": {"workload": wl + (", one clustering sharded by record over %d GPU(s)" % world if shard else
+                                     ", %d independent replica(s)" % world if replicas else ", one GPU"),
+                   "workload_config": a.workload, "mode": mode,
+                   "reads": a.n * (world if replicas else 1), "read_len": a.len, "k": s0["k"],
+                   "histogram_bits": 8 * width,
                    "parallelism": ("one clustering sharded by record x%d (device mailbox exchange per get_close "
                                    "step, RCCL all-gather per mean-shift iteration)" % world) if shard
-                   else "replicas x%d" % world},
+                   else "replicas x%d" % world if replicas else "single GPU"},
         "roofline": roof,
         "cpu_baseline": cpu,
-        "extra": {"nw_cell_updates_per_s": nw_rate, "nw_roofline": nw_roof, "clusters": s0["clusters"],
-                  "dominant_family": dominant,
+        "extra": {"nw_cell_updates_per_s": nw_rate, "nw_roofline": nw_roof, "kernel_rooflines": others,
+                  "clusters": s0["clusters"], "dominant_family": dominant,
                   "resident_sequences_per_s": round(a.n / min(res_t), 1),
                   "resident_ms_per_run": [round(x * 1e3, 2) for x in res_t],
                   "step_split_ms": {"parse": round(1e3 * sum(s["parse_s"] for s in stats) / a.steps, 2),
@@ -307,12 +375,18 @@ def main():
                   "device_ms_per_step": {f: round(v / a.steps, 3) for f, v in fam_ms.items()},
                   "launches_per_step": {f: round(v / a.steps, 1) for f, v in fam_n.items()},
                   "host_phases_ms": s0["phases_ms"], "accum_path": s0.get("accum_path"),
-                  "warmup_s": round(first_s, 3), "scan_steps": s0["scan_steps"]},
+                  "warmup_s": round(first_s, 3), "scan_steps": s0["scan_steps"],
+                  "rehearsal_one_gpu": one_gpu},
     }
+    if cpu is None and world == 1 and a.workload != "B":
+        line["extra"]["cpu_baseline_note"] = "the reference is timed on config B only (config D takes it hours)"
     print(json.dumps(line), flush=True)
     if a.stats_out:
         with open(a.stats_out, "w") as f:
             json.dump({"line": line, "stats": stats, "timers": tim}, f, indent=1)
+    if a.keep_clstr and last_clstr[0]:
+        import shutil
+        shutil.copyfile(last_clstr[0], a.keep_clstr)
     if comm is not None:
         comm.close()
     eng.close()

@@ -34,6 +34,7 @@ extern "C" {
 #define MC_ERR_OOM 4     /* device allocation failed                              */
 #define MC_ERR_INPUT 5   /* input the reference would reject (bad nucleotide ...) */
 #define MC_ERR_UNSUPPORTED 6 /* this device path cannot take the request; use the step API  */
+#define MC_ERR_TIMEOUT 7 /* a persistent kernel's hand-off deadline expired (a peer never answered) */
 
 /* Feature flags and combo kinds: identical values to src/cluster/src/Feature.h:9-22. */
 #define MC_FEAT_ALIGN (1 << 0)
@@ -263,7 +264,7 @@ int mc_accumulate(mc_ctx *ctx, const uint32_t *bin_lo, const uint64_t *bounds, u
  * per step the kernels exchange {first maximum of combo 0, flagged positions} through the
  * mailbox without the host, and every rank applies the same remove_available + get_mean, so
  * every rank returns the same partition as a single-rank run.  A rank that fails stops the
- * others after the exchange's deadline (MC_ERR_HIP).  world 0 detaches.
+ * others after the exchange's deadline (MC_ERR_TIMEOUT).  world 0 detaches.
  */
 uint64_t mc_mailbox_bytes(int world, uint64_t n);
 /* share: how many ranks' kernels run on this rank's GPU (>= 1; each then takes that share of
@@ -271,6 +272,17 @@ uint64_t mc_mailbox_bytes(int world, uint64_t n);
 int mc_set_mailbox(mc_ctx *ctx, void *host, uint64_t bytes, int rank, int world, int share);
 /* the PCI bus id of the context's GPU (ranks sharing a GPU find each other with it) */
 int mc_ctx_pci_bus_id(mc_ctx *ctx, char *buf, int len);
+/*
+ * The accumulation kernel's plan for this context and bvec (call after mc_set_order and
+ * mc_set_mailbox): info[0] workgroups, info[1] static positions per tile of ownership (every
+ * rank sharing a mailbox must use the same tile: tile t belongs to rank t mod world), info[2]
+ * flags {1 dense resident workers, 2 wide rows, 4 resident rows, 8 streaming rows}, info[3]
+ * the dynamic LDS bytes.  MC_ERR_UNSUPPORTED when mc_accumulate would not take it.
+ * mc_set_accum_grid caps the workgroups (0: one per CU, or the CU share of the ranks on this
+ * GPU): ranks sharing a mailbox take the smallest grid among them, so each derives the same plan.
+ */
+int mc_accum_plan_info(mc_ctx *ctx, uint32_t nbins, uint32_t info[4]);
+int mc_set_accum_grid(mc_ctx *ctx, uint32_t grid);
 
 /*
  * One mean-shift iteration over all centres (the omp parallel for of ClusterFactory.cpp:
@@ -355,7 +367,9 @@ int mc_comm_destroy(mc_comm *comm, int abort);
 /* Wait for all work on the context's GPU (every stream; benchmark boundaries). */
 int mc_sync(mc_ctx *ctx);
 
-/* Device time (ms) accumulated per kernel family since the last reset (diagnostics). */
+/* Device time (ms) and launches accumulated per kernel family since the last reset
+   (diagnostics): ms_out[2f], ms_out[2f+1] for f = k-mer, keys, pairs, scan, finalize,
+   mean shift, NW, static layout. */
 int mc_timers(mc_ctx *ctx, double *ms_out, int n, int reset);
 
 #ifdef __cplusplus

@@ -27,7 +27,7 @@ HEADER = os.path.join(ROOT, "include", "meshclust_amd.h")
 FEAT_ALIGN, FEAT_LD, FEAT_MANHATTAN = 1, 2, 4
 FEAT_INTERSECTION, FEAT_PEARSON, FEAT_KULCZYNSKI2 = 16, 32, 1024
 COMBO_SQUARED, COMBO_SELF = 1, 2
-FAMILIES = ("kmer", "keys", "pairs", "scan", "finalize", "mean_shift", "nw")
+FAMILIES = ("kmer", "keys", "pairs", "scan", "finalize", "mean_shift", "nw", "layout")
 
 
 class MCError(RuntimeError):

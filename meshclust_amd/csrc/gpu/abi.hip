@@ -958,6 +958,7 @@ static void mailbox_detach(mc_ctx *c) {
   c->mb_bytes = 0;
   c->mb_rank = c->mb_world = 0;
   c->mb_share = 1;
+  c->acc_grid = 0;
 }
 
 uint64_t mc_mailbox_bytes(int world, uint64_t n) {
@@ -1006,6 +1007,22 @@ int mc_set_mailbox(mc_ctx *c, void *host, uint64_t bytes, int rank, int world, i
   return MC_OK;
 }
 
+int mc_accum_plan_info(mc_ctx *c, uint32_t nbins, uint32_t info[4]) {
+  if (!c || !info || nbins == 0) return MC_ERR_ARG;
+  if (!c->has_cls || c->norder == 0) return MC_ERR_STATE;
+  if (!fused(c) || !accum_plan_info(c, nbins, info)) {
+    set_error("device-resident accumulation does not take this configuration");
+    return MC_ERR_UNSUPPORTED;
+  }
+  return MC_OK;
+}
+
+int mc_set_accum_grid(mc_ctx *c, uint32_t grid) {
+  if (!c) return MC_ERR_ARG;
+  c->acc_grid = grid;
+  return MC_OK;
+}
+
 int mc_accumulate(mc_ctx *c, const uint32_t *bin_lo, const uint64_t *bounds, uint32_t nbins, double sim,
                   uint32_t *centre_ids, uint64_t *member_off, uint32_t *member_ids, uint64_t *nclusters,
                   uint64_t *stats) {
@@ -1042,7 +1059,7 @@ int mc_accumulate(mc_ctx *c, const uint32_t *bin_lo, const uint64_t *bounds, uin
     set_error(out[3] == 99 ? "device accumulation: hand-off timed out"
               : out[3] == 11 ? "bvec_iterator dereference out of range (the reference throws here)"
                              : "tried incrementing null iterator (the reference throws here)");
-    return out[3] == 99 ? MC_ERR_HIP : MC_ERR_INPUT;
+    return out[3] == 99 ? MC_ERR_TIMEOUT : MC_ERR_INPUT;
   }
   const uint64_t ncl = out[0], nmem = out[4];
   if (ncl > n || nmem != n) {

@@ -2195,6 +2195,9 @@ uint32_t accum_grid(const mc_ctx *c) {
   // MC_ACCUM_GRID (tests): fewer workgroups, e.g. two ranks' kernels sharing one GPU
   if (const char *g = getenv("MC_ACCUM_GRID")) cus = std::min(cus, atoi(g));
   if (c->mb_world > 0 && c->mb_share > 1) cus /= c->mb_share;  // ranks sharing this GPU
+  // mc_set_accum_grid: ranks sharing a mailbox run the smallest grid among them, so that every
+  // rank derives the same tile of ownership from it (accum_plan's dense test depends on G)
+  if (c->acc_grid > 0) cus = std::min<int>(cus, (int)c->acc_grid);
   uint32_t G = (uint32_t)cus / 8 * 8;
   if (G > GMAX) G = GMAX;
   if (G < 8) G = 8;
@@ -2285,6 +2288,17 @@ uint64_t mailbox_slot_granules(uint32_t world, uint64_t n) {
 bool accum_supported(const mc_ctx *c, uint32_t nb) {
   AccPlan pl;
   return accum_plan(c, nb, &pl);
+}
+
+bool accum_plan_info(const mc_ctx *c, uint32_t nb, uint32_t info[4]) {
+  AccPlan pl;
+  if (!accum_plan(c, nb, &pl)) return false;
+  info[0] = pl.G;
+  info[1] = pl.dense ? (uint32_t)DT : pl.wide ? (uint32_t)NW : (uint32_t)NT;  // the kernel's TSZ
+  info[2] = (pl.dense ? 1u : 0u) | (pl.wide ? 2u : 0u) | (pl.res > 0 ? 4u : 0u) |
+            (!pl.dense && !pl.wide && pl.res == 0 ? 8u : 0u);
+  info[3] = (uint32_t)pl.lds;
+  return true;
 }
 
 int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, uint32_t nb, double sim,

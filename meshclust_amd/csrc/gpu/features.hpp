@@ -505,12 +505,12 @@ __device__ __forceinline__ void add_rows(const RowRef &R, const uint32_t *rows, 
 // up over all M rows in registers (a wave reads 64 consecutive chunks of one row: 1 KiB
 // contiguous), then stores its bins -- no atomics, which at B = 4,096 bins would be M x 4,096
 // per workgroup.  Overwrites sum[0..B).
-template <typename T, int NTH>
-__device__ __forceinline__ void add_rows_owned(const RowRef &R, const uint32_t *rows, uint32_t M, int nch, int B,
-                                               uint64_t *sum) {
+template <typename T, int NTH, typename S>
+__device__ __forceinline__ void add_rows_owned_as(const RowRef &R, const uint32_t *rows, uint32_t M, int nch, int B,
+                                                  uint64_t *sum) {
   constexpr int per = 16 / (int)sizeof(T);
   for (int c = threadIdx.x; c < nch; c += NTH) {
-    uint32_t acc[per];
+    S acc[per];
 #pragma unroll
     for (int e = 0; e < per; e++) acc[e] = 0;
     uint32_t q = 0;
@@ -520,7 +520,7 @@ __device__ __forceinline__ void add_rows_owned(const RowRef &R, const uint32_t *
       const T *p0 = reinterpret_cast<const T *>(&v0), *p1 = reinterpret_cast<const T *>(&v1),
               *p2 = reinterpret_cast<const T *>(&v2), *p3 = reinterpret_cast<const T *>(&v3);
 #pragma unroll
-      for (int e = 0; e < per; e++) acc[e] += (uint32_t)p0[e] + (uint32_t)p1[e] + (uint32_t)p2[e] + (uint32_t)p3[e];
+      for (int e = 0; e < per; e++) acc[e] += (S)p0[e] + (S)p1[e] + (S)p2[e] + (S)p3[e];
     }
     for (; q < M; q++) {
       const uint4 v = R.chunk(rows[q], c);
@@ -532,6 +532,15 @@ __device__ __forceinline__ void add_rows_owned(const RowRef &R, const uint32_t *
     for (int e = 0; e < per; e++)
       if (c * per + e < B) sum[c * per + e] = acc[e];
   }
+}
+// 32-bit accumulators while M rows of T cannot carry a bin past 2^32 (every 8-bit input below
+// 16.8M members; 16-bit rows up to 65,537 members), 64-bit beyond
+template <typename T, int NTH>
+__device__ __forceinline__ void add_rows_owned(const RowRef &R, const uint32_t *rows, uint32_t M, int nch, int B,
+                                               uint64_t *sum) {
+  constexpr uint64_t tmax = sizeof(T) == 1 ? 0xffull : sizeof(T) == 2 ? 0xffffull : 0xffffffffull;
+  if ((uint64_t)M * tmax <= 0xffffffffull) add_rows_owned_as<T, NTH, uint32_t>(R, rows, M, nch, B, sum);
+  else add_rows_owned_as<T, NTH, uint64_t>(R, rows, M, nch, B, sum);
 }
 
 // One workgroup.  rows[q] (q < M) are row indices into R with magnitudes mags[rows[q]];

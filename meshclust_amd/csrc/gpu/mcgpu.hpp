@@ -27,7 +27,8 @@ namespace mcg {
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); }
 
 // Kernel families for the device timers (mc_timers): ms and launch count per family.
-enum Family { F_KMER = 0, F_KEYS, F_PAIRS, F_SCAN, F_FINAL, F_MSHIFT, F_NW, F_NFAM };
+// F_LAYOUT: the static bvec-order copies of the rows (build_static), after K1
+enum Family { F_KMER = 0, F_KEYS, F_PAIRS, F_SCAN, F_FINAL, F_MSHIFT, F_NW, F_LAYOUT, F_NFAM };
 
 // Classifier in the form the kernels consume (mc_classifier + the exact decision threshold).
 struct DevClassifier {
@@ -146,6 +147,7 @@ struct mc_ctx {
   void *mb_host = nullptr, *mb_dev = nullptr;
   uint64_t mb_bytes = 0;
   int mb_rank = 0, mb_world = 0, mb_share = 1;
+  uint32_t acc_grid = 0;  // mc_set_accum_grid: cap on the accumulation kernel's workgroups (0: none)
   // scratch
   mcg::Buf s_a, s_b, s_c, s_d, s_e, s_f, s_g, s_h, s_i, s_j, s_k;
   // mc_update_iteration's member lists on the device and their host shadow: re-uploaded only
@@ -199,6 +201,7 @@ int launch_mean_shift(mc_ctx *c, const uint32_t *d_cid, uint32_t C, const uint64
                       uint32_t j1);
 int build_static(mc_ctx *c);
 bool accum_supported(const mc_ctx *c, uint32_t nb);
+bool accum_plan_info(const mc_ctx *c, uint32_t nb, uint32_t info[4]);
 uint64_t mailbox_slot_granules(uint32_t world, uint64_t n);  // mailbox granules per rank slot
 int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, uint32_t nb, double sim,
                  uint32_t *d_mem_pos, uint64_t *d_mkeys, uint32_t *d_cl_centre, uint64_t *d_cl_off, uint64_t *d_out);

@@ -368,7 +368,7 @@ int build_static(mc_ctx *c) {
       break;
   }
   MCG_CHECK(hipGetLastError());
-  timed_end(c, F_KMER);
+  timed_end(c, F_LAYOUT);
   return MC_OK;
 }
 

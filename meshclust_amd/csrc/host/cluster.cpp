@@ -223,11 +223,12 @@ struct SharedMailbox {
   }
 };
 
-static bool attach_mailbox(const ShardComm &comm, mc_ctx *ctx, uint64_t n, SharedMailbox &mb) {
+static bool attach_mailbox(const ShardComm &comm, mc_ctx *ctx, uint64_t n, uint32_t nbins, SharedMailbox &mb) {
   struct Blk {
     char name[56];
-    int32_t ok, pad;
-    char pci[64];  // this rank's GPU: ranks on one GPU split its CUs
+    int32_t ok;
+    uint32_t grid;  // this rank's accumulation grid (then: its plan's tile of ownership)
+    char pci[64];   // this rank's GPU: ranks on one GPU split its CUs
   };
   static_assert(sizeof(Blk) == 128, "mailbox exchange block");
   const int W = comm.world;
@@ -256,12 +257,29 @@ static bool attach_mailbox(const ShardComm &comm, mc_ctx *ctx, uint64_t n, Share
   if (fd >= 0) close(fd);
   int share = 0;
   for (const auto &b : all) share += strncmp(b.pci, mine.pci, sizeof mine.pci) == 0;
-  if (mb.p && mc_set_mailbox(ctx, mb.p, bytes, comm.rank, W, std::max(share, 1)) == MC_OK) mb.ctx = ctx;
+  uint32_t info[4] = {0, 0, 0, 0};
+  if (mb.p && mc_set_mailbox(ctx, mb.p, bytes, comm.rank, W, std::max(share, 1)) == MC_OK &&
+      mc_accum_plan_info(ctx, nbins, info) == MC_OK)
+    mb.ctx = ctx;
   mine.ok = mb.ctx != nullptr;
+  mine.grid = info[0];
   if (comm.allgather(comm.user, &mine, sizeof mine, all.data()) != 0)
     throw PeerError("mailbox all-gather across ranks failed");
   if (comm.rank == 0 && all[0].name[0]) shm_unlink(all[0].name);  // every rank has mapped it (or failed)
   for (const auto &b : all) ok &= b.ok != 0;
+  // Tile t of the static order belongs to rank t mod W, so every rank must deal tiles of the
+  // same size -- which the plan derives from the grid (the dense form needs a worker's share
+  // to fit one workgroup).  Every rank takes the smallest grid among the ranks, and the ranks
+  // compare the resulting tiles; any disagreement (e.g. an MC_ACCUM_* override on one rank
+  // only) sends all of them to the host-driven sharded steps.
+  if (ok) {
+    uint32_t gmin = ~0u;
+    for (const auto &b : all) gmin = std::min(gmin, b.grid);
+    mine.grid = (mc_set_accum_grid(ctx, gmin) == MC_OK && mc_accum_plan_info(ctx, nbins, info) == MC_OK) ? info[1] : 0;
+    if (comm.allgather(comm.user, &mine, sizeof mine, all.data()) != 0)
+      throw PeerError("mailbox all-gather across ranks failed");
+    for (const auto &b : all) ok &= b.grid != 0 && b.grid == all[0].grid;
+  }
   if (!ok && mb.ctx) {
     mc_set_mailbox(ctx, nullptr, 0, 0, 0, 1);
     mb.ctx = nullptr;
@@ -395,7 +413,7 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
   fault_point(cfg.comm, "accumulate");
   SharedMailbox mbox;
   const bool dev_shard = shard && !getenv("MC_SHARD_HOST_STEPS") && !getenv("MC_ACCUM_STEPS") &&
-                         attach_mailbox(*shard, ctx, order.size(), mbox);
+                         attach_mailbox(*shard, ctx, order.size(), (uint32_t)bv.bins().size(), mbox);
   // The device-resident loop (mc_accumulate) unless alignment mode or the configuration
   // asks for the step API; MC_ACCUM_STEPS=1 forces the host-driven loop (both are GPU paths).
   bool done = false;
@@ -415,28 +433,35 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
     std::string mbox_note;
     if (dev_shard) {
       // every rank learns every rank's outcome: a mailbox the ranks' GPUs could not all see
-      // (each kernel's hand-off deadline expired) sends all of them to the host-driven sharded
-      // steps together; any other failure stops all of them
+      // (each kernel's hand-off deadline expired: MC_ERR_TIMEOUT) sends all of them to the
+      // host-driven sharded steps together; any other failure stops all of them, with this
+      // rank's own message where it failed itself
+      const std::string own = rc == MC_OK ? std::string() : std::string(mc_last_error());
       int32_t mine[2] = {rc, 0}, all[2 * 64];
       if (shard->allgather(shard->user, mine, sizeof mine, all) != 0) throw PeerError("all-gather across ranks failed");
       int worst = MC_OK;  // MC_OK < timeouts / unsupported (fall back) < anything else (stop)
       for (int r = 0; r < shard->world; r++) {
         const int e = all[2 * r];
         if (e == MC_OK) continue;
-        if (e == MC_ERR_HIP || e == MC_ERR_UNSUPPORTED) {
-          if (worst == MC_OK) worst = e;
+        if (e == MC_ERR_TIMEOUT || e == MC_ERR_UNSUPPORTED) {
+          if (worst == MC_OK || (worst == MC_ERR_UNSUPPORTED && e == MC_ERR_TIMEOUT)) worst = e;
         } else {
           worst = e;
           break;
         }
       }
-      if (worst == MC_ERR_HIP) {
-        fprintf(stderr, "meshclust: device-sharded accumulation: the ranks' mailbox hand-offs failed or timed out; "
+      if (worst == MC_ERR_TIMEOUT) {
+        fprintf(stderr, "meshclust: device-sharded accumulation: the ranks' mailbox hand-offs timed out; "
                         "taking the host-driven sharded steps\n");
         mbox_note = " (mailbox timed out)";
-        worst = MC_ERR_UNSUPPORTED;
+        rc = MC_ERR_UNSUPPORTED;
+      } else if (worst != MC_OK && worst != MC_ERR_UNSUPPORTED) {
+        // a real failure somewhere: this rank's own error goes to check() below with its message
+        if (rc == MC_OK || rc == MC_ERR_TIMEOUT || rc == MC_ERR_UNSUPPORTED)
+          throw PeerError("device-sharded accumulation failed on another rank" + (own.empty() ? "" : " (here: " + own + ")"));
+      } else {
+        rc = worst;
       }
-      rc = worst;
     }
     if (rc == MC_OK) {
       for (uint64_t c = 0; c < ncl; c++)

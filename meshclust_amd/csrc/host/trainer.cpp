@@ -140,13 +140,9 @@ std::vector<PairId> Trainer::split() {
   if (cfg_.verbose) printf("Point pairs: %zu\n", indices.size());
   const size_t to_add_each = cfg_.max_pts_from_one / 2;
   const size_t P = indices.size();
-  // every pivot's distance to every point on the GPU (in chunks, below).  Each pivot's std::sort runs on
-  // (key << 32 | id) words with a comparator that looks only at the key: the comparison
-  // outcomes -- and so the permutation -- are those of sorting ids by keys[id].
-  // std::sort(pts, by distance to pivot i) is evaluated lazily (lazysort.hpp): only the
-  // positions the binary search and the sampler read are resolved, with std::sort's exact
-  // tie order.
-  // Each pivot's std::sort(points, by distance to pivot i) (Trainer.cpp:691-701) is evaluated
+  // Each pivot's std::sort runs on (key << 32 | id) words with a comparator that looks only at
+  // the key: the comparison outcomes -- and so the permutation -- are those of sorting ids by
+  // keys[id].  Each pivot's std::sort(points, by distance to pivot i) (Trainer.cpp:691-701) is evaluated
   // on the device (mc_split_*, split.hip): the (key << 32 | id) arrays stay in HBM and only
   // the positions the binary search and the sampler read are resolved, with std::sort's exact
   // tie order.

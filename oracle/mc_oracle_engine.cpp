@@ -495,6 +495,10 @@ int mc_ctx_pci_bus_id(mc_ctx *, char *buf, int len) {
 int mc_set_mailbox(mc_ctx *, void *, uint64_t, int, int world, int) {
   return world == 0 ? MC_OK : fail(MC_ERR_UNSUPPORTED, "no device-sharded accumulation in the CPU oracle engine");
 }
+int mc_accum_plan_info(mc_ctx *, uint32_t, uint32_t *) {
+  return fail(MC_ERR_UNSUPPORTED, "the CPU oracle engine drives accumulation step by step");
+}
+int mc_set_accum_grid(mc_ctx *, uint32_t) { return MC_OK; }
 
 // RCCL is a GPU-side transport: the CPU engine's ranks exchange through the caller's callback.
 int mc_comm_unique_id(uint8_t *) { return fail(MC_ERR_UNSUPPORTED, "no RCCL in the CPU oracle engine"); }

@@ -21,14 +21,14 @@
 #include <algorithm>
 #define private public
 #define protected public
-#include "../../reference/src/nonltr/ChromListMaker.h"
-#include "../../reference/src/nonltr/ChromosomeOneDigit.h"
-#include "../../reference/src/nonltr/KmerHashTable.h"
-#include "../../reference/src/cluster/src/ClusterFactory.h"
-#include "../../reference/src/cluster/src/DivergencePoint.h"
-#include "../../reference/src/cluster/src/Trainer.h"
-#include "../../reference/src/cluster/src/Feature.h"
-#include "../../reference/src/utility/GlobAlignE.h"
+#include "nonltr/ChromListMaker.h"
+#include "nonltr/ChromosomeOneDigit.h"
+#include "nonltr/KmerHashTable.h"
+#include "cluster/src/ClusterFactory.h"
+#include "cluster/src/DivergencePoint.h"
+#include "cluster/src/Trainer.h"
+#include "cluster/src/Feature.h"
+#include "utility/GlobAlignE.h"
 #undef private
 #undef protected
 

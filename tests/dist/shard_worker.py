@@ -1,8 +1,10 @@
 """One rank of a sharded clustering (launched by torch.distributed.run; see
 tests/test_distributed.py).  Engine: the CPU oracle engine (test-only) or, with --gpu, the
-product's libmcgpu on cuda:0 (every rank: the test boxes have one GPU).  Exchange: a gloo
-all-gather through a Python callback, or with --rccl libmcgpu's RCCL communicator called from
-C++ (one rank per GPU, so world size 1 on a one-GPU box)."""
+product's libmcgpu on cuda:0 (every rank: the test boxes have one GPU), or with --per-rank-gpu
+on the rank's own GPU (LOCAL_RANK; boxes with several GPUs).  Exchange: a gloo all-gather
+through a Python callback, or with --rccl libmcgpu's RCCL communicator called from C++ (one
+rank per GPU).  --grid-per-rank G0,G1,...: rank r caps its accumulation grid at G_r
+(MC_ACCUM_GRID), so the ranks start from different plans."""
 import argparse
 import ctypes as C
 import json
@@ -19,6 +21,8 @@ def main():
     ap.add_argument("out")
     ap.add_argument("--gpu", action="store_true")
     ap.add_argument("--rccl", action="store_true")
+    ap.add_argument("--per-rank-gpu", action="store_true")
+    ap.add_argument("--grid-per-rank", default=None)
     ap.add_argument("flags", nargs="*")
     a = ap.parse_args()
     import datetime
@@ -28,10 +32,13 @@ def main():
     dist.init_process_group("gloo", init_method="env://",
                             timeout=datetime.timedelta(seconds=float(os.environ.get("MC_DIST_TIMEOUT_S", "600"))))
     from meshclust_amd.dist import RcclShardComm, TorchShardComm
+    if a.grid_per_rank:
+        os.environ["MC_ACCUM_GRID"] = a.grid_per_rank.split(",")[dist.get_rank()]
     if a.gpu:
         import meshclust_amd as M
-        eng = M.Engine(0)
-        comm = RcclShardComm(0) if a.rccl else TorchShardComm()
+        dev = int(os.environ.get("LOCAL_RANK", "0")) if a.per_rank_gpu else 0
+        eng = M.Engine(dev)
+        comm = RcclShardComm(dev) if a.rccl else TorchShardComm()
         ds = M.Dataset([a.fasta], threads=4)
         st = ds.run(eng, a.flags + ["--threads", "4"], upload=True, clstr=a.out if comm.rank == 0 else None,
                     comm=comm)

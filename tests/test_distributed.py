@@ -31,10 +31,10 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _launch(fa, flags, out, gpu, world, rccl=False, env_extra=None, timeout=600):
+def _launch(fa, flags, out, gpu, world, rccl=False, env_extra=None, timeout=600, worker_args=()):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), WORKER]
-    cmd += (["--gpu"] if gpu else []) + (["--rccl"] if rccl else []) + [fa, out, "--"] + flags
+    cmd += (["--gpu"] if gpu else []) + (["--rccl"] if rccl else []) + list(worker_args) + [fa, out, "--"] + flags
     env = dict(os.environ, OMP_NUM_THREADS="2", **(env_extra or {}))
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
@@ -44,14 +44,14 @@ def _launch(fa, flags, out, gpu, world, rccl=False, env_extra=None, timeout=600)
     return ranks
 
 
-def _run_world(name, tmp_path, gpu, world=2, rccl=False, env_extra=None):
+def _run_world(name, tmp_path, gpu, world=2, rccl=False, env_extra=None, worker_args=()):
     """Rank 0's .clstr against the reference golden.  The GPU ranks run ONE device-resident
     accumulation together (mailbox exchange between their kernels: "device xW"), unless
     MC_SHARD_HOST_STEPS asks for the host-driven sharded steps (one all-gather per step: the
     CPU engine's only form)."""
     fa, flags = fixtures.e2e_input(name, tmp_path)
     out = str(tmp_path / (name + ".clstr"))
-    ranks = _launch(fa, flags, out, gpu, world, rccl, env_extra)
+    ranks = _launch(fa, flags, out, gpu, world, rccl, env_extra, worker_args=worker_args)
     with gzip.open(fixtures.golden("e2e_%s.clstr.gz" % name), "rb") as f:
         assert open(out, "rb").read() == f.read()
     host_steps = not gpu or "MC_SHARD_HOST_STEPS" in (env_extra or {})
@@ -174,6 +174,92 @@ def test_sharded_D1M_equals_single_gpu(tmp_path):
     assert BG.canonical_digest(BG.clusters_of(out)) == BG.canonical_digest(BG.clusters_of(one))
 
 
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+def test_sharded_uneven_grids_B100k_equals_reference(tmp_path):
+    """Two ranks on one GPU whose own grids differ (MC_ACCUM_GRID 64 and 256: rank 0 alone would
+    take 512-position tiles, rank 1 alone the dense 64-position tiles).  Tile t belongs to rank
+    t mod 2, so the ranks must agree on the tile: attach_mailbox gives both the smaller grid and
+    compares the plans (cluster.cpp).  The partition must be the reference's."""
+    g = np.load(fixtures.golden("cfg_B100k.npz"))
+    fa = _big_input("B100k")
+    out = str(tmp_path / "B100k.clstr")
+    ranks = _launch(fa, ["--id", "0.90"], out, True, 2, False, {}, timeout=800, worker_args=["--grid-per-rank", "64,256"])
+    assert ranks[0]["accum_path"] == "device x2"
+    assert BG.canonical_digest(BG.clusters_of(out)) == str(g["digest"])
+
+
+def _bench_line(extra_env, args, timeout=900):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                       timeout=timeout, env=dict(os.environ, **extra_env))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    return json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+def test_bench_two_ranks_one_gpu_D100k(tmp_path):
+    """bench.py --gpus 2 spawns its two ranks itself (no launcher), and they share ONE config-D
+    clustering; MC_BENCH_ONE_GPU=1 puts both on the box's one GPU.  The line reports two GPUs
+    and the partition is the reference's (cfg_D100k: config D's shape at 100k reads)."""
+    g = np.load(fixtures.golden("cfg_D100k.npz"))  # (bench.py --workload D --n 100000: the same generator and seed)
+    keep = str(tmp_path / "bench_D100k.clstr")
+    line = _bench_line({"MC_BENCH_ONE_GPU": "1", "OMP_NUM_THREADS": "4"},
+                       ["--gpus", "2", "--workload", "D", "--n", "100000", "--steps", "1", "--warmup", "1",
+                        "--no-cpu-baseline", "--keep-clstr", keep])
+    assert line["n_gpus"] == 2 and line["config"]["mode"] == "shard" and line["config"]["workload_config"] == "D"
+    assert line["extra"]["accum_path"] == "device x2"
+    assert line["value"] > 0 and line["steps"] == 1
+    got = BG.clusters_of(keep)
+    assert sorted(c for c, _ in got) == [int(x) for x in g["centres"]]
+    assert BG.canonical_digest(got) == str(g["digest"])
+
+
+# ---- boxes with two or more GPUs (the driver's multi-GPU node): one rank per GPU ------------
+def _gpu_count():
+    try:
+        import torch
+        return torch.cuda.device_count()  # (does not initialise HIP on this image)
+    except Exception:
+        return 0
+
+
+multi_gpu = pytest.mark.skipif(_gpu_count() < 2, reason="needs two GPUs")
+
+
+@pytest.mark.gpu
+@multi_gpu
+@pytest.mark.parametrize("name", ["a1k", "fam2k", "big2_3k", "s1k_k5"])
+def test_rccl_world2_two_gpus_byte_identical(name, tmp_path):
+    """Two processes, one GPU each, RCCL over xGMI for the all-gathers and the mailbox between
+    two devices' kernels: byte-identical to the reference golden."""
+    _run_world(name, tmp_path, gpu=True, world=2, rccl=True, worker_args=["--per-rank-gpu"])
+
+
+@pytest.mark.gpu
+@multi_gpu
+@pytest.mark.timeout(900)
+def test_rccl_world2_two_gpus_B100k_equals_reference(tmp_path):
+    g = np.load(fixtures.golden("cfg_B100k.npz"))
+    fa = _big_input("B100k")
+    out = str(tmp_path / "B100k.clstr")
+    ranks = _launch(fa, ["--id", "0.90"], out, True, 2, True, {}, timeout=800, worker_args=["--per-rank-gpu"])
+    assert ranks[0]["accum_path"] == "device x2"
+    assert BG.canonical_digest(BG.clusters_of(out)) == str(g["digest"])
+
+
+@pytest.mark.gpu
+@multi_gpu
+@pytest.mark.timeout(900)
+def test_bench_two_gpus_D100k(tmp_path):
+    g = np.load(fixtures.golden("cfg_D100k.npz"))
+    keep = str(tmp_path / "bench_D100k.clstr")
+    line = _bench_line({"OMP_NUM_THREADS": "4"}, ["--gpus", "2", "--workload", "D", "--n", "100000", "--steps", "1",
+                                                  "--warmup", "1", "--no-cpu-baseline", "--keep-clstr", keep])
+    assert line["n_gpus"] == 2 and line["extra"]["accum_path"] == "device x2"
+    assert BG.canonical_digest(BG.clusters_of(keep)) == str(g["digest"])
+
+
 # ---- one process, several ranks (bin/meshclust --devices): threads sharing a host exchange ----
 HARNESS = os.path.join(ROOT, "oracle", "_build", "meshclust_cpu")
 
@@ -228,7 +314,10 @@ def test_processes_fault_stops_every_rank(cpu_lib, stage, tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,devices", [("fam2k", "0"), ("fam2k", "0,0"), ("big2_3k", "0,0"), ("s1k_k5", "0,0")])
+@pytest.mark.parametrize("name,devices", [("fam2k", "0"), ("fam2k", "0,0"), ("big2_3k", "0,0"), ("s1k_k5", "0,0"),
+                                          pytest.param("fam2k", "0,1", marks=multi_gpu),
+                                          pytest.param("big2_3k", "0,1", marks=multi_gpu),
+                                          pytest.param("s1k_k5", "0,0,1", marks=multi_gpu)])
 def test_devices_cli_gpu_byte_identical(name, devices, tmp_path):
     """bin/meshclust --devices on the product: one GPU, or two ranks (threads, contexts) on the
     test box's one GPU sharing the accumulation through the mailbox (each kernel takes half of
