@@ -16,7 +16,8 @@ parse / upload / write) is reported in "extra" as resident_sequences_per_s.
 
 GPUs.  ``--gpus N`` runs N ranks, one process per GPU: launched by the driver through
 torch.distributed.run, or -- when WORLD_SIZE is not set -- spawned here as N child processes
-(torch.distributed.run, 127.0.0.1) before anything touches a GPU; rank 0 prints the line.
+(RANK / WORLD_SIZE / MASTER_* as torch.distributed.run sets them, 127.0.0.1) before anything
+touches a GPU; rank 0 prints the line.
 The N ranks share ONE clustering of the same workload at every N, sharded by record (strong
 scaling): every rank's persistent accumulation kernel scans its interleaved tiles of each
 get_close window and the kernels exchange each step's {first maximum, flagged reads} through a
@@ -108,15 +109,32 @@ def cpu_baseline(fasta, args, n_reads, threads, repeats, limit_s=600):
 
 
 def spawn_ranks(n):
-    """--gpus N without a launcher: N child processes through torch.distributed.run (each
-    child sees WORLD_SIZE and runs one rank); this process never touches a GPU and exits with
-    the launcher's status."""
+    """--gpus N without a launcher: N child processes of this script, one rank each (RANK,
+    LOCAL_RANK, WORLD_SIZE and MASTER_* set as torch.distributed.run sets them, 127.0.0.1);
+    this process never touches a GPU.  A rank that fails ends the others; the exit status is
+    the first failure's."""
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
-           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
-    return subprocess.run(cmd).returncode
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 1
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
 
 
 def kernel_pmc(kname):
