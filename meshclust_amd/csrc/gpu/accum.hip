@@ -143,6 +143,7 @@ struct AccArgs {
   uint64_t fcap;
   int res;        // chunks per worker whose rows live in its LDS (0: rows stream from memory)
   uint4 *cc;      // streaming: per-chunk compacted copies of the alive rows (null: read hs)
+  uint4 *srows;   // dense streaming workers: two row buffers of fcap entries per worker
   uint32_t mrow;  // member cache entries (LDS)
   // output
   uint32_t *mem_pos;    // N: member static positions, cluster after cluster
@@ -622,7 +623,7 @@ __device__ __forceinline__ void worker(const AccArgs &A, const DevClassifier &C,
     const uint32_t *hdr = srec + (WIDE ? 0 : 4 * nch);
     if (hdr[0] == NONE) return;  // accumulation finished
     const uint64_t P_S = hdr[1], P_E = hdr[2];
-    const uint32_t kend = hdr[3];
+    const uint32_t kend = hdr[3] & 0x7fffffffu;  // (bit 31: the dense form's exact-span flag)
     const PInfo pc{(uint64_t)hdr[4 + KINL] | ((uint64_t)hdr[5 + KINL] << 32),
                    (uint64_t)hdr[6 + KINL] | ((uint64_t)hdr[7 + KINL] << 32),
                    (uint64_t)hdr[8 + KINL] | ((uint64_t)hdr[9 + KINL] << 32)};
@@ -970,6 +971,7 @@ __device__ __forceinline__ void worker_dense(const AccArgs &A, const DevClassifi
   __shared__ int s_abort;
   __shared__ uint64_t s_b[2];  // spec: part B of the step, {tag << 32 | S}, {tag << 32 | E}
   __shared__ uint64_t s_tw[NW];  // MC_ACCUM_PROFILE=4: each wave's scores-done time
+  __shared__ uint64_t s_t0[3];   // ... thread 0's record-seen, scores-done and part-B times
   __shared__ uint32_t s_arr;     // waves that have reduced this step's scores
   constexpr int NC = NCH > 0 ? NCH : DMAXCH;
   const uint32_t GW = gridDim.x - 1, w = blockIdx.x - 1;
@@ -1083,7 +1085,9 @@ __device__ __forceinline__ void worker_dense(const AccArgs &A, const DevClassifi
     const uint32_t *hdr = srec + 4 * nch;
     if (hdr[0] == NONE) return;  // accumulation finished
     const uint64_t P_S = hdr[1], P_E = hdr[2];
-    const uint32_t kend = hdr[3];
+    // bit 31 of the kill-log word: the record's span IS the exact window (no part B follows)
+    const uint32_t kend = hdr[3] & 0x7fffffffu;
+    const bool exact = (hdr[3] >> 31) != 0;
     const PInfo pc{(uint64_t)hdr[4 + KINL] | ((uint64_t)hdr[5 + KINL] << 32),
                    (uint64_t)hdr[6 + KINL] | ((uint64_t)hdr[7 + KINL] << 32),
                    (uint64_t)hdr[8 + KINL] | ((uint64_t)hdr[9 + KINL] << 32)};
@@ -1143,10 +1147,15 @@ __device__ __forceinline__ void worker_dense(const AccArgs &A, const DevClassifi
     }
     if (A.trace && t == 0) t_scanned = now();
     if (A.trace2 && lane == 0) s_tw[wv] = now();
+    if (A.trace2 && t == 0) {
+      s_t0[0] = t_seen;
+      s_t0[1] = t_scanned;
+      s_t0[2] = 0;
+    }
     uint64_t W_S = P_S, W_E = P_E;  // the exact window
     bool abandon = false;
     uint64_t t_bgot = 0, t_red = 0;
-    if (A.spec) {
+    if (A.spec && !exact) {
       // part B: from the LDS copy once a wave has it, else polled by this wave's lanes 0 / 1.
       // (A wave that gives up marks the abort and takes the step as abandoned, so every wave
       // still reaches the one barrier below.)
@@ -1177,6 +1186,7 @@ __device__ __forceinline__ void worker_dense(const AccArgs &A, const DevClassifi
         __builtin_amdgcn_s_sleep(1);
       }
       if (A.trace2 && t == 0) t_bgot = now();
+      if (A.trace2 && t == 0) s_t0[2] = t_bgot;
       W_S = (uint32_t)b0;
       W_E = (uint32_t)b1;
       abandon = (uint32_t)W_S == NONE;
@@ -1209,7 +1219,17 @@ __device__ __forceinline__ void worker_dense(const AccArgs &A, const DevClassifi
         }
       }
       const uint64_t scanned = __ballot(nscan != 0);
-      if (__ballot(best_p != NONE64)) wave_best_all(best_v, best_p, better);  // (waves with no candidate skip it)
+      // the wave's first maximum: entry e is lane e % 64 of wave e / 64 and entries are in
+      // static-position order, so of the lanes holding the wave's largest value the lowest one
+      // holds the first maximum (a max reduction and a ballot, no (value, position) pairs moved)
+      const uint64_t cands = __ballot(best_p != NONE64);
+      if (cands) {  // (waves with no candidate skip it)
+        const double m = wave_ext_f64_all<true>(best_v);
+        const uint64_t hit = __ballot(best_p != NONE64 && best_v == m);
+        const int L = __builtin_ctzll(hit);
+        best_v = __builtin_bit_cast(double, readlane64(__builtin_bit_cast(uint64_t, best_v), L));
+        best_p = readlane64(best_p, L);
+      }
       if (lane == 0) {
         s_bv[wv] = best_v;
         s_bp[wv] = best_p;
@@ -1271,12 +1291,12 @@ __device__ __forceinline__ void worker_dense(const AccArgs &A, const DevClassifi
           }
           if (A.trace2 && j == 0 && seen < TRACE2_STEPS) {
             uint64_t *tr = A.trace2 + ((uint64_t)seen * GMAX + w) * T2W;
-            tr[0] = t_seen;
-            tr[1] = t_scanned;
+            tr[0] = s_t0[0];
+            tr[1] = s_t0[1];
             tr[2] = now();
             uint64_t tw = 0;
             for (int i = 0; i < NW; i++) tw = s_tw[i] > tw ? s_tw[i] : tw;
-            tr[3] = t_bgot;
+            tr[3] = s_t0[2];
             tr[4] = tw;
             tr[5] = t_red;
           }
@@ -1347,6 +1367,356 @@ __device__ __forceinline__ void worker_dense(const AccArgs &A, const DevClassifi
 }
 
 // ============================================================================================
+// Dense streaming workers (narrow rows, more than NT candidates per worker: config D on one to
+// four GPUs).  Tiles of DT positions are dealt round-robin as in the dense form, and a worker
+// keeps its alive candidates as ONE dense list in static-position order -- but the rows live in
+// HBM, in a per-worker buffer laid out for the scan: entry e is lane e % 64 of group e / 64, and a
+// group's chunk k is 64 consecutive 16-byte words (one coalesced 1 KiB load per wave).  Thread t
+// takes entries t, t + NT, ...  A dead entry's row is simply not loaded; once a quarter of the
+// list has died the worker rewrites the alive rows densely into its other buffer (off the
+// critical path, after its partial), so the streamed bytes stay within 4/3 of the alive rows'
+// -- the chunk-major static layout fetched every 128-byte line that held one alive row, 1.8x the
+// alive bytes at config D (profiles/r03_v11/config_d_pmc.json).  The compaction's traffic is
+// the alive rows once per quarter of deaths: gigabytes against the scan's terabytes.
+// LDS: record words | entry positions (compaction staging)
+// ============================================================================================
+constexpr int SJ = 32;  // entries per thread the dense streaming form takes (fcap <= SJ * NT: bits of a mask)
+
+// 16-byte load that bypasses this CU's vector L1 (sc1): the rows were written by other threads
+// of this workgroup (compaction), whose stores reached L2 before the barrier
+__device__ __forceinline__ uint4 ld_sc1_16(const __amdgpu_buffer_rsrc_t r, uint32_t off) {
+  const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 16);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+template <typename T, int NCH>
+__device__ __forceinline__ void worker_dstream(const AccArgs &A, const DevClassifier &C, uint4 *dyn) {
+  __shared__ double s_bv[NW];
+  __shared__ uint64_t s_bp[NW];
+  __shared__ uint32_t s_nfl, s_go, s_inl[INL], s_wc[NW], s_cnt;
+  __shared__ int s_abort;
+  __shared__ uint32_t s_arr;
+  constexpr int NC = NCH > 0 ? NCH : DMAXCH;
+  const uint32_t GW = gridDim.x - 1, w = blockIdx.x - 1;
+  const Div32 dgw(GW);
+  const int lane = threadIdx.x & 63, wv = wave_id();
+  const uint32_t t = threadIdx.x;
+  const int nch = NCH > 0 ? NCH : A.nch;
+  const int rec_words = (int)A.rec_g;
+  uint32_t *srec = reinterpret_cast<uint32_t *>(dyn);
+  const uint4 *clds = dyn;  // the centre row: record words 0 .. 4 nch
+  // entry positions of the current list and the rebuild's target (fcap each)
+  uint32_t *lpos[2] = {reinterpret_cast<uint32_t *>(dyn + (rec_words + 3) / 4), nullptr};
+  lpos[1] = lpos[0] + (A.fcap + 3) / 4 * 4;
+  // this worker's two row buffers (fcap entries each), as buffer resources for sc1 loads
+  const uint64_t wrow = A.fcap * (uint64_t)nch;  // uint4 per buffer
+  uint4 *rb[2] = {A.srows + (uint64_t)w * 2 * wrow, A.srows + ((uint64_t)w * 2 + 1) * wrow};
+  const __amdgpu_buffer_rsrc_t rr[2] = {__builtin_amdgcn_make_buffer_rsrc(rb[0], 0, (int)(wrow * 16), 0x00020000),
+                                        __builtin_amdgcn_make_buffer_rsrc(rb[1], 0, (int)(wrow * 16), 0x00020000)};
+  int cur = 0;
+  const uint32_t J = (uint32_t)((A.fcap + NT - 1) / NT);  // entries per thread (<= SJ)
+  auto slot = [&](uint32_t e, int k) -> uint32_t {  // uint4 index of entry e's chunk k in a buffer
+    return ((e >> 6) * (uint32_t)nch + (uint32_t)k) * 64u + (e & 63u);
+  };
+  // entry e = t + NT j: this worker's (e / DT)-th tile, offset e % DT (positions increase with
+  // the entry, so the entries below N are a prefix)
+  uint32_t alive = 0;  // bit j: entry t + NT j alive
+  for (uint32_t j = 0; j < J; j++) {
+    const uint32_t e = t + NT * j;
+    if (e >= A.fcap) break;
+    const uint64_t lt = (uint64_t)w + (uint64_t)(e / DT) * GW;
+    const uint64_t p = (lt * A.W + A.rank) * DT + (e % DT);
+    if (p >= A.N) break;
+    lpos[0][e] = (uint32_t)p;
+    alive |= 1u << j;
+    for (int k = 0; k < nch; k++) rb[0][slot(e, k)] = A.hs[(uint64_t)k * A.npad + p];
+  }
+  drain();  // (the rows are read back with sc1 loads after the barrier below)
+  if (t == 0) {
+    s_cnt = 0;
+    s_abort = 0;
+    s_arr = 0;
+  }
+  __syncthreads();
+  {
+    const uint32_t c = wave_sum32((uint32_t)__popc(alive));
+    if (lane == 0 && c) atomicAdd(&s_cnt, c);
+  }
+  __syncthreads();
+  uint32_t n_ent = s_cnt;  // list length (alive or not since the last rebuild)
+  uint32_t kcur = 0, seen = 0;
+  for (;;) {
+    // ---- wait for the next step's record (wave 0), as `worker` ---------------------------
+    if (wv == 0) {
+      const uint64_t t0 = now();
+      const uint32_t want = seen + 1;
+      int state = 0;
+      uint32_t got = want;
+      bool late = false;
+      const uint64_t *rn = A.ring + (uint64_t)(want % RING) * A.rec_g;
+      for (uint32_t it = 1;; it++) {
+        bool ok = true, ahead = false;
+        for (int j = lane; j < rec_words; j += 64) {
+          const uint64_t x = ld64(rn + j);
+          const uint32_t tg = (uint32_t)(x >> 32);
+          ok &= tg == want;
+          ahead |= (int32_t)(tg - want) > 0;
+          srec[j] = (uint32_t)x;
+        }
+        if (__ballot(!ok) == 0) {
+          state = 1;
+          break;
+        }
+        if (__ballot(ahead) != 0) {
+          late = true;
+          break;
+        }
+        if ((it & 255) == 0 && timed_out(A, t0)) {
+          state = 2;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      while (late && state == 0) {
+        uint32_t v = 0;
+        if (lane == 0) {
+          for (uint32_t it = 1; (v = ld32(A.go)) == seen; it++) {
+            if ((it & 255) == 0 && timed_out(A, t0)) break;
+            __builtin_amdgcn_s_sleep(1);
+          }
+        }
+        v = (uint32_t)__builtin_amdgcn_readlane((int)v, 0);
+        if (v == seen) {
+          state = 2;
+          break;
+        }
+        const uint64_t *r = A.ring + (uint64_t)(v % RING) * A.rec_g;
+        bool ok = true;
+        for (int j = lane; j < rec_words; j += 64) {
+          const uint64_t x = ld64(r + j);
+          ok &= (uint32_t)(x >> 32) == v;
+          srec[j] = (uint32_t)x;
+        }
+        if (__ballot(!ok) == 0) {
+          state = 1;
+          got = v;
+        }
+      }
+      if (lane == 0) {
+        if (state == 2) s_abort = 1;
+        s_go = got;
+        s_nfl = 0;
+      }
+    }
+    __syncthreads();
+    if (s_abort) {
+      if (t == 0) atomicMax((unsigned long long *)&A.out[3], 99ull);
+      return;
+    }
+    seen = s_go;
+    const uint32_t *hdr = srec + 4 * nch;
+    if (hdr[0] == NONE) return;  // accumulation finished
+    uint64_t W_S = hdr[1], W_E = hdr[2];
+    const uint32_t kend = hdr[3] & 0x7fffffffu;
+    const bool exact = (hdr[3] >> 31) != 0;
+    const PInfo pc{(uint64_t)hdr[4 + KINL] | ((uint64_t)hdr[5 + KINL] << 32),
+                   (uint64_t)hdr[6 + KINL] | ((uint64_t)hdr[7 + KINL] << 32),
+                   (uint64_t)hdr[8 + KINL] | ((uint64_t)hdr[9 + KINL] << 32)};
+    const PTerms tq = pterms(pc.mag, pc.sumsq, A.B);
+    const uint32_t *lp = lpos[cur];
+    // the controller's kills since the last record, against each entry of this thread
+    {
+      const uint32_t kinl0 = kend > (uint32_t)KINL ? kend - KINL : 0;
+      const uint64_t t0k = kinl0 > kcur ? now() : 0;
+      for (uint32_t e = kcur; e < kend; e++) {
+        uint32_t p;
+        if (e >= kinl0) {
+          p = hdr[4 + KINL - (kend - e)];
+        } else {
+          uint64_t g = ld64(A.klog + e);
+          for (uint32_t it = 1; (uint32_t)(g >> 32) != e + 1; it++) {
+            if ((it & 255) == 0 && timed_out(A, t0k)) {
+              s_abort = 1;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            g = ld64(A.klog + e);
+          }
+          p = (uint32_t)g;
+        }
+        for (uint32_t j = 0; j < J; j++)
+          if (((alive >> j) & 1u) && lp[t + NT * j] == p) alive &= ~(1u << j);
+      }
+      kcur = kend;
+    }
+    // the exact window: the record's span, or part B (a superset span was published first)
+    bool abandon = false;
+    if (A.spec && !exact) {
+      const uint64_t *rbp = A.ringb + (uint64_t)(seen % RING) * 2;
+      const uint64_t t0 = now();
+      uint64_t b0 = 0, b1 = 0;
+      for (uint32_t it = 1;; it++) {
+        const uint64_t g = lane < 2 ? ld64(rbp + lane) : 0;
+        b0 = readlane64(g, 0);
+        b1 = readlane64(g, 1);
+        if ((uint32_t)(b0 >> 32) == seen && (uint32_t)(b1 >> 32) == seen) break;
+        if ((it & 255) == 0 && timed_out(A, t0)) {
+          if (lane == 0) s_abort = 1;
+          b0 = b1 = NONE;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      W_S = (uint32_t)b0;
+      W_E = (uint32_t)b1;
+      abandon = (uint32_t)W_S == NONE;
+    }
+    uint64_t c0 = 0, c1 = 0;
+    const bool any_tile = !abandon && rank_tiles(W_S / DT, W_E / DT, A.W, A.rank, &c0, &c1);
+    const uint32_t nact = any_tile ? (uint32_t)(c1 - c0 + 1 < (uint64_t)GW ? c1 - c0 + 1 : (uint64_t)GW) : 0u;
+    const uint32_t mine = any_tile ? dgw.mod(w + GW - dgw.mod((uint32_t)c0)) : 0u;
+    const bool active = any_tile && mine < nact;  // (uniform)
+    if (active) {
+      double best_v = -1.0;
+      uint64_t best_p = NONE64;
+      uint32_t nscan = 0;
+      bool listed = false;
+      const __amdgpu_buffer_rsrc_t R = rr[cur];
+      for (uint32_t j = 0; j < J; j++) {
+        const uint32_t e = t + NT * j;
+        if (!((alive >> j) & 1u)) continue;
+        const uint32_t p = lp[e];
+        if (p < W_S || p > W_E) continue;
+        nscan++;
+        uint4 v[NC];
+#pragma unroll
+        for (int k = 0; k < NC; k++)
+          if (k < nch) v[k] = ld_sc1_16(R, slot(e, k) * 16u);
+        const PInfo pi{A.mag_s[p], A.sumsq_s[p], A.len_s[p]};
+        Acc<T> acc;
+#pragma unroll
+        for (int k = 0; k < NC; k++)
+          if (k < nch) acc.add(v[k], clds[k]);
+        double cv;
+        const PTerms pt = pterms(pi.mag, pi.sumsq, A.B);
+        const int d = A.fc.on    ? classify_fast(C, A.fc, acc.finish(pi.mag, pc.mag), pi, pt, pc, tq, A.B, &cv)
+                      : C.layout ? classify_std(C, acc.finish(pi.mag, pc.mag), pi, pt, pc, tq, A.B, &cv)
+                                 : classify_cand<T>(acc, pi, pc, A.B, C, &cv);
+        if (d) {
+          alive &= ~(1u << j);
+          const uint32_t idx = atomicAdd(&s_nfl, 1u);
+          if (idx < (uint32_t)INL) s_inl[idx] = p;
+          else {
+            st32(A.fpos + (uint64_t)w * A.fcap + idx, p);
+            listed = true;
+          }
+        }
+        if (cv > -1.0 && better(cv, p, best_v, best_p)) {
+          best_v = cv;
+          best_p = p;
+        }
+      }
+      nscan = wave_sum32(nscan);
+      // the wave's first maximum (a lane's entries are not adjacent: pairs only on ties)
+      if (__ballot(best_p != NONE64)) {
+        const double m = wave_ext_f64_all<true>(best_v);
+        const uint64_t hit = __ballot(best_p != NONE64 && best_v == m);
+        if (__popcll(hit) > 1) {
+          wave_best_all(best_v, best_p, better);
+        } else {
+          const int L = __builtin_ctzll(hit);
+          best_v = __builtin_bit_cast(double, readlane64(__builtin_bit_cast(uint64_t, best_v), L));
+          best_p = readlane64(best_p, L);
+        }
+      }
+      if (lane == 0) {
+        s_bv[wv] = best_v;
+        s_bp[wv] = best_p;
+        s_wc[wv] = nscan;
+      }
+      if (__ballot(listed)) drain();
+      // arrival: the wave that completes the workgroup's scores publishes the partial
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      uint32_t arr = 0;
+      if (lane == 0) arr = atomicAdd(&s_arr, 1u);
+      arr = (uint32_t)__builtin_amdgcn_readfirstlane((int)arr);
+      if (arr == (uint32_t)NW - 1) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        if (lane < PART_G) {
+          double v = s_bv[0];
+          uint64_t pp = s_bp[0];
+          uint32_t ns = s_wc[0];
+#pragma unroll
+          for (int i = 1; i < NW; i++) {
+            ns += s_wc[i];
+            if (better(s_bv[i], s_bp[i], v, pp)) {
+              v = s_bv[i];
+              pp = s_bp[i];
+            }
+          }
+          const uint64_t vb = (uint64_t)__double_as_longlong(v);
+          const int jj = lane;
+          const uint32_t nfl = s_nfl;
+          const uint32_t data = jj == 0   ? (uint32_t)(vb >> 32)
+                                : jj == 1 ? (uint32_t)vb
+                                : jj == 2 ? (pp == NONE64 ? NONE : (uint32_t)pp)
+                                : jj == 3 ? nfl
+                                : jj == 4 ? ns
+                                          : ((uint32_t)(jj - 5) < nfl ? s_inl[jj - 5] : NONE);
+          st64(A.partials + (uint64_t)w * PART_G + jj, gran(seen, data));
+          if (jj == 0) s_arr = 0;  // (the next step's arrivals come after the next record)
+        }
+      }
+    }
+    // ---- the list's rebuild once a quarter of it has died (off the critical path: the
+    // controller is collecting) -----------------------------------------------------------
+    if (t == 0) s_cnt = 0;
+    __syncthreads();
+    if (s_abort) {
+      if (t == 0) atomicMax((unsigned long long *)&A.out[3], 99ull);
+      return;
+    }
+    {
+      const uint32_t c = wave_sum32((uint32_t)__popc(alive));
+      if (lane == 0 && c) atomicAdd(&s_cnt, c);
+    }
+    __syncthreads();
+    const uint32_t nal = s_cnt;
+    if ((n_ent - nal) * 4 >= n_ent && nal < n_ent) {
+      // new index of an alive entry = alive entries before it in entry order (entry
+      // e = t + NT j: by j, then by t): one block scan per j
+      const int nxt = cur ^ 1;
+      uint32_t base = 0;
+      for (uint32_t j = 0; j < J; j++) {
+        const bool al = (alive >> j) & 1u;
+        const uint64_t bal = __ballot(al);
+        if (lane == 0) s_wc[wv] = (uint32_t)__popcll(bal);
+        __syncthreads();
+        uint32_t r = base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull)), tot = 0;
+        for (int i = 0; i < NW; i++) {
+          if (i < wv) r += s_wc[i];
+          tot += s_wc[i];
+        }
+        if (al) {
+          const uint32_t e = t + NT * j;
+          for (int k = 0; k < nch; k++) rb[nxt][slot(r, k)] = ld_sc1_16(rr[cur], slot(e, k) * 16u);
+          lpos[nxt][r] = lp[e];
+        }
+        base += tot;
+        __syncthreads();  // (s_wc is rewritten by the next round)
+      }
+      drain();  // every row store has reached L2 before the barrier (the next reads are sc1)
+      __syncthreads();
+      n_ent = base;
+      alive = 0;
+      for (uint32_t j = 0; j < J; j++)
+        if (t + NT * j < n_ent) alive |= 1u << j;
+      cur = nxt;
+    }
+  }
+}
+
+// ============================================================================================
 // Controller (WG 0).  LDS: integer mean row | column sums | bvec (counts, Fenwick tree, bin
 // starts, begin bounds, bitmap unless global) | member cache
 // ============================================================================================
@@ -1411,6 +1781,7 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
   uint32_t step = 0;
   uint64_t err = 0;
   uint32_t kn = 0;      // kill-log length
+  bool rec_exact = false;  // the record being published carries the exact window (no part B)
   uint32_t npend = 0;   // new members s_plist[0, npend) whose bvec kills are still to be done
   uint64_t t_wait = 0, t_coll = 0, t_mark = 0;
   const uint64_t clk0 = A.prof ? __builtin_amdgcn_s_memtime() : 0, rt0 = A.prof ? now() : 0;
@@ -1427,14 +1798,28 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
     M = 0;
   };
   // accumulate's `current = {last}`: member 0 of a new cluster, its row, sums and window data
-  auto new_cluster = [&](uint64_t pos) {
+  // (kill: the seed also leaves the bvec here -- bvec::erase of get_close's best candidate --
+  // with its bin from the member info, no search for it)
+  auto log_kill = [&](uint64_t p) {  // thread 0: a pop / erase, for the workers
+    st64(A.klog + kn, gran(kn + 1, (uint32_t)p));
+    s_klast[kn % KINL] = (uint32_t)p;
+  };
+  auto new_cluster = [&](uint64_t pos, bool kill = false) {
     if (threadIdx.x == 0) {
       st32(A.mem_pos + cl_start, (uint32_t)pos);
       st64(A.mkeys + cl_start, 0);
+      if (kill && !A.mrow) {
+        bv.kill_one(pos);
+        log_kill(pos);
+      }
       if (A.mrow) {
         uint2 w[MINFO_W];
         minfo_issue(A.minfo + pos, w);
         const MInfo mi = minfo_take(w);
+        if (kill) {
+          bv.kill_in(pos, mi.bin);
+          log_kill(pos);
+        }
         mc.pos[0] = (uint32_t)pos;
         mc.key[0] = 0;
         mc.info[0] = mi.mag;
@@ -1448,21 +1833,18 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
     for (int b = threadIdx.x; b < A.B; b += NT) msum[b] = reinterpret_cast<const T *>(A.hr + pos * nch)[b];
     M = 1;
     last_q = 0;
+    if (kill) kn++;
     // (no drain: the seed's member-list entries are never read back in the kernel -- member 0
     // is always in the LDS cache -- and the kill log is tagged, so the stores need not have
     // landed before the next step is published)
     __syncthreads();
-  };
-  auto log_kill = [&](uint64_t p) {  // thread 0: a pop / erase, for the workers
-    st64(A.klog + kn, gran(kn + 1, (uint32_t)p));
-    s_klast[kn % KINL] = (uint32_t)p;
   };
   auto pop = [&]() -> uint64_t {  // bvec::pop (bvec.cpp:26-37): static position or ~0
     const int64_t b = bv.first_nonempty();
     if (b < 0) return NONE64;
     const uint64_t p = bv.select((uint64_t)b, 0);
     if (threadIdx.x == 0) {
-      bv.kill_one(p);
+      bv.kill_in(p, (uint64_t)b);
       log_kill(p);
     }
     kn++;
@@ -1481,7 +1863,7 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
     if (h == 0) return have ? last : NONE;
     if (h == 1) return (uint32_t)S;
     if (h == 2) return (uint32_t)E;
-    if (h == 3) return kn;
+    if (h == 3) return kn | (rec_exact ? 0x80000000u : 0u);
     if (h < 4 + KINL) {  // kill-log entry kn - KINL + (h - 4)
       const int64_t e = (int64_t)kn - KINL + (h - 4);
       return e >= 0 ? s_klast[e % KINL] : NONE;
@@ -1604,6 +1986,12 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
         // step's new members are not killed in the bvec yet: an edge bin with more alive
         // entries than that is nonempty after the kills.)
         const bool fast_after = wt.fb < A.nb && wt.bb < A.nb && cnt[wt.fb] > npend && cnt[wt.bb] > npend;
+        // When the window lengths take both edge bins whole -- no static position of bin fb is
+        // shorter than len * sim (kf = 0) and none of bin bb longer than len / sim (kble = its
+        // size) -- the fast window is [first alive of fb, last alive of bb]: every alive
+        // position of the span.  The record then says so and no part B follows (configs B and
+        // D: reads within 10 % of each other's length make every window such a span).
+        rec_exact = fast_after && wt.kf == 0 && (uint64_t)wt.kble == (uint64_t)(lo[wt.bb + 1] - lo[wt.bb]);
         step++;
         if (wv == 0) publish(fast_after ? lo[wt.fb] : 0, fast_after ? lo[wt.bb + 1] - 1 : A.N - 1, true);
         if (A.trace2 && threadIdx.x == 0 && step < TRACE_STEPS) A.trace[(uint64_t)step * TRACE_W + 6] = now();
@@ -1619,6 +2007,18 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
         }
         npend = 0;
         __syncthreads();
+      }
+      if (A.spec && rec_exact) {  // the span of the record is the window (alive after the kills)
+        S = lo[wt.fb];
+        E = lo[wt.bb + 1] - 1;
+        rec_exact = false;
+        if (A.prof && threadIdx.x == 0) {
+          const uint64_t t = now();
+          t_ws[1] += t - t_mark;
+          t_mark = t;
+        }
+        have = true;
+        break;
       }
       const bool fast = wt.fb < A.nb && wt.bb < A.nb && cnt[wt.fb] > 0 && cnt[wt.bb] > 0;
       int64_t count = 0;
@@ -1758,8 +2158,22 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
       t_wait += t - t_mark;
       t_mark = t;
     }
-    // block reduction: the first maximum, the flagged and scanned totals
-    wave_best_all(bv_, bp_, better);
+    // block reduction: the first maximum, the flagged and scanned totals (the wave's largest
+    // value by a max reduction; only equal values from several workers need the positions)
+    {
+      const double m = wave_ext_f64_all<true>(bv_);
+      const uint64_t hit = __ballot(bp_ != NONE64 && bv_ == m);
+      if (__popcll(hit) > 1) {
+        wave_best_all(bv_, bp_, better);
+      } else if (hit) {
+        const int L = __builtin_ctzll(hit);
+        bv_ = __builtin_bit_cast(double, readlane64(__builtin_bit_cast(uint64_t, bv_), L));
+        bp_ = readlane64(bp_, L);
+      } else {
+        bv_ = -1.0;
+        bp_ = NONE64;
+      }
+    }
     const uint32_t wscan = wave_sum32(scan_w), wflag = wave_sum32(cnt_w);
     if (lane == 0) {
       s_bv[wv] = bv_;
@@ -2061,16 +2475,16 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
                 fv[k] = F4[k0 + k];
               }
 #pragma unroll
-              for (int k = 0; k < HB; k++) acc.add(rv[k], fv[k]);
+              for (int k = 0; k < HB; k++) acc.add_sad(rv[k], fv[k]);  // (distance_d needs no dot product)
             }
           } else {
-            for (int k = 0; k < nch; k++) acc.add(row[k], F4[k]);
+            for (int k = 0; k < nch; k++) acc.add_sad(row[k], F4[k]);
           }
           mp = mc.info[q * 3];
           key = mc.key[q];
         } else {
           const uint64_t r = ld32(A.mem_pos + cl_start + q);
-          for (int k = 0; k < nch; k++) acc.add(A.hr[r * nch + k], F4[k]);
+          for (int k = 0; k < nch; k++) acc.add_sad(A.hr[r * nch + k], F4[k]);
           mp = A.mag_s[r];
           key = ld64(A.mkeys + cl_start + q);
         }
@@ -2083,15 +2497,23 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
           bq = q;
         }
       }
-      {  // first minimum by (distance, key); keys are unique, so the lane holding it gives q
-        double rd = bd;
-        uint64_t rk = bk;
-        wave_best_all(rd, rk, [](double a, uint64_t ka, double b, uint64_t kb) { return a < b || (a == b && ka < kb); });
-        const uint64_t hit = __ballot(bd == rd && bk == rk);
+      {  // first minimum by (distance, key); keys are unique, so the lane holding it gives q.
+         // The wave's smallest distance by a min reduction; only a tie between lanes needs the
+         // (distance, key) pair reduction
+        const double md = wave_ext_f64_all<false>(bd);
+        uint64_t hit = __ballot(bk != NONE64 && bd == md);
+        double rd = md;
+        uint64_t rk = NONE64;
+        if (__popcll(hit) > 1) {
+          rd = bd;
+          rk = bk;
+          wave_best_all(rd, rk, [](double a, uint64_t ka, double b, uint64_t kb) { return a < b || (a == b && ka < kb); });
+          hit = __ballot(bd == rd && bk == rk);
+        }
         const int L = hit ? __builtin_ctzll(hit) : 0;
-        bq = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(bq >> 32), L) << 32) |
-             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bq, L);
-        bd = rd;
+        if (hit) rk = readlane64(bk, L);
+        bq = readlane64(bq, L);
+        bd = hit ? rd : __builtin_inf();
         bk = rk;
       }
       if (lane == 0) {
@@ -2115,15 +2537,9 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
       if (A.prof && threadIdx.x == 0) t_sub[3] += now() - tq;
     } else if (best_pos != NONE64) {
       // is_min with a result: the best candidate seeds the next cluster (bvec::erase)
-      if (threadIdx.x == 0) {
-        bv.kill_one(best_pos);
-        log_kill(best_pos);
-      }
-      kn++;
-      __syncthreads();
       finish_cluster();
       last = (uint32_t)best_pos;
-      new_cluster(best_pos);
+      new_cluster(best_pos, true);
     } else {
       const uint64_t p = pop();
       finish_cluster();
@@ -2157,12 +2573,14 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
 // NCH: compile-time chunks per row (0: A.nch at run time).
 // CPT: streaming rows with per-chunk compaction (A.cc; the resident form compiled out)
 // DENSE: dense resident workers (worker_dense, DT-position tiles)
-template <typename T, int NCH, bool WIDE = false, bool CPT = false, bool DENSE = false>
+// DSTREAM: dense streaming workers (worker_dstream, DT-position tiles, rows in HBM)
+template <typename T, int NCH, bool WIDE = false, bool CPT = false, bool DENSE = false, bool DSTREAM = false>
 __global__ __launch_bounds__(NT) void accum_kernel(AccArgs A, DevClassifier C) {
   extern __shared__ __attribute__((aligned(16))) uint4 dyn[];
-  constexpr int TSZ = DENSE ? DT : WIDE ? NW : NT;
+  constexpr int TSZ = (DENSE || DSTREAM) ? DT : WIDE ? NW : NT;
   if (blockIdx.x == 0) controller<T, NCH, WIDE, TSZ>(A, dyn);
   else if constexpr (DENSE) worker_dense<T, NCH>(A, C, dyn);
+  else if constexpr (DSTREAM) worker_dstream<T, NCH>(A, C, dyn);
   else worker<T, NCH, WIDE, CPT>(A, C, dyn);
 }
 
@@ -2181,6 +2599,7 @@ struct AccPlan {
   bool wide = false;   // a wave per candidate (accum_kernel<T, 0, true>)
   bool compact = false;  // streaming rows with per-chunk compaction (A.cc)
   bool dense = false;    // dense resident workers (worker_dense)
+  bool dstream = false;  // dense streaming workers (worker_dstream)
   uint32_t mrow = 0;   // member cache entries
   size_t lds = 0;
   uint32_t G = 0;
@@ -2250,6 +2669,23 @@ bool accum_plan(const mc_ctx *c, uint32_t nb, AccPlan *pl) {
                              : reinterpret_cast<const void *>(&accum_kernel<uint16_t, 0, false, false, true>);
     }
   }
+  // dense streaming workers (config D on one to four GPUs): DT-position tiles, one dense list of
+  // at most SJ * NT entries per worker with its rows in HBM; MC_ACCUM_NO_DSTREAM keeps the
+  // 512-position-chunk streaming form
+  if (!pl->dense && !wide && nch <= DMAXCH && pl->res == 0 && !getenv("MC_ACCUM_NO_DSTREAM") &&
+      !getenv("MC_ACCUM_STREAM") && !getenv("MC_ACCUM_COMPACT")) {
+    const uint64_t dchunks = ((c->norder + DT - 1) / DT + W - 1) / W;
+    const uint64_t dper = (dchunks + GW - 1) / GW;
+    const size_t dfix = (size_t)(pl->rec_g + 3) / 4 * 16 + 2 * (size_t)((dper * DT + 3) / 4 * 4) * 4;
+    if (dper * DT <= (uint64_t)SJ * NT && dfix <= cap) {
+      pl->dstream = true;
+      pl->fcap = dper * DT;
+      wfix_dense = dfix;
+      pl->fn = c->width == 1 ? (nch == 16 ? reinterpret_cast<const void *>(&accum_kernel<uint8_t, 16, false, false, false, true>)
+                                          : reinterpret_cast<const void *>(&accum_kernel<uint8_t, 0, false, false, false, true>))
+                             : reinterpret_cast<const void *>(&accum_kernel<uint16_t, 0, false, false, false, true>);
+    }
+  }
   // streaming rows (config D): compacted per chunk by its worker, the slot list in LDS -- opt in
   // (MC_ACCUM_COMPACT): measured slower at D1M, accumulation 1060 -> 1424 ms (profiles/r03_v10)
   pl->compact = !pl->dense && !wide && nch == 16 && c->width == 1 && pl->res == 0 && per_w <= 64 && getenv("MC_ACCUM_COMPACT") &&
@@ -2271,7 +2707,7 @@ bool accum_plan(const mc_ctx *c, uint32_t nb, AccPlan *pl) {
     if (m >= 64 || (gb == 1 && m >= 1)) {
       pl->gbits = gb != 0;
       pl->mrow = (uint32_t)m;
-      pl->lds = std::max(f + m * per_entry, pl->dense ? wfix_dense
+      pl->lds = std::max(f + m * per_entry, (pl->dense || pl->dstream) ? wfix_dense
                                                       : wfix + (size_t)pl->res * chunk_bytes + (pl->compact ? pl->fcap * 2 : 0));
       return true;
     }
@@ -2294,9 +2730,9 @@ bool accum_plan_info(const mc_ctx *c, uint32_t nb, uint32_t info[4]) {
   AccPlan pl;
   if (!accum_plan(c, nb, &pl)) return false;
   info[0] = pl.G;
-  info[1] = pl.dense ? (uint32_t)DT : pl.wide ? (uint32_t)NW : (uint32_t)NT;  // the kernel's TSZ
+  info[1] = (pl.dense || pl.dstream) ? (uint32_t)DT : pl.wide ? (uint32_t)NW : (uint32_t)NT;  // the kernel's TSZ
   info[2] = (pl.dense ? 1u : 0u) | (pl.wide ? 2u : 0u) | (pl.res > 0 ? 4u : 0u) |
-            (!pl.dense && !pl.wide && pl.res == 0 ? 8u : 0u);
+            (!pl.dense && !pl.wide && pl.res == 0 ? 8u : 0u) | (pl.dstream ? 16u : 0u);
   info[3] = (uint32_t)pl.lds;
   return true;
 }
@@ -2339,8 +2775,11 @@ int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, 
     return MC_ERR_OOM;
   if (ensure(c->s_i, c->norder * sizeof(MInfo) + 64) || ensure(c->s_j, c->norder * (size_t)nch * 16 + 64))
     return MC_ERR_OOM;
-  // compacted row copies: one region of NT rows per local chunk (this rank's chunks)
-  const size_t cc_bytes = pl.compact ? (size_t)(pl.fcap / NT) * GW * NT * (size_t)nch * 16 : 0;
+  // compacted row copies: one region of NT rows per local chunk (this rank's chunks); or the
+  // dense streaming workers' two row buffers each
+  const size_t cc_bytes = pl.compact    ? (size_t)(pl.fcap / NT) * GW * NT * (size_t)nch * 16
+                          : pl.dstream ? (size_t)2 * GW * pl.fcap * (size_t)nch * 16
+                                       : 0;
   if (cc_bytes && ensure(c->s_k, cc_bytes)) return MC_ERR_OOM;
   MInfo *d_minfo = (MInfo *)c->s_i.p;
   uint4 *d_hr = (uint4 *)c->s_j.p;
@@ -2376,7 +2815,7 @@ int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, 
   A.go = (uint32_t *)c->s_a.p;
   A.ring = (uint64_t *)((char *)c->s_a.p + 256);
   A.ringb = A.ring + (size_t)RING * pl.rec_g;
-  A.spec = pl.dense && !getenv("MC_ACCUM_NO_SPEC") ? 1 : 0;
+  A.spec = (pl.dense || pl.dstream) && !getenv("MC_ACCUM_NO_SPEC") ? 1 : 0;
   A.poll1 = getenv("MC_ACCUM_POLL1") ? 1 : 0;
   A.rec_g = pl.rec_g;
   A.partials = (uint64_t *)c->s_b.p;
@@ -2386,6 +2825,7 @@ int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, 
   A.fcap = fcap;
   A.res = pl.res;
   A.cc = pl.compact ? (uint4 *)c->s_k.p : nullptr;
+  A.srows = pl.dstream ? (uint4 *)c->s_k.p : nullptr;
   A.mrow = pl.mrow;
   A.mem_pos = d_mem_pos;
   A.mkeys = d_mkeys;
@@ -2410,8 +2850,9 @@ int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, 
     A.trace2 = atoi(getenv("MC_ACCUM_PROFILE")) >= 4 ? (uint64_t *)((char *)c->s_h.p + tb) : nullptr;
   }
   if (getenv("MC_ACCUM_PROFILE"))
-    fprintf(stderr, "[accum] variant: width %d nch %d wide %d dense %d resident chunks/worker %d compact %d global-bitmap %d member-cache %u lds %zu G %u rank %u/%u\n",
-            c->width, nch, (int)pl.wide, (int)pl.dense, pl.res, (int)pl.compact, (int)pl.gbits, pl.mrow, pl.lds, G, A.rank, A.W);
+    fprintf(stderr, "[accum] variant: width %d nch %d wide %d dense %d dstream %d resident chunks/worker %d compact %d global-bitmap %d member-cache %u lds %zu G %u rank %u/%u fcap %llu\n",
+            c->width, nch, (int)pl.wide, (int)pl.dense, (int)pl.dstream, pl.res, (int)pl.compact, (int)pl.gbits, pl.mrow, pl.lds, G,
+            A.rank, A.W, (unsigned long long)pl.fcap);
   DevClassifier cls = c->cls;
   void *args[] = {&A, &cls};
   timed_begin(c);

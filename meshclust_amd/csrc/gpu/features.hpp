@@ -42,6 +42,12 @@ struct Acc<uint8_t> {
     d4[2] = __builtin_amdgcn_udot4(a.z, b.z, d4[2], false);
     d4[3] = __builtin_amdgcn_udot4(a.w, b.w, d4[3], false);
   }
+  __device__ __forceinline__ void add_sad(const uint4 &a, const uint4 &b) {  // (sum |p - q| only)
+    s4[0] = __builtin_amdgcn_sad_u8(a.x, b.x, s4[0]);
+    s4[1] = __builtin_amdgcn_sad_u8(a.y, b.y, s4[1]);
+    s4[2] = __builtin_amdgcn_sad_u8(a.z, b.z, s4[2]);
+    s4[3] = __builtin_amdgcn_sad_u8(a.w, b.w, s4[3]);
+  }
   __device__ __forceinline__ void fold() {
     sad += (s4[0] + s4[1]) + (s4[2] + s4[3]);
     dot += (d4[0] + d4[1]) + (d4[2] + d4[3]);
@@ -101,6 +107,29 @@ __device__ __forceinline__ uint64_t wave_sum64_all(uint64_t v) {
   const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 63);
   return ((uint64_t)hi << 32) | lo;
 }
+// max / min of a double over the wave (DPP moves of the two halves + v_max_f64 / v_min_f64),
+// in every lane; the value is one of the inputs, bit for bit
+template <bool MAX>
+__device__ __forceinline__ double wave_ext_f64_all(double v) {
+#define MCG_EXT_STEP(C, R)                                                                            \
+  {                                                                                                   \
+    const uint64_t vb = __builtin_bit_cast(uint64_t, v);                                              \
+    const uint64_t ov = ((uint64_t)dpp_mv<C, R>((uint32_t)(vb >> 32), (uint32_t)(vb >> 32)) << 32) |  \
+                        dpp_mv<C, R>((uint32_t)vb, (uint32_t)vb);                                     \
+    const double o = __builtin_bit_cast(double, ov);                                                  \
+    v = MAX ? __builtin_fmax(v, o) : __builtin_fmin(v, o);                                            \
+  }
+  MCG_DPP_STEPS(MCG_EXT_STEP)
+#undef MCG_EXT_STEP
+  const uint64_t vb = __builtin_bit_cast(uint64_t, v);
+  return __builtin_bit_cast(double, ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(vb >> 32), 63) << 32) |
+                                        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)vb, 63));
+}
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int L) {
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), L) << 32) |
+         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, L);
+}
+
 // the best (value, key) pair of the wave under a strict total order `better(a, ka, b, kb)`,
 // returned in every lane; V is double or uint64_t, keys uint64_t
 template <typename V, typename Better>
@@ -163,6 +192,7 @@ struct Acc {
       sdot += x * y;
     }
   }
+  __device__ __forceinline__ void add_sad(const uint4 &a, const uint4 &b) { add(a, b); }
   __device__ __forceinline__ void reduce16() {
 #pragma unroll
     for (int o = 8; o >= 1; o >>= 1) {

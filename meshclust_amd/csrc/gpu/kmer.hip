@@ -27,7 +27,7 @@
 // sum of squares and length, and the row maxima are reduced; the reference's largest-count
 // pass (Runner.cpp:57-67) is that maximum, so a second pass runs only when 8 bits do not hold
 // it.
-#include "mcgpu.hpp"
+#include "features.hpp"
 
 namespace mcg {
 
@@ -199,10 +199,52 @@ __device__ __forceinline__ void tab_drain(bool glob) {
 
 // Row of sequence s from the summed tables tabs[0..ntab) (stride B): write (width T) + stats;
 // the calling wave only.  Zeroes the tables for the next sequence.
+// 8-bit rows from one LDS table with B a multiple of 256 (k >= 4): every lane takes 32-bit
+// words of the row (four bins: one 16-byte LDS read and one zeroing write), the wave's stores
+// are 256 contiguous bytes, and the magnitude / sum of squares / maximum are DPP reductions
+__device__ __forceinline__ void write_row8(const KArgs &A, uint64_t s, uint32_t *tab, int B, bool write, uint64_t *wmax) {
+  const int lane = threadIdx.x & 63;
+  uint32_t m = 0, mx = 0;  // (a magnitude is the record's k-mer count + B: 32 bits below 4 Gb)
+  uint64_t sq64 = 0;
+  uint8_t *row = A.hist + s * A.pitch;
+  for (int q = lane; q < B / 4; q += 64) {
+    uint4 c = reinterpret_cast<const uint4 *>(tab)[q];
+    reinterpret_cast<uint4 *>(tab)[q] = make_uint4(0, 0, 0, 0);
+    c.x += 1;  // pseudocount (ClusterFactory.cpp:995)
+    c.y += 1;
+    c.z += 1;
+    c.w += 1;
+    m += c.x + c.y + c.z + c.w;
+    sq64 += (uint64_t)c.x * c.x + (uint64_t)c.y * c.y + (uint64_t)c.z * c.z + (uint64_t)c.w * c.w;
+    mx = max(max(c.x, c.y), max(max(c.z, c.w), mx));
+    if (write) reinterpret_cast<uint32_t *>(row)[q] = (c.x & 0xffu) | (c.y & 0xffu) << 8 | (c.z & 0xffu) << 16 | (c.w & 0xffu) << 24;
+  }
+  if (write)  // the row's padding up to the pitch
+    for (uint64_t b = (uint64_t)B + lane; b < A.pitch; b += 64) row[b] = 0;
+  const uint64_t m64 = wave_sum64_all(m), s64 = wave_sum64_all(sq64);
+  uint32_t wm = mx;
+#define MCG_MAX_STEP(C, R) wm = max(wm, dpp_mv<C, R>(wm, wm));
+  MCG_DPP_STEPS(MCG_MAX_STEP)
+#undef MCG_MAX_STEP
+  wm = (uint32_t)__builtin_amdgcn_readlane((int)wm, 63);
+  if (lane == 0 && write) {
+    A.mag[s] = m64;
+    A.sumsq[s] = s64;
+    A.len_out[s] = A.seq_off[s + 1] - A.seq_off[s];
+  }
+  *wmax = wm > *wmax ? wm : *wmax;
+}
+
 template <typename T>
 __device__ __forceinline__ void write_row(const KArgs &A, uint64_t s, uint32_t *tab0, int ntab, int B, bool write,
                                           bool glob, uint64_t *wmax) {
   const int lane = threadIdx.x & 63;
+  if constexpr (sizeof(T) == 1) {
+    if (ntab == 1 && !glob && (B & 255) == 0) {
+      write_row8(A, s, tab0, B, write, wmax);
+      return;
+    }
+  }
   constexpr int per = 16 / (int)sizeof(T);  // bins per 16-byte store
   uint64_t m = 0, sq = 0, mx = 0;
   uint8_t *row = A.hist + s * A.pitch;

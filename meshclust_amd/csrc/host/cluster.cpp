@@ -170,8 +170,11 @@ void sharded_step(mc_ctx *ctx, const ShardComm &comm, uint32_t centre, uint64_t 
   mine.n_flagged = (uint32_t)loc.n_flagged;
   memcpy(mine.flagged, flag_buf.data(), std::min<uint64_t>(loc.n_flagged, ShardBlock::kInline) * 4);
   std::vector<ShardBlock> all(W);
-  if (comm.allgather(comm.user, &mine, sizeof mine, all.data()) != 0)
+  if (comm.allgather(comm.user, &mine, sizeof mine, all.data()) != 0) {
+    // (a peer that saw this rank's failure may end the exchange first: the cause is ours)
+    if (!scan_err.empty()) throw Error(scan_err, 1);
     throw PeerError("get_close all-gather across ranks failed");
+  }
   for (int r = 0; r < W; r++)
     if (all[r].failed) {
       if (scan_err.empty()) throw PeerError("get_close failed on rank " + std::to_string(r));
@@ -532,8 +535,11 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
         ms_err = e.what();
         mine[0] = 1;
       }
-      if (cfg.comm->allgather(cfg.comm->user, mine.data(), (uint64_t)blk * 4, all.data()) != 0)
+      if (cfg.comm->allgather(cfg.comm->user, mine.data(), (uint64_t)blk * 4, all.data()) != 0) {
+        // (a peer that saw this rank's failure may end the exchange first: the cause is ours)
+        if (!ms_err.empty()) throw Error(ms_err, 1);
         throw PeerError("centre all-gather across ranks failed");
+      }
       for (uint32_t r = 0; r < W; r++)
         if (all[(size_t)r * blk]) {
           if (ms_err.empty()) throw PeerError("mean-shift update failed on rank " + std::to_string(r));

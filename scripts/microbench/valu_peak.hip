@@ -1,5 +1,6 @@
 // valu_peak.hip -- the gfx950 VALU issue rate for the 32-bit integer instruction classes the NW
-// kernel's cell update is made of: independent streams of one instruction,
+// kernel's cell update and the accumulation scan are made of: independent
+// streams of one instruction (the compare + select pair counts as one "instruction" here),
 // at 1, 2, 4 and 8 waves per SIMD.  Prints lane-instructions per clock per CU and per second
 // (the NW roofline's peak, bench.py nw_roofline).  Each thread runs 8 independent register
 // chains so no instruction waits on its predecessor's result.
@@ -29,7 +30,17 @@ __device__ __forceinline__ void op(uint32_t &a, uint32_t b, uint32_t c) {
   else if constexpr (OP == 3) asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(a) : "v"(b), "v"(c));
   else if constexpr (OP == 4) asm volatile("v_pk_add_u16 %0, %0, %1" : "+v"(a) : "v"(b));
   else if constexpr (OP == 5) asm volatile("v_pk_max_i16 %0, %0, %1" : "+v"(a) : "v"(b));
-  else asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(a) : "v"(b) : "vcc");
+  else if constexpr (OP == 6) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(a) : "v"(b) : "vcc");
+  else if constexpr (OP == 7) asm volatile("v_cndmask_b32_e64 %0, %0, %1, s[20:21]" : "+v"(a) : "v"(b) : "s20", "s21");
+  else if constexpr (OP == 8)  // the select pattern: a compare into an SGPR pair, then a select on it
+    asm volatile("v_cmp_gt_i32_e64 s[22:23], %0, %1\n\tv_cndmask_b32_e64 %0, %0, %1, s[22:23]" : "+v"(a) : "v"(b) : "s22", "s23");
+  else if constexpr (OP == 9) asm volatile("v_bfi_b32 %0, %1, %0, %2" : "+v"(a) : "v"(b), "v"(c));
+  else if constexpr (OP == 10) asm volatile("v_sad_u8 %0, %1, %2, %0" : "+v"(a) : "v"(b), "v"(c));
+  else if constexpr (OP == 11) asm volatile("v_dot4_u32_u8 %0, %1, %2, %0" : "+v"(a) : "v"(b), "v"(c));
+  else if constexpr (OP == 12) asm volatile("v_mov_b32 %0, %1" : "=v"(a) : "v"(b));
+  else if constexpr (OP == 13) asm volatile("v_sub_u32 %0, %0, %1" : "+v"(a) : "v"(b));
+  else if constexpr (OP == 14) asm volatile("v_max_u32 %0, %0, %1" : "+v"(a) : "v"(b));
+  else asm volatile("v_and_or_b32 %0, %0, %1, %2" : "+v"(a) : "v"(b), "v"(c));
 }
 
 template <int OP>
@@ -84,10 +95,13 @@ int main() {
   CHECK(hipGetDeviceProperties(&p, 0));
   const int cus = p.multiProcessorCount;
   const double clk = p.clockRate / 1e3;  // MHz (peak engine clock)
-  const char *names[7] = {"v_add_u32", "v_max_i32", "v_max3_i32", "v_add3_u32", "v_pk_add_u16", "v_pk_max_i16", "v_cndmask_b32"};
+  constexpr int NOPS = 16;
+  const char *names[NOPS] = {"v_add_u32", "v_max_i32", "v_max3_i32", "v_add3_u32", "v_pk_add_u16", "v_pk_max_i16",
+                             "v_cndmask_b32 (vcc)", "v_cndmask_b32_e64 (sgpr pair)", "v_cmp_gt_i32_e64 + v_cndmask_b32_e64 (pair)",
+                             "v_bfi_b32", "v_sad_u8", "v_dot4_u32_u8", "v_mov_b32", "v_sub_u32", "v_max_u32", "v_and_or_b32"};
   printf("{\"device\": \"%s\", \"cus\": %d, \"clock_mhz\": %.0f, \"results\": [\n", p.gcnArchName, cus, clk);
   bool first = true;
-  for (int o = 0; o < 7; o++) {
+  for (int o = 0; o < NOPS; o++) {
     for (int w : {1, 2, 4, 8}) {
       double r = 0;
       switch (o) {
@@ -97,7 +111,16 @@ int main() {
         case 3: r = run<3>(w, cus, nullptr); break;
         case 4: r = run<4>(w, cus, nullptr); break;
         case 5: r = run<5>(w, cus, nullptr); break;
-        default: r = run<6>(w, cus, nullptr); break;
+        case 6: r = run<6>(w, cus, nullptr); break;
+        case 7: r = run<7>(w, cus, nullptr); break;
+        case 8: r = run<8>(w, cus, nullptr); break;
+        case 9: r = run<9>(w, cus, nullptr); break;
+        case 10: r = run<10>(w, cus, nullptr); break;
+        case 11: r = run<11>(w, cus, nullptr); break;
+        case 12: r = run<12>(w, cus, nullptr); break;
+        case 13: r = run<13>(w, cus, nullptr); break;
+        case 14: r = run<14>(w, cus, nullptr); break;
+        default: r = run<15>(w, cus, nullptr); break;
       }
       printf("%s {\"inst\": \"%s\", \"waves_per_simd\": %d, \"lane_insts_per_s\": %.4e, \"lane_insts_per_clk_per_cu\": %.2f}",
              first ? "" : ",\n", names[o], w, r, r / (clk * 1e6) / cus);

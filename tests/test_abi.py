@@ -40,8 +40,11 @@ def test_libmcgpu_loads_and_has_gfx950_code(product):
     assert lib.mc_abi_version() == 1
     # the bundled device code object targets gfx950
     import tempfile
-    with tempfile.TemporaryDirectory() as td:
-        r = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", M.GPU_LIB],
+    import shutil
+    with tempfile.TemporaryDirectory() as td:  # (--offloading extracts the bundles next to its input)
+        lib = os.path.join(td, "libmcgpu.so")
+        shutil.copyfile(M.GPU_LIB, lib)
+        r = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", lib],
                            capture_output=True, text=True, cwd=td)
     assert "amdgcn-amd-amdhsa--gfx950" in r.stdout + r.stderr
 

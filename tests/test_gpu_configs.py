@@ -118,13 +118,24 @@ def test_config_B100k_accum_variants_equal_reference(product, env, tag):
     assert st["accum_path"] == "device"
 
 
-@pytest.mark.parametrize("env", [{}, {"MC_ACCUM_STEPS": "1"}])
+@pytest.mark.parametrize("env,tag", [({"MC_ACCUM_GRID": "64"}, ".g64"), ({"MC_ACCUM_GRID": "32"}, ".g32"),
+                                     ({"MC_ACCUM_GRID": "64", "MC_ACCUM_NO_DSTREAM": "1"}, ".g64chunks")])
+def test_config_B100k_streaming_forms_equal_reference(product, env, tag):
+    """The streaming accumulation forms config D takes on one to four GPUs, forced at config B by a
+    small grid (more candidates per worker than one workgroup holds): the dense streaming workers
+    (one position-ordered list per worker, rows in HBM, rebuilt as candidates die) at 63 and 31
+    workers, and the 512-position-chunk streaming form (MC_ACCUM_NO_DSTREAM)."""
+    st = _big("B100k", product, 300, env=env, tag=tag)
+    assert st["accum_path"] == "device"
+
+
+@pytest.mark.parametrize("env", [{}, {"MC_ACCUM_STEPS": "1"}, {"MC_ACCUM_GRID": "64"}])
 def test_config_D100k_partition_equals_reference(product, env):
     """Config D's shape (10 reads per template, 10,000 clusters) at 100k reads: the device loop
     and the host-driven steps against the reference's own partition (tests/golden/cfg_D100k.npz,
     oracle/_ref/meshclust --threads 1, 48 min here)."""
-    st = _big("D100k", product, 300, env=env, tag=".steps" if env else "")
-    assert st["accum_path"] == ("device" if not env else "steps (MC_ACCUM_STEPS)")
+    st = _big("D100k", product, 300, env=env, tag=".steps" if "MC_ACCUM_STEPS" in env else ".g64" if env else "")
+    assert st["accum_path"] == ("steps (MC_ACCUM_STEPS)" if "MC_ACCUM_STEPS" in env else "device")
 
 
 def _partition(path):
@@ -158,9 +169,77 @@ def test_config_D1M_properties():
     st2 = _run(fa, flags, out_steps, 900, env={"MC_ACCUM_STEPS": "1"})
     got2, _ = _partition(out_steps)
     assert BG.canonical_digest(got2) == BG.canonical_digest(got)
+    # the 512-position-chunk streaming form (the dense streaming workers are the default here)
+    out_chk = fa[:-3] + ".chunks.clstr"
+    st4 = _run(fa, flags, out_chk, 600, env={"MC_ACCUM_NO_DSTREAM": "1"})
+    assert st4["accum_path"] == "device", st4["accum_path"]
+    got4, _ = _partition(out_chk)
+    assert BG.canonical_digest(got4) == BG.canonical_digest(got)
     # the streaming form's opt-in per-chunk compaction of alive rows (MC_ACCUM_COMPACT)
     out_cmp = fa[:-3] + ".compact.clstr"
     st3 = _run(fa, flags, out_cmp, 600, env={"MC_ACCUM_COMPACT": "1"})
     assert st3["accum_path"] == "device", st3["accum_path"]
     got3, _ = _partition(out_cmp)
     assert BG.canonical_digest(got3) == BG.canonical_digest(got)
+
+
+def _properties(path, n):
+    """Every read in exactly one cluster, every centre one of its own cluster's members."""
+    got, ids = _partition(path)
+    assert len(ids) == n and np.array_equal(np.sort(ids), np.arange(n))
+    centres = [c for c, _ in got]
+    assert None not in centres and len(set(centres)) == len(centres)
+    assert all(c in m for c, m in got)
+    return got
+
+
+def _families_input(name, *gen):
+    fa = os.path.join(_cache_dir(), "%s.fa" % name)
+    if not os.path.exists(fa):
+        synth.write_fasta(fa + ".tmp", synth.families(*gen))
+        os.replace(fa + ".tmp", fa)
+    return fa
+
+
+@pytest.mark.timeout(900)
+def test_config_E9100_properties(product):
+    """Config E scaled (70 families x 130 genomes, 8-12 kb, k = 6, --id 0.80: the input that
+    gives 8 GPUs work).  No reference partition exists at this size (the reference needs hours):
+    the partition must be a partition with member centres, and identical across the accumulation
+    kernel's wide form, its lane-per-candidate form (MC_ACCUM_NARROW), the host-driven get_close
+    steps, and the NW kernels' forms (every batch in the throughput form / in the 8-wave latency
+    form).  E91 pins these forms against the reference (test_config_E91_partition_equals_reference)."""
+    fa = _families_input("E9100", 70, 130, 8000, 12000, 0.05, 0.15, 61)
+    base = fa[:-3] + ".clstr"
+    st = _run(fa, ["--id", "0.80"], base, 600)
+    assert st["k"] == 6 and st["n"] == 9100 and st["accum_path"] == "device"
+    want = BG.canonical_digest(_properties(base, 9100))
+    for tag, env in (("narrow", {"MC_ACCUM_NARROW": "1"}), ("steps", {"MC_ACCUM_STEPS": "1"}),
+                     ("nwtp", {"MC_NW_MW_MAX": "0"}), ("nw8", {"MC_NW_MW_MAX": "100000000", "MC_NW_WAVES": "8"})):
+        out = fa[:-3] + "." + tag + ".clstr"
+        _run(fa, ["--id", "0.80"], out, 600, env)
+        assert BG.canonical_digest(_properties(out, 9100)) == want, tag
+
+
+@pytest.mark.timeout(900)
+def test_config_C20k_align_properties(product):
+    """Config C's shape at 20k reads (200 templates, --id 0.55 --align: one NW alignment per centre
+    x candidate through the memo replay).  The reference needs days at 100k; its
+    partitions at 2k reads of this shape are the e2e_c2k goldens.  Here: a partition with member
+    centres, identical whether every NW batch runs in the one-wave throughput form
+    (MC_NW_MW_MAX=0), in the 4-wave or the 8-wave latency form."""
+    gen = (20000, 1000, 200, 0.03, 41)
+    fa = os.path.join(_cache_dir(), "C20k.fa")
+    if not os.path.exists(fa):
+        synth.generate(fa + ".tmp", *gen)
+        os.replace(fa + ".tmp", fa)
+    flags = ["--id", "0.55", "--align"]
+    base = fa[:-3] + ".clstr"
+    st = _run(fa, flags, base, 600)
+    assert st["accum_path"] == "steps (alignment mode)" and st["align_nw_pairs"] > 0
+    want = BG.canonical_digest(_properties(base, gen[0]))
+    for tag, env in (("tp", {"MC_NW_MW_MAX": "0"}), ("w4", {"MC_NW_MW_MAX": "100000000", "MC_NW_WAVES": "4"}),
+                     ("w8", {"MC_NW_MW_MAX": "100000000", "MC_NW_WAVES": "8"})):
+        out = fa[:-3] + "." + tag + ".clstr"
+        _run(fa, flags, out, 600, env)
+        assert BG.canonical_digest(_properties(out, gen[0])) == want, tag
