@@ -289,9 +289,10 @@ def main():
     scan_evals = sum(s["scan_candidates"] for s in stats)
     dominant = max(fam_ms, key=lambda f: fam_ms[f])
     roof = None
+    acc_split = shard and str(s0.get("accum_path", "")).startswith("device x")  # (vs replicated)
     if fam_n["scan"]:
-        # (sharded: each rank's kernel scans its 1/world of every window)
-        per_launch_bytes = scan_evals * eval_bytes / fam_n["scan"] / (world if shard else 1)
+        # (accumulation split over the ranks: each rank's kernel scans its 1/world of every window)
+        per_launch_bytes = scan_evals * eval_bytes / fam_n["scan"] / (world if acc_split else 1)
         avg_s = fam_ms["scan"] / fam_n["scan"] / 1e3
         ach = per_launch_bytes / avg_s / 1e9
         # one launch per clustering = the device-resident accumulation (accum.hip); otherwise
@@ -374,8 +375,11 @@ def main():
                    "workload_config": a.workload, "mode": mode,
                    "reads": a.n * (world if replicas else 1), "read_len": a.len, "k": s0["k"],
                    "histogram_bits": 8 * width,
-                   "parallelism": ("one clustering sharded by record x%d (device mailbox exchange per get_close "
-                                   "step, RCCL all-gather per mean-shift iteration)" % world) if shard
+                   "parallelism": ("one clustering over %d GPUs: accumulation %s; training pivots / labels and "
+                                   "every mean-shift iteration split by rank, RCCL all-gathers"
+                                   % (world, "sharded by record (device mailbox exchange per get_close step)" if acc_split
+                                      else "replicated (every row resident in one GPU's LDS: the per-step exchange "
+                                           "would lengthen the chain)")) if shard
                    else "replicas x%d" % world if replicas else "single GPU"},
         "roofline": roof,
         "cpu_baseline": cpu,

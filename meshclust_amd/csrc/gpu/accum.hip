@@ -133,6 +133,7 @@ struct AccArgs {
   uint64_t *ringb;  // spec: RING x 2 granules, the exact window {S, E} of step s (NONE: no scan)
   int spec;         // the record carries a superset of the window; the exact one follows (dense)
   int poll1;        // the controller polls a partial's tag granule before loading it whole
+  int psleep;       // s_sleep between the controller's polls of a partial (0, 1, 2, 4)
   uint32_t rec_g;
   uint64_t *klog;      // static positions killed by the controller (pop / erase), append-only,
                        // entry e a granule tagged e + 1 (a reader checks the tag: no drain
@@ -2130,7 +2131,10 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
           s_abort = 1;
           break;
         }
-        __builtin_amdgcn_s_sleep(1);
+        // (MC_ACCUM_POLL_SLEEP: the pause between two polls of a partial, 64-clock units)
+        if (A.psleep == 1) __builtin_amdgcn_s_sleep(1);
+        else if (A.psleep == 2) __builtin_amdgcn_s_sleep(2);
+        else if (A.psleep == 4) __builtin_amdgcn_s_sleep(4);
       }
       if (!s_abort) {
         bv_ = __longlong_as_double((long long)((g8[0] << 32) | (g8[1] & 0xffffffffull)));
@@ -2817,6 +2821,7 @@ int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, 
   A.ringb = A.ring + (size_t)RING * pl.rec_g;
   A.spec = (pl.dense || pl.dstream) && !getenv("MC_ACCUM_NO_SPEC") ? 1 : 0;
   A.poll1 = getenv("MC_ACCUM_POLL1") ? 1 : 0;
+  A.psleep = getenv("MC_ACCUM_POLL_SLEEP") ? atoi(getenv("MC_ACCUM_POLL_SLEEP")) : 1;
   A.rec_g = pl.rec_g;
   A.partials = (uint64_t *)c->s_b.p;
   char *sc = (char *)c->s_c.p;

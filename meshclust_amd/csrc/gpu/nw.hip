@@ -414,12 +414,12 @@ __global__ __launch_bounds__(64 * W) void nw_mw_kernel(NWPairs q) {
 // measured fastest; longer pairs (config E's 8-12 kb genomes) run eight (two waves per SIMD,
 // one wave's dependent-issue stalls filled by the other's cells): 14 % less end-to-end time
 // on the 10 kb sets, while eight waves on 1 kb pairs cost 7 % more NW time (profiles/
-// r01_v7_nw_waves.txt).  MC_NW_WAVES = 4, 8 or 16 forces one width for every pair.
+// r01_v7_nw_waves.txt).  MC_NW_WAVES = 2, 4, 8 or 16 forces one width for every pair.
 inline int mw_waves(uint64_t la) {
   static const int forced = [] {
     const char *e = getenv("MC_NW_WAVES");
     const int v = e ? atoi(e) : 0;
-    return v == 4 || v == 8 || v == 16 ? v : 0;
+    return v == 2 || v == 4 || v == 8 || v == 16 ? v : 0;
   }();
   return forced ? forced : la <= 1024 ? 4 : 8;
 }
@@ -436,6 +436,7 @@ template <int R, typename P>
 int launch_bucket_mw(mc_ctx *c, NWPairs q, int waves) {
   if (q.npairs == 0) return MC_OK;
   switch (waves) {
+    case 2: nw_mw_kernel<R, P, 2><<<q.npairs, 128, 0, c->stream>>>(q); break;
     case 4: nw_mw_kernel<R, P, 4><<<q.npairs, 256, 0, c->stream>>>(q); break;
     case 16: nw_mw_kernel<R, P, 16><<<q.npairs, 1024, 0, c->stream>>>(q); break;
     default: nw_mw_kernel<R, P, 8><<<q.npairs, 512, 0, c->stream>>>(q); break;
@@ -459,7 +460,7 @@ int launch_nw(mc_ctx *c, const uint8_t *d_A, const uint64_t *d_aoff, const uint3
     return e ? (uint64_t)atoll(e) : (uint64_t)1024;
   }();
   const bool mw = m < mw_max;
-  enum { NB = 24 };  // latency form: (R, payload) x waves 4 / 8 / 16
+  enum { NB = 32 };  // latency form: (R, payload) x waves 2 / 4 / 8 / 16
   int bucket_waves[NB] = {0};
   std::vector<uint32_t> bucket[NB];
   std::vector<uint64_t> boff[NB];
@@ -481,7 +482,7 @@ int launch_nw(mc_ctx *c, const uint8_t *d_A, const uint64_t *d_aoff, const uint3
       const int wv = mw_waves(la);
       const uint64_t w64 = 64ull * wv;  // rows of R = 1
       r = la <= w64 ? 0 : la <= 2 * w64 ? 1 : la <= 4 * w64 ? 2 : 3;  // R = 1, 2, 4, 8 over the waves
-      bk = r + (wide ? 4 : 0) + (wv == 4 ? 0 : wv == 8 ? 8 : 16);
+      bk = r + (wide ? 4 : 0) + (wv == 2 ? 24 : wv == 4 ? 0 : wv == 8 ? 8 : 16);
       bucket_waves[bk] = wv;
       rows = w64 << r;
     } else {

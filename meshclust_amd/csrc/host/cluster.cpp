@@ -12,6 +12,7 @@
 #include <cfloat>
 #include <cstdio>
 #include <cstdlib>
+#include <atomic>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -409,13 +410,35 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
   // MC_SHARD_FORCE=1 (tests) takes the sharded code path with a single rank too.
   const bool multi = cfg.comm && (cfg.comm->world > 1 || getenv("MC_SHARD_FORCE"));
   const ShardComm *shard = (multi && !memo && cfg.width <= 2 && !getenv("MC_SHARD_REPLICATE")) ? cfg.comm : nullptr;
+  // The accumulation is split over the ranks only when one GPU would stream its rows from HBM
+  // (more reads than the dense resident form holds in the workers' LDS: ~130k on 256 CUs).
+  // Below that a get_close step is bound by its latency chain -- hand-offs, fan-in, collect --
+  // not by the scan the ranks would split, and the per-step mailbox exchange between GPUs would
+  // lengthen the chain: every rank then runs the whole (identical) chain itself, while the
+  // training and the mean-shift iterations stay sharded.  MC_SHARD_ACCUM=1 shards at any size
+  // (tests); the ranks take the same decision (one all-gather).
+  const char *force_acc = getenv("MC_SHARD_ACCUM");
+  if (shard && cfg.comm->world > 1 && !(force_acc && *force_acc && strcmp(force_acc, "0") != 0) && !getenv("MC_SHARD_FORCE")) {
+    uint32_t info[4] = {0, 0, 0, 0};
+    const int32_t fits = mc_accum_plan_info(ctx, (uint32_t)bv.bins().size(), info) == MC_OK && (info[2] & 1u) ? 1 : 0;
+    std::vector<int32_t> all(cfg.comm->world);
+    if (cfg.comm->allgather(cfg.comm->user, &fits, sizeof fits, all.data()) != 0)
+      throw PeerError("all-gather across ranks failed");
+    bool every = true;
+    for (int32_t f : all) every &= f != 0;
+    if (every) shard = nullptr;
+  }
   // Sharded ranks run ONE device-resident loop together: every rank's persistent kernel
   // scans its tiles and the kernels exchange each step through the shared mailbox
   // (mc_set_mailbox); MC_SHARD_HOST_STEPS=1, or a mailbox that cannot be attached on every
   // rank, keeps the host-driven sharded steps (mc_scan_part + all-gather + mc_scan_commit).
   fault_point(cfg.comm, "accumulate");
   SharedMailbox mbox;
-  const bool dev_shard = shard && !getenv("MC_SHARD_HOST_STEPS") && !getenv("MC_ACCUM_STEPS") &&
+  // (a mailbox whose hand-offs once timed out on these ranks is not tried again by this process:
+  // every clustering after the first goes straight to the host-driven sharded steps; all ranks
+  // saw the same timeout, so they agree)
+  static std::atomic<bool> mailbox_failed{false};
+  const bool dev_shard = shard && !getenv("MC_SHARD_HOST_STEPS") && !getenv("MC_ACCUM_STEPS") && !mailbox_failed.load() &&
                          attach_mailbox(*shard, ctx, order.size(), (uint32_t)bv.bins().size(), mbox);
   // The device-resident loop (mc_accumulate) unless alignment mode or the configuration
   // asks for the step API; MC_ACCUM_STEPS=1 forces the host-driven loop (both are GPU paths).
@@ -457,6 +480,7 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
         fprintf(stderr, "meshclust: device-sharded accumulation: the ranks' mailbox hand-offs timed out; "
                         "taking the host-driven sharded steps\n");
         mbox_note = " (mailbox timed out)";
+        mailbox_failed.store(true);
         rc = MC_ERR_UNSUPPORTED;
       } else if (worst != MC_OK && worst != MC_ERR_UNSUPPORTED) {
         // a real failure somewhere: this rank's own error goes to check() below with its message
@@ -475,7 +499,9 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
       timer.add("accumulate.dev_wait", st[3] / 1000.0);
       timer.add("accumulate.dev_collect", st[4] / 1000.0);
       done = true;
-      stats.accum_path = dev_shard ? "device x" + std::to_string(shard->world) : "device";
+      stats.accum_path = dev_shard                              ? "device x" + std::to_string(shard->world)
+                         : (multi && cfg.comm->world > 1) ? "device (replicated x" + std::to_string(cfg.comm->world) + ")"
+                                                          : "device";
     } else if (rc != MC_ERR_UNSUPPORTED) {
       check(rc, "mc_accumulate");
     } else if (dev_shard) {  // (every rank: the same configuration) -> the host-driven sharded steps

@@ -35,7 +35,10 @@ def _launch(fa, flags, out, gpu, world, rccl=False, env_extra=None, timeout=600,
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), WORKER]
     cmd += (["--gpu"] if gpu else []) + (["--rccl"] if rccl else []) + list(worker_args) + [fa, out, "--"] + flags
-    env = dict(os.environ, OMP_NUM_THREADS="2", **(env_extra or {}))
+    # (MC_SHARD_ACCUM: split the accumulation over the ranks even where one GPU holds every row
+    # resident -- the product replicates it there, cluster.cpp -- so the mailbox path is tested)
+    env = dict(os.environ, OMP_NUM_THREADS="2", MC_SHARD_ACCUM="1")
+    env.update(env_extra or {})
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     ranks = [json.load(open(out + ".rank%d.json" % i)) for i in range(world)]
@@ -191,7 +194,7 @@ def test_sharded_uneven_grids_B100k_equals_reference(tmp_path):
 
 def _bench_line(extra_env, args, timeout=900):
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
-                       timeout=timeout, env=dict(os.environ, **extra_env))
+                       timeout=timeout, env={**os.environ, "MC_SHARD_ACCUM": "1", **extra_env})
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     return json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
 
@@ -213,6 +216,18 @@ def test_bench_two_ranks_one_gpu_D100k(tmp_path):
     got = BG.clusters_of(keep)
     assert sorted(c for c, _ in got) == [int(x) for x in g["centres"]]
     assert BG.canonical_digest(got) == str(g["digest"])
+
+
+@pytest.mark.gpu
+def test_world2_replicated_accumulation_byte_identical(tmp_path):
+    """Without MC_SHARD_ACCUM the ranks replicate the accumulation when one GPU holds every row
+    resident (here: 3k reads), sharding the training and the mean shift only."""
+    fa, flags = fixtures.e2e_input("big2_3k", tmp_path)
+    out = str(tmp_path / "big2_3k.clstr")
+    ranks = _launch(fa, flags, out, True, 2, False, {"MC_SHARD_ACCUM": ""})
+    assert ranks[0]["accum_path"] == "device (replicated x2)", ranks[0]["accum_path"]
+    with gzip.open(fixtures.golden("e2e_big2_3k.clstr.gz"), "rb") as f:
+        assert open(out, "rb").read() == f.read()
 
 
 # ---- boxes with two or more GPUs (the driver's multi-GPU node): one rank per GPU ------------
@@ -270,7 +285,7 @@ def _cli(binary, name, tmp_path, devices, env_extra=None, timeout=600):
     st = out + ".json"
     r = subprocess.run([binary, fa] + flags + ["--devices", devices, "--output", out, "--stats-json", st, "--quiet",
                         "--threads", "4"], capture_output=True, text=True, timeout=timeout,
-                       env=dict(os.environ, **(env_extra or {})))
+                       env={**os.environ, "MC_SHARD_ACCUM": "1", **(env_extra or {})})
     return r, out, st
 
 
