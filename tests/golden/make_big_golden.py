@@ -46,8 +46,9 @@ BIG = {
 
 
 def read_id(header):
-    """'>read123 template_4' -> 123"""
-    return int(header[1:].split(" ", 1)[0][4:])
+    """'>read123 template_4' -> 123 ('>genome5221 family_41' -> 5221: the first number)"""
+    name = header[1:].split(" ", 1)[0]
+    return int(name[len(name.rstrip("0123456789")):])
 
 
 def clusters_of(clstr_path):
