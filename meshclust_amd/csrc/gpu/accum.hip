@@ -2617,7 +2617,11 @@ uint32_t accum_grid(const mc_ctx *c) {
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess) cus = 256;
   // MC_ACCUM_GRID (tests): fewer workgroups, e.g. two ranks' kernels sharing one GPU
   if (const char *g = getenv("MC_ACCUM_GRID")) cus = std::min(cus, atoi(g));
-  if (c->mb_world > 0 && c->mb_share > 1) cus /= c->mb_share;  // ranks sharing this GPU
+  // ranks sharing this GPU (tests): each takes its share of the CUs less one per XCD -- the
+  // kernels are launched plainly at different times, and a workgroup the dispatcher places on
+  // a busier XCD must still find a free CU there (round-robin XCD placement is observed, not
+  // promised: two exactly-fitting grids once left one workgroup waiting for the other kernel)
+  if (c->mb_world > 0 && c->mb_share > 1) cus = cus / c->mb_share - 8;
   // mc_set_accum_grid: ranks sharing a mailbox run the smallest grid among them, so that every
   // rank derives the same tile of ownership from it (accum_plan's dense test depends on G)
   if (c->acc_grid > 0) cus = std::min<int>(cus, (int)c->acc_grid);
