@@ -1112,6 +1112,8 @@ int mc_accumulate(mc_ctx *c, const uint32_t *bin_lo, const uint64_t *bounds, uin
             "(stragglers+reduce %.3f column sums %.3f [takes %.3f] mean %.3f closest %.3f) ms\n",
             (unsigned long long)out[1], out[5] / 1e5, out[12] / 1e5, out[13] / 1e5, out[14] / 1e5, out[6] / 1e5,
             out[7] / 1e5, out[8] / 1e5, out[9] / 1e5, out[15] / 1e5, out[10] / 1e5, out[11] / 1e5);
+    fprintf(stderr, "[accum] closest: members scored %.3f, reduced %.3f, winner %.3f ms\n", out[18] / 1e5, out[19] / 1e5,
+            out[20] / 1e5);
     if (out[17])  // the controller's shader-clock ticks over its 100 MHz real-time ticks
       fprintf(stderr, "[accum] controller shader clock %.0f MHz over %.3f ms\n", (double)out[16] / ((double)out[17] / 100.0),
               out[17] / 1e5);

@@ -1788,6 +1788,7 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
   const uint64_t clk0 = A.prof ? __builtin_amdgcn_s_memtime() : 0, rt0 = A.prof ? now() : 0;
   uint64_t t_sub[4] = {0, 0, 0, 0};  // collect: reduce (stragglers), column sums, mean, closest
   uint64_t t_ws[4] = {0, 0, 0, 0};   // window: centre window data, window, record; [3] collect's takes
+  uint64_t t_cl[3] = {0, 0, 0};      // closest: members scored (wave 0), reduced + barrier, winner + barrier
 
   auto finish_cluster = [&]() {
     if (threadIdx.x == 0) {
@@ -2195,15 +2196,30 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
       if (threadIdx.x == 0) atomicMax((unsigned long long *)&A.out[3], 99ull);
       return;
     }
-    uint64_t nflag = 0, nsc = 0;
-    double best_val = s_bv[0];
-    uint64_t best_pos = s_bp[0];
-    for (int i = 0; i < NW; i++) {
-      nflag += s_red[i];
-      nsc += s_red[NW + i];
-      if (i && better(s_bv[i], s_bp[i], best_val, best_pos)) {
-        best_val = s_bv[i];
-        best_pos = s_bp[i];
+    // the eight waves' results, one per lane (every wave the same): totals by DPP sums, the
+    // first maximum by a max reduction (positions only on equal values)
+    uint64_t nflag, nsc;
+    double best_val;
+    uint64_t best_pos;
+    {
+      const uint32_t fl = lane < NW ? (uint32_t)s_red[lane] : 0u, sc = lane < NW ? (uint32_t)s_red[NW + lane] : 0u;
+      double v = lane < NW ? s_bv[lane] : -1.0;
+      uint64_t p = lane < NW ? s_bp[lane] : NONE64;
+      nflag = wave_sum32(fl);
+      nsc = wave_sum32(sc);
+      const double m = wave_ext_f64_all<true>(v);
+      const uint64_t hit = __ballot(p != NONE64 && v == m);
+      if (__popcll(hit) > 1) {
+        wave_best_all(v, p, better);
+        best_val = v;
+        best_pos = p;
+      } else if (hit) {
+        const int L = __builtin_ctzll(hit);
+        best_val = __builtin_bit_cast(double, readlane64(__builtin_bit_cast(uint64_t, v), L));
+        best_pos = readlane64(p, L);
+      } else {
+        best_val = -1.0;
+        best_pos = NONE64;
       }
     }
     if (mslot) {
@@ -2501,6 +2517,11 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
           bq = q;
         }
       }
+      uint64_t tc0 = 0;
+      if (A.prof && threadIdx.x == 0) {
+        tc0 = now();
+        t_cl[0] += tc0 - tq;
+      }
       {  // first minimum by (distance, key); keys are unique, so the lane holding it gives q.
          // The wave's smallest distance by a min reduction; only a tie between lanes needs the
          // (distance, key) pair reduction
@@ -2526,19 +2547,44 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
         s_bp[wv] = bq;
       }
       __syncthreads();
-      double d = s_bv[0];
-      uint64_t k = s_red[2 * NW], win = s_bp[0];
-      for (int i = 1; i < NW; i++)
-        if (s_bv[i] < d || (s_bv[i] == d && s_red[2 * NW + i] < k)) {
-          d = s_bv[i];
-          k = s_red[2 * NW + i];
-          win = s_bp[i];
+      uint64_t tc1 = 0;
+      if (A.prof && threadIdx.x == 0) {
+        tc1 = now();
+        t_cl[1] += tc1 - tc0;
+      }
+      // the eight waves' minima, one per lane (every wave the same): the smallest distance by a
+      // min reduction, the smallest key among equal distances (keys are unique)
+      uint64_t win;
+      {
+        const double dd = lane < NW ? s_bv[lane] : __builtin_inf();
+        const uint64_t kk = lane < NW ? s_red[2 * NW + lane] : NONE64;
+        const uint64_t pp = lane < NW ? s_bp[lane] : 0;
+        const double md = wave_ext_f64_all<false>(dd);
+        uint64_t hit = __ballot(kk != NONE64 && dd == md);
+        int L = hit ? __builtin_ctzll(hit) : 0;
+        if (__popcll(hit) > 1) {
+          uint64_t bestk = NONE64;
+          for (uint64_t m = hit; m; m &= m - 1) {
+            const int l = __builtin_ctzll(m);
+            const uint64_t kl = readlane64(kk, l);
+            if (kl < bestk) {
+              bestk = kl;
+              L = l;
+            }
+          }
         }
+        win = readlane64(pp, L);
+      }
       last_q = (uint32_t)win;
-      last = win < A.mrow ? mc.pos[win] : ld32(A.mem_pos + cl_start + win);
+      if (win < A.mrow) last = mc.pos[win];  // (uniform branch: no global load on the cached path)
+      else last = ld32(A.mem_pos + cl_start + win);
       if (threadIdx.x == 0) s_new = 0;
       __syncthreads();  // s_bv / s_bp / s_new are reused by the next step
-      if (A.prof && threadIdx.x == 0) t_sub[3] += now() - tq;
+      if (A.prof && threadIdx.x == 0) {
+        const uint64_t t = now();
+        t_sub[3] += t - tq;
+        t_cl[2] += t - tc1;
+      }
     } else if (best_pos != NONE64) {
       // is_min with a result: the best candidate seeds the next cluster (bvec::erase)
       finish_cluster();
@@ -2567,6 +2613,7 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
     A.out[7] = t_coll;
     for (int i = 0; i < 4; i++) A.out[8 + i] = t_sub[i];
     for (int i = 0; i < 4; i++) A.out[12 + i] = t_ws[i];
+    for (int i = 0; i < 3; i++) A.out[18 + i] = t_cl[i];
     if (A.prof) {
       A.out[16] = __builtin_amdgcn_s_memtime() - clk0;
       A.out[17] = now() - rt0;
