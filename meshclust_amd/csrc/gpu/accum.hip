@@ -2578,8 +2578,9 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
       last_q = (uint32_t)win;
       if (win < A.mrow) last = mc.pos[win];  // (uniform branch: no global load on the cached path)
       else last = ld32(A.mem_pos + cl_start + win);
+      // (no barrier: s_bv / s_bp / s_red / s_new are next written in the next step's fan-in,
+      // after the barrier that ends this step's deferred bvec kills -- npend > 0 here)
       if (threadIdx.x == 0) s_new = 0;
-      __syncthreads();  // s_bv / s_bp / s_new are reused by the next step
       if (A.prof && threadIdx.x == 0) {
         const uint64_t t = now();
         t_sub[3] += t - tq;
