@@ -568,6 +568,8 @@ int mc_set_classifier(mc_ctx *c, const mc_classifier *cls) {
   }
   if (getenv("MC_CLASSIFY_GENERIC")) c->cls.layout = 0;  // diagnostics: the generic form only
   c->fcls.on = c->cls.layout != 0 && !getenv("MC_CLASSIFY_EXACT");
+  c->fcls.mk = c->fcls.on && !getenv("MC_CLASSIFY_NO_SMALL");
+  c->fcls.rB = 0.0;
   for (int i = 0; i < MC_MAX_SINGLE; i++) {
     c->fcls.rinv[i] = 0.0;
     c->fcls.noff[i] = 0.0;
@@ -578,7 +580,12 @@ int mc_set_classifier(mc_ctx *c, const mc_classifier *cls) {
       c->fcls.nsgn[i] = -1.0;
     }
     const double r = cls->maxs[i] - cls->mins[i];
+    c->fcls.range[i] = r;
     c->fcls.rinv[i] = 1.0 / r;
+    if (i < 2) {  // mk_div's operands stay normal: |range|, |min| (or min = 0) within 2^-200 .. 2^200
+      const auto mid = [](double x) { return std::isfinite(x) && std::fabs(x) >= 0x1p-200 && std::fabs(x) <= 0x1p200; };
+      if (!(mid(r) && mid(c->fcls.rinv[i]) && (cls->mins[i] == 0.0 || mid(cls->mins[i])))) c->fcls.mk = 0;
+    }
     if (i >= 2 && !(std::isfinite(r) && r != 0.0 && std::isfinite(c->fcls.rinv[i]) && c->fcls.rinv[i] != 0.0 &&
                     std::isfinite(cls->mins[i])))
       c->fcls.on = 0;
@@ -1114,6 +1121,7 @@ int mc_accumulate(mc_ctx *c, const uint32_t *bin_lo, const uint64_t *bounds, uin
             out[7] / 1e5, out[8] / 1e5, out[9] / 1e5, out[15] / 1e5, out[10] / 1e5, out[11] / 1e5);
     fprintf(stderr, "[accum] closest: members scored %.3f, reduced %.3f, winner %.3f ms\n", out[18] / 1e5, out[19] / 1e5,
             out[20] / 1e5);
+    fprintf(stderr, "[accum] window: record span %.3f, record stores issued %.3f ms\n", out[21] / 1e5, out[22] / 1e5);
     if (out[17])  // the controller's shader-clock ticks over its 100 MHz real-time ticks
       fprintf(stderr, "[accum] controller shader clock %.0f MHz over %.3f ms\n", (double)out[16] / ((double)out[17] / 100.0),
               out[17] / 1e5);

@@ -175,6 +175,31 @@ __device__ __forceinline__ uint4 ld_nt16(const uint4 *p) {
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+// LDS reads through LDS-typed pointers.  Where a value comes from the controller's LDS cache or
+// from global memory (cached ? LDS : global), the compiler otherwise merges the two loads into
+// ONE flat load through a select of the pointers -- and a flat load waits on every outstanding
+// vector memory operation (s_waitcnt vmcnt(0) lgkmcnt(0)): the step record's stores included
+// (0.7 us of each config-B step, the record's second word waited for its first to land).
+#define MC_LDS __attribute__((address_space(3)))
+#define MC_GLB __attribute__((address_space(1)))
+__device__ __forceinline__ uint32_t lds_u32(const uint32_t *p) { return *(const MC_LDS uint32_t *)p; }
+__device__ __forceinline__ uint64_t lds_u64(const uint64_t *p) { return *(const MC_LDS uint64_t *)p; }
+__device__ __forceinline__ uint4 lds_u4(const uint4 *p) {
+  const u32x4_t v = *(const MC_LDS u32x4_t *)p;
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void glb_st16(MC_GLB u32x4_t *p, const uint4 &v) { *p = (u32x4_t){v.x, v.y, v.z, v.w}; }
+__device__ __forceinline__ WinTab lds_wt(const WinTab *p) {
+  static_assert(sizeof(WinTab) == 40, "WinTab is read as five 8-byte words");
+  const MC_LDS uint64_t *q = (const MC_LDS uint64_t *)p;
+  uint64_t w[5];
+#pragma unroll
+  for (int i = 0; i < 5; i++) w[i] = q[i];
+  WinTab r;
+  __builtin_memcpy(&r, w, sizeof(WinTab));
+  return r;
+}
+
 // Step trace (MC_ACCUM_PROFILE=2/3), words per step: 0 record published, 7 controller has
 // every partial, 8 collect done, 9 active workers; =3: 1/2 first/last worker saw it, 3/4
 // first/last scan done, 5/6 first/last partial stored (minima kept as maxima of ~t); =2: the
@@ -255,7 +280,8 @@ __device__ __forceinline__ bool better(double v, uint64_t p, double bv, uint64_t
 // callers keep queries uniform and put a barrier between kills and the next query.  The
 // closed forms are checked against the host bvec in tests/native/bvec_check.cpp.
 struct DevBvec {
-  uint32_t *bits;
+  uint32_t *gbits;        // the bitmap in global memory (gb), else null
+  MC_LDS uint32_t *bits;  // ... in LDS (!gb)
   bool gb;  // bits in global memory: sc1 loads (the atomics that clear bits act in L2)
   uint32_t *cn;
   uint32_t *fw;
@@ -266,7 +292,11 @@ struct DevBvec {
   WinTab h{~0ull, ~0ull, ~0u, ~0u, 0, 0, 0, 0};
 
   __device__ uint64_t nbins() const { return nb; }
-  __device__ uint32_t word(uint64_t w) const { return gb ? ld32(bits + w) : bits[w]; }
+  __device__ uint32_t word(uint64_t w) const { return gb ? ld32(gbits + w) : bits[w]; }
+  __device__ __forceinline__ void clear_bit(uint64_t p) {
+    if (gb) atomicAnd(&gbits[p >> 5], ~(1u << (p & 31)));
+    else __hip_atomic_fetch_and(&bits[p >> 5], ~(1u << (p & 31)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
   __device__ uint64_t cnt(uint64_t b) { return b < nb ? cn[b] : 0; }
   __device__ void index_of(uint64_t point, uint64_t *plow, uint64_t *phigh) {
     bv_index_of_sorted(bnd, nb, point, plow, phigh);
@@ -392,7 +422,7 @@ struct DevBvec {
   // kill one static position (bvec::pop / erase / remove_available); any thread, atomics
   __device__ __forceinline__ void kill_one(uint64_t p) { kill_in(p, bin_of(p)); }
   __device__ __forceinline__ void kill_in(uint64_t p, uint64_t b) {  // ... when its bin b is known
-    atomicAnd(&bits[p >> 5], ~(1u << (p & 31)));
+    clear_bit(p);
     count_sub(b, 1u);
   }
   __device__ __forceinline__ void count_sub(uint64_t b, uint32_t n) {  // n kills in bin b: counts only
@@ -403,7 +433,7 @@ struct DevBvec {
   // atomic each, the counts once per distinct bin of each wave (a step's new members share a
   // few bins: per-member Fenwick walks were same-address LDS atomics in series)
   __device__ __forceinline__ void kill_list(bool act, uint64_t p, uint64_t b) {
-    if (act) atomicAnd(&bits[p >> 5], ~(1u << (p & 31)));
+    if (act) clear_bit(p);
     uint64_t pending = __ballot(act);
     while (pending) {
       const int L = __builtin_ctzll(pending);
@@ -1001,10 +1031,14 @@ __device__ __forceinline__ void worker_dense(const AccArgs &A, const DevClassifi
   uint32_t n_ent = (uint32_t)__syncthreads_count(al_t);
   PInfo pi_t{0, 0, 0};
   PTerms pt_t{0, 0, 0.0};
+  PSm ps_t{0, 0, 0, 0, false};
   if (al_t) {
     pi_t = PInfo{A.mag_s[pos_t], A.sumsq_s[pos_t], A.len_s[pos_t]};
     pt_t = pterms(pi_t.mag, pi_t.sumsq, A.B);
+    ps_t = psmall(pi_t, pt_t);
   }
+  // classify_small: 8-bit bins and the host's mk_div conditions (per pair: both PSm ok)
+  const bool small_on = sizeof(T) == 1 && A.fc.on && A.fc.mk;
   if (t == 0) {
     s_abort = 0;
     s_b[0] = s_b[1] = 0;
@@ -1092,7 +1126,9 @@ __device__ __forceinline__ void worker_dense(const AccArgs &A, const DevClassifi
     const PInfo pc{(uint64_t)hdr[4 + KINL] | ((uint64_t)hdr[5 + KINL] << 32),
                    (uint64_t)hdr[6 + KINL] | ((uint64_t)hdr[7 + KINL] << 32),
                    (uint64_t)hdr[8 + KINL] | ((uint64_t)hdr[9 + KINL] << 32)};
-    const PTerms tq = pterms(pc.mag, pc.sumsq, A.B);
+    const PTerms tq = pterms_mk(pc.mag, pc.sumsq, A.B, A.fc.rB);
+    const PSm ps_q = psmall(pc, tq);
+    const double kq = (double)((int64_t)pc.mag - (int64_t)A.B * tq.ap);
     // the controller's kills since the last record: every thread compares them with its own
     // entry (one or two per step; no search, no barrier)
     {
@@ -1142,9 +1178,22 @@ __device__ __forceinline__ void worker_dense(const AccArgs &A, const DevClassifi
       } else {
         for (int k = 0; k < nch; k++) acc.add(rr[(uint64_t)k * NT], clds[k]);
       }
-      d_t = A.fc.on    ? classify_fast(C, A.fc, acc.finish(pi_t.mag, pc.mag), pi_t, pt_t, pc, tq, A.B, &cv_t)
-            : C.layout ? classify_std(C, acc.finish(pi_t.mag, pc.mag), pi_t, pt_t, pc, tq, A.B, &cv_t)
-                       : classify_cand<T>(acc, pi_t, pc, A.B, C, &cv_t);
+      bool und = true;
+      if constexpr (sizeof(T) == 1) {
+        if (small_on && ps_q.ok && ps_t.ok) {
+          acc.fold();
+          d_t = classify_small(C, A.fc, acc.sad, acc.dot, ps_t, ps_q, kq, pt_t.da, tq.da, A.B, &cv_t, &und);
+          if (und) {
+            double cx;
+            d_t = classify_std(C, acc.finish(pi_t.mag, pc.mag), pi_t, pt_t, pc, tq, A.B, &cx);
+            und = false;
+          }
+        }
+      }
+      if (und)
+        d_t = A.fc.on    ? classify_fast(C, A.fc, acc.finish(pi_t.mag, pc.mag), pi_t, pt_t, pc, tq, A.B, &cv_t)
+              : C.layout ? classify_std(C, acc.finish(pi_t.mag, pc.mag), pi_t, pt_t, pc, tq, A.B, &cv_t)
+                         : classify_cand<T>(acc, pi_t, pc, A.B, C, &cv_t);
     }
     if (A.trace && t == 0) t_scanned = now();
     if (A.trace2 && lane == 0) s_tw[wv] = now();
@@ -1361,6 +1410,7 @@ __device__ __forceinline__ void worker_dense(const AccArgs &A, const DevClassifi
           pos_t = np;
           pi_t = PInfo{A.mag_s[pos_t], A.sumsq_s[pos_t], A.len_s[pos_t]};
           pt_t = pterms(pi_t.mag, pi_t.sumsq, A.B);
+          ps_t = psmall(pi_t, pt_t);
         }
       }
     }
@@ -1407,13 +1457,15 @@ __device__ __forceinline__ void worker_dstream(const AccArgs &A, const DevClassi
   uint32_t *srec = reinterpret_cast<uint32_t *>(dyn);
   const uint4 *clds = dyn;  // the centre row: record words 0 .. 4 nch
   // entry positions of the current list and the rebuild's target (fcap each)
-  uint32_t *lpos[2] = {reinterpret_cast<uint32_t *>(dyn + (rec_words + 3) / 4), nullptr};
+  // (LDS- and global-typed: a buffer picked by index would otherwise be a flat access)
+  MC_LDS uint32_t *lpos[2] = {(MC_LDS uint32_t *)reinterpret_cast<uint32_t *>(dyn + (rec_words + 3) / 4), nullptr};
   lpos[1] = lpos[0] + (A.fcap + 3) / 4 * 4;
   // this worker's two row buffers (fcap entries each), as buffer resources for sc1 loads
   const uint64_t wrow = A.fcap * (uint64_t)nch;  // uint4 per buffer
-  uint4 *rb[2] = {A.srows + (uint64_t)w * 2 * wrow, A.srows + ((uint64_t)w * 2 + 1) * wrow};
-  const __amdgpu_buffer_rsrc_t rr[2] = {__builtin_amdgcn_make_buffer_rsrc(rb[0], 0, (int)(wrow * 16), 0x00020000),
-                                        __builtin_amdgcn_make_buffer_rsrc(rb[1], 0, (int)(wrow * 16), 0x00020000)};
+  MC_GLB u32x4_t *rb[2] = {(MC_GLB u32x4_t *)(A.srows + (uint64_t)w * 2 * wrow),
+                           (MC_GLB u32x4_t *)(A.srows + ((uint64_t)w * 2 + 1) * wrow)};
+  const __amdgpu_buffer_rsrc_t rr[2] = {__builtin_amdgcn_make_buffer_rsrc((u32x4_t *)rb[0], 0, (int)(wrow * 16), 0x00020000),
+                                        __builtin_amdgcn_make_buffer_rsrc((u32x4_t *)rb[1], 0, (int)(wrow * 16), 0x00020000)};
   int cur = 0;
   const uint32_t J = (uint32_t)((A.fcap + NT - 1) / NT);  // entries per thread (<= SJ)
   auto slot = [&](uint32_t e, int k) -> uint32_t {  // uint4 index of entry e's chunk k in a buffer
@@ -1430,7 +1482,7 @@ __device__ __forceinline__ void worker_dstream(const AccArgs &A, const DevClassi
     if (p >= A.N) break;
     lpos[0][e] = (uint32_t)p;
     alive |= 1u << j;
-    for (int k = 0; k < nch; k++) rb[0][slot(e, k)] = A.hs[(uint64_t)k * A.npad + p];
+    for (int k = 0; k < nch; k++) glb_st16(rb[0] + slot(e, k), A.hs[(uint64_t)k * A.npad + p]);
   }
   drain();  // (the rows are read back with sc1 loads after the barrier below)
   if (t == 0) {
@@ -1524,7 +1576,7 @@ __device__ __forceinline__ void worker_dstream(const AccArgs &A, const DevClassi
                    (uint64_t)hdr[6 + KINL] | ((uint64_t)hdr[7 + KINL] << 32),
                    (uint64_t)hdr[8 + KINL] | ((uint64_t)hdr[9 + KINL] << 32)};
     const PTerms tq = pterms(pc.mag, pc.sumsq, A.B);
-    const uint32_t *lp = lpos[cur];
+    const MC_LDS uint32_t *lp = lpos[cur];
     // the controller's kills since the last record, against each entry of this thread
     {
       const uint32_t kinl0 = kend > (uint32_t)KINL ? kend - KINL : 0;
@@ -1700,7 +1752,7 @@ __device__ __forceinline__ void worker_dstream(const AccArgs &A, const DevClassi
         }
         if (al) {
           const uint32_t e = t + NT * j;
-          for (int k = 0; k < nch; k++) rb[nxt][slot(r, k)] = ld_sc1_16(rr[cur], slot(e, k) * 16u);
+          for (int k = 0; k < nch; k++) glb_st16(rb[nxt] + slot(r, k), ld_sc1_16(rr[cur], slot(e, k) * 16u));
           lpos[nxt][r] = lp[e];
         }
         base += tot;
@@ -1773,7 +1825,7 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
   // the workers' partials as a buffer resource (16-byte sc1 polls, aux 16 = sc1)
   const __amdgpu_buffer_rsrc_t prs =
       __builtin_amdgcn_make_buffer_rsrc(A.partials, 0, (int)(GW * PART_G * 8), 0x00020000);
-  DevBvec bv{A.gbits ? A.gbits : lbits, A.gbits != nullptr, cnt, fw, lo, bnd, A.len_s, A.nb, lg};
+  DevBvec bv{A.gbits, (MC_LDS uint32_t *)lbits, A.gbits != nullptr, cnt, fw, lo, bnd, A.len_s, A.nb, lg};
   uint32_t last = NONE;   // current centre (static position)
   uint32_t last_q = 0;    // its member index in the current cluster
   uint64_t cl_start = 0;  // first member index of the current cluster
@@ -1789,6 +1841,7 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
   uint64_t t_sub[4] = {0, 0, 0, 0};  // collect: reduce (stragglers), column sums, mean, closest
   uint64_t t_ws[4] = {0, 0, 0, 0};   // window: centre window data, window, record; [3] collect's takes
   uint64_t t_cl[3] = {0, 0, 0};      // closest: members scored (wave 0), reduced + barrier, winner + barrier
+  uint64_t t_pub[2] = {0, 0};        // window (spec): the record's span, the record's stores issued
 
   auto finish_cluster = [&]() {
     if (threadIdx.x == 0) {
@@ -1806,14 +1859,13 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
     st64(A.klog + kn, gran(kn + 1, (uint32_t)p));
     s_klast[kn % KINL] = (uint32_t)p;
   };
+  // (thread 0's global stores come after every load of the seed: a load behind a store waits
+  // for the store, see publish)
   auto new_cluster = [&](uint64_t pos, bool kill = false) {
+    if (A.mrow && !WIDE)
+      for (int c = threadIdx.x; c < nch; c += NT) mc.row[c] = A.hr[pos * nch + c];
+    for (int b = threadIdx.x; b < A.B; b += NT) msum[b] = reinterpret_cast<const T *>(A.hr + pos * nch)[b];
     if (threadIdx.x == 0) {
-      st32(A.mem_pos + cl_start, (uint32_t)pos);
-      st64(A.mkeys + cl_start, 0);
-      if (kill && !A.mrow) {
-        bv.kill_one(pos);
-        log_kill(pos);
-      }
       if (A.mrow) {
         uint2 w[MINFO_W];
         minfo_issue(A.minfo + pos, w);
@@ -1828,11 +1880,13 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
         mc.info[1] = mi.sumsq;
         mc.info[2] = mi.len;
         mc.wt[0] = mi.wt;
+      } else if (kill) {
+        bv.kill_one(pos);
+        log_kill(pos);
       }
+      st32(A.mem_pos + cl_start, (uint32_t)pos);
+      st64(A.mkeys + cl_start, 0);
     }
-    if (A.mrow && !WIDE)
-      for (int c = threadIdx.x; c < nch; c += NT) mc.row[c] = A.hr[pos * nch + c];
-    for (int b = threadIdx.x; b < A.B; b += NT) msum[b] = reinterpret_cast<const T *>(A.hr + pos * nch)[b];
     M = 1;
     last_q = 0;
     if (kill) kn++;
@@ -1858,7 +1912,7 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
     const bool cached = last_q < A.mrow;
     if (!WIDE && j < 4 * nch) {
       if (last == NONE) return 0;
-      const uint4 v = cached ? mc.row[(size_t)last_q * mc.rp + j / 4] : A.hr[(uint64_t)last * nch + j / 4];
+      const uint4 v = cached ? lds_u4(mc.row + (size_t)last_q * mc.rp + j / 4) : A.hr[(uint64_t)last * nch + j / 4];
       return (j & 3) == 0 ? v.x : (j & 3) == 1 ? v.y : (j & 3) == 2 ? v.z : v.w;
     }
     const int h = j - (WIDE ? 0 : 4 * nch);
@@ -1873,7 +1927,7 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
     if (last == NONE) return 0;
     const int f = (h - 4 - KINL) / 2, hi = (h - 4 - KINL) & 1;
     const uint64_t v =
-        cached ? mc.info[(size_t)last_q * 3 + f] : (f == 0 ? A.mag_s[last] : f == 1 ? A.sumsq_s[last] : A.len_s[last]);
+        cached ? lds_u64(mc.info + (size_t)last_q * 3 + f) : (f == 0 ? A.mag_s[last] : f == 1 ? A.sumsq_s[last] : A.len_s[last]);
     return hi ? (uint32_t)(v >> 32) : (uint32_t)v;
   };
 
@@ -1881,9 +1935,53 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
   // granule tagged with the step).  Kill-log entries are tagged granules: a worker that needs
   // one checks its tag, so the record is not held back until they land.  `go` is only a hint
   // for a worker that fell RING steps behind: it re-validates the record's tags after reading.
+  // rec_word for a cached centre (row and magnitudes in the member cache): every word is one
+  // LDS read from a per-lane address or a uniform value -- no per-word branches (the general
+  // form's divergent cases cost a single wave ≈0.7 us per record)
+  auto rec_word_cached = [&](int j, bool have, uint64_t S, uint64_t E) -> uint32_t {
+    const int h = j - 4 * nch;
+    const int64_t e = (int64_t)kn - KINL + (h - 4);
+    const MC_LDS uint32_t *row = (const MC_LDS uint32_t *)(mc.row + (size_t)last_q * mc.rp);
+    const MC_LDS uint32_t *inf = (const MC_LDS uint32_t *)(mc.info + (size_t)last_q * 3);
+    const MC_LDS uint32_t *p = h < 0               ? row + j
+                               : h < 4 + KINL      ? (const MC_LDS uint32_t *)s_klast + (e >= 0 ? (uint32_t)e % KINL : 0u)
+                                                   : inf + (h - 4 - KINL);
+    const uint32_t x = *p;
+    if (h < 0) return x;
+    if (h == 0) return have ? last : NONE;
+    if (h == 1) return (uint32_t)S;
+    if (h == 2) return (uint32_t)E;
+    if (h == 3) return kn | (rec_exact ? 0x80000000u : 0u);
+    if (h < 4 + KINL) return e >= 0 ? x : NONE;
+    return x;
+  };
+  // (Every word of a lane is read before its first store: on gfx9 stores count in vmcnt, so a
+  // load issued after a store waits for that store to complete -- a write-through round trip.)
   auto publish = [&](uint64_t S, uint64_t E, bool have) {
     uint64_t *r = A.ring + (uint64_t)(step % RING) * A.rec_g;
-    for (int j = lane; j < rec_words; j += 64) st64(r + j, gran(step, rec_word(j, have, S, E)));
+    constexpr int PW = 4;  // words per lane read before the lane's stores
+    const bool fastw = !WIDE && last != NONE && last_q < A.mrow;  // (uniform)
+    for (int j0 = 0; j0 < rec_words; j0 += 64 * PW) {
+      uint32_t d[PW];
+      if (fastw) {
+#pragma unroll
+        for (int u = 0; u < PW; u++) {
+          const int j = j0 + u * 64 + lane;
+          d[u] = j < rec_words ? rec_word_cached(j, have, S, E) : 0u;
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < PW; u++) {
+          const int j = j0 + u * 64 + lane;
+          d[u] = j < rec_words ? rec_word(j, have, S, E) : 0u;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < PW; u++) {
+        const int j = j0 + u * 64 + lane;
+        if (j < rec_words) st64(r + j, gran(step, d[u]));
+      }
+    }
     if (lane == 0) st32(A.go, step);
   };
 
@@ -1974,7 +2072,7 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
     uint64_t S = 0, E = 0;
     bool have = false;
     while (last != NONE && !err) {
-      const WinTab wt = last_q < A.mrow ? mc.wt[last_q] : A.minfo[last].wt;  // the centre's window data
+      const WinTab wt = last_q < A.mrow ? lds_wt(mc.wt + last_q) : A.minfo[last].wt;  // the centre's window data
       if (A.prof && threadIdx.x == 0) {
         drain();
         const uint64_t t = now();
@@ -1995,7 +2093,14 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
         // D: reads within 10 % of each other's length make every window such a span).
         rec_exact = fast_after && wt.kf == 0 && (uint64_t)wt.kble == (uint64_t)(lo[wt.bb + 1] - lo[wt.bb]);
         step++;
+        uint64_t tp0 = 0;
+        if (A.prof && threadIdx.x == 0) tp0 = now();
         if (wv == 0) publish(fast_after ? lo[wt.fb] : 0, fast_after ? lo[wt.bb + 1] - 1 : A.N - 1, true);
+        if (A.prof && threadIdx.x == 0) {
+          const uint64_t t = now();
+          t_pub[0] += tp0 - t_mark;  // the record's span (edge bins' counts)
+          t_pub[1] += t - tp0;       // the record's words and stores issued
+        }
         if (A.trace2 && threadIdx.x == 0 && step < TRACE_STEPS) A.trace[(uint64_t)step * TRACE_W + 6] = now();
       }
       if (npend) {  // the last step's bvec kills, after the record is out
@@ -2403,7 +2508,7 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
         // one member per wave (rows from `hr`, 64 lanes over the row): every lane ends with
         // the wave's first minimum
         for (uint64_t q = wv; q < M; q += NW) {
-          const uint32_t r = q < A.mrow ? mc.pos[q] : ld32(A.mem_pos + cl_start + q);
+          const uint32_t r = q < A.mrow ? lds_u32(mc.pos + q) : ld32(A.mem_pos + cl_start + q);
           const uint4 *row = A.hr + (uint64_t)r * nch;
           Acc<T> acc;
           int c = lane;
@@ -2416,8 +2521,8 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
           }
           for (; c < nch; c += 64) acc.add(row[c], F4[c]);
           acc.wave_reduce();
-          const uint64_t mp = q < A.mrow ? mc.info[q * 3] : A.mag_s[r];
-          const uint64_t key = q < A.mrow ? mc.key[q] : ld64(A.mkeys + cl_start + q);
+          const uint64_t mp = q < A.mrow ? lds_u64(mc.info + q * 3) : A.mag_s[r];
+          const uint64_t key = q < A.mrow ? lds_u64(mc.key + q) : ld64(A.mkeys + cl_start + q);
           const PS s = acc.finish(mp, sumF);
           const double frac = (double)(2 * s.smin) / (double)(mp + sumF);
           const double d = __builtin_fma(-frac, frac, 1.0) * 10000.0;
@@ -2466,8 +2571,8 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
           sad += dpp_mv<0xB1>(0u, sad);  // quad_perm [1,0,3,2]
           sad += dpp_mv<0x4E>(0u, sad);  // quad_perm [2,3,0,1]: every lane of the quad has the sum
           if (sub == 0) {
-            const uint64_t mp = q < A.mrow ? mc.info[q * 3] : A.mag_s[ld32(A.mem_pos + cl_start + q)];
-            const uint64_t key = q < A.mrow ? mc.key[q] : ld64(A.mkeys + cl_start + q);
+            const uint64_t mp = q < A.mrow ? lds_u64(mc.info + q * 3) : A.mag_s[ld32(A.mem_pos + cl_start + q)];
+            const uint64_t key = q < A.mrow ? lds_u64(mc.key + q) : ld64(A.mkeys + cl_start + q);
             const uint64_t smin = (mp + sumF - sad) >> 1;
             const double frac = (double)(2 * smin) / (double)(mp + sumF);
             const double d = __builtin_fma(-frac, frac, 1.0) * 10000.0;
@@ -2576,7 +2681,7 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
         win = readlane64(pp, L);
       }
       last_q = (uint32_t)win;
-      if (win < A.mrow) last = mc.pos[win];  // (uniform branch: no global load on the cached path)
+      if (win < A.mrow) last = lds_u32(mc.pos + win);  // (uniform branch: no global load on the cached path)
       else last = ld32(A.mem_pos + cl_start + win);
       // (no barrier: s_bv / s_bp / s_red / s_new are next written in the next step's fan-in,
       // after the barrier that ends this step's deferred bvec kills -- npend > 0 here)
@@ -2615,6 +2720,7 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
     for (int i = 0; i < 4; i++) A.out[8 + i] = t_sub[i];
     for (int i = 0; i < 4; i++) A.out[12 + i] = t_ws[i];
     for (int i = 0; i < 3; i++) A.out[18 + i] = t_cl[i];
+    for (int i = 0; i < 2; i++) A.out[21 + i] = t_pub[i];
     if (A.prof) {
       A.out[16] = __builtin_amdgcn_s_memtime() - clk0;
       A.out[17] = now() - rt0;
@@ -2890,6 +2996,7 @@ int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, 
   A.cl_off = d_cl_off;
   A.out = d_out;
   A.fc = c->fcls;
+  A.fc.rB = 1.0 / (double)A.B;
   A.dbg = getenv("MC_ACCUM_DBG") ? atoi(getenv("MC_ACCUM_DBG")) : 0;
   A.budget = 20ull * 100000000ull;  // a single hand-off never takes 20 s: give up, report error 99
   A.W = c->mb_world > 0 ? (uint32_t)c->mb_world : 1u;

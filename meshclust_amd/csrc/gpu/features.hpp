@@ -453,6 +453,94 @@ __device__ __forceinline__ int classify_fast(const DevClassifier &C, const FastC
   return classify_std(C, s, p, tp, q, tq, B, &cx);
 }
 
+// ---- the accumulation workers' short form (8-bit bins, every magnitude < 2^24) ------------
+// RN(a / b) for a constant b from the host's y = RN(1 / b): q0 = RN(a y), r = a - b q0 (exact
+// by fma), RN(q0 + r y) is the correctly rounded quotient (Markstein's theorem; b, y, a and the
+// remainder normal: FastCls::mk and the raw features' ranges keep them so).
+__device__ __forceinline__ double mk_div(double a, double b, double y) {
+  const double q0 = a * y;
+  return __builtin_fma(__builtin_fma(-q0, b, a), y, q0);
+}
+// pterms with the division by B as mk_div (the same PTerms, bit for bit)
+__device__ __forceinline__ PTerms pterms_mk(uint64_t mag, uint64_t sumsq, int B, double rB) {
+  const double da = mk_div((double)mag, (double)B, rB);
+  const int64_t a = (int)round(da), m = (int64_t)mag, b = B;
+  return PTerms{a, (int64_t)sumsq - 2 * a * m + b * a * a, da};
+}
+// a histogram's terms in 32 bits; ok = they bound every integer of the pair arithmetic below
+// 2^53 (magnitude < 2^24, length < 2^31, sum (p - ap)^2 < 2^26), so doubles hold it exactly
+struct PSm {
+  uint32_t mag, len, ap, np;
+  bool ok;
+};
+__device__ __forceinline__ PSm psmall(const PInfo &p, const PTerms &t) {
+  const bool ok = p.mag < (1ull << 24) && p.len < (1ull << 31) && t.ap >= 0 && t.np >= 0 && t.np < (1ll << 26);
+  return PSm{(uint32_t)p.mag, (uint32_t)p.len, (uint32_t)t.ap, (uint32_t)t.np, ok};
+}
+// classify_fast from the 8-bit sums (sad = sum |p - q|, dot = sum p q) and the PSm terms of
+// both histograms (kq = mag_q - B aq): LD, INTERSECTION and combo 0 exact (the LD / INT
+// normalisations as mk_div by the host's RN(1 / range)), MANHATTAN exact, PEARSON's integers
+// exact in doubles (every one below 2^53), the decision by classify_fast's margin.  *undecided:
+// the caller decides by classify_std.  Every value it returns or stores is classify_std's.
+__device__ __forceinline__ int classify_small(const DevClassifier &C, const FastCls &F, uint32_t sad, uint32_t dot,
+                                              const PSm &p, const PSm &q, double kq, double dap, double daq, int B,
+                                              double *c0, bool *undecided) {
+  const mc_classifier &c = C.c;
+  const bool kul = C.layout == 4;
+  const uint32_t dl = p.len > q.len ? p.len - q.len : q.len - p.len;
+  const uint32_t ms = p.mag + q.mag, s2 = ms - sad;  // s2 = 2 Smin
+  double v0 = mk_div((double)dl - c.mins[0], F.range[0], F.rinv[0]);
+  double v1 = mk_div((double)s2 / (double)ms - c.mins[1], F.range[1], F.rinv[1]);
+  v0 = c.is_sim[0] ? v0 : 1 - v0;
+  v1 = c.is_sim[1] ? v1 : 1 - v1;
+  const double a0 = v0 * v1;
+  *c0 = a0;
+  double r[5], e[5], v[5];
+  r[2] = (double)(int32_t)sad;
+  {
+    const double d = __builtin_fma(-(double)p.ap, kq, __builtin_fma(-(double)q.ap, (double)p.mag, (double)dot));
+    const double prod = (double)p.np * (double)q.np;
+    const double pr = 0.5 < prod ? prod : 0.5;
+    r[3] = d * rsq_nr(pr);
+  }
+  r[4] = kul ? ((double)B * (dap + daq)) * rcp_nr((2.0 * dap) * daq) * (double)(s2 >> 1) : 0.0;
+  const int nf = kul ? 5 : 4;
+#pragma unroll
+  for (int i = 2; i < 5; i++) {
+    if (i >= nf) {
+      v[i] = e[i] = 0.0;
+      continue;
+    }
+    const double n = (r[i] - c.mins[i]) * F.rinv[i];
+    v[i] = F.noff[i] + F.nsgn[i] * n;
+    e[i] = 0x1p-40 * ((__builtin_fabs(r[i]) + __builtin_fabs(c.mins[i])) * __builtin_fabs(F.rinv[i]) +
+                      __builtin_fabs(v[i]) + 1.0);
+  }
+  const double q00 = v0 * v0;
+  const double a1 = q00 * (v[2] * v[2]);
+  const double a2 = v[3];
+  const double a3 = q00 * (v[4] * v[4]);
+  double sum = c.weights[0];
+  sum = __builtin_fma(c.weights[1], a0, sum);
+  sum = __builtin_fma(c.weights[2], a1, sum);
+  sum = __builtin_fma(c.weights[3], a2, sum);
+  if (kul) sum = __builtin_fma(c.weights[4], a3, sum);
+  const double d1 = q00 * (2.0 * __builtin_fabs(v[2]) + e[2]) * e[2] + 0x1p-40 * __builtin_fabs(a1);
+  const double d3 = q00 * (2.0 * __builtin_fabs(v[4]) + e[4]) * e[4] + 0x1p-40 * __builtin_fabs(a3);
+  const double mag = __builtin_fabs(c.weights[0]) + __builtin_fabs(c.weights[1] * a0) + __builtin_fabs(c.weights[2] * a1) +
+                     __builtin_fabs(c.weights[3] * a2) + (kul ? __builtin_fabs(c.weights[4] * a3) : 0.0);
+  const double margin = 2.0 * (__builtin_fabs(c.weights[2]) * d1 + __builtin_fabs(c.weights[3]) * e[3] +
+                               (kul ? __builtin_fabs(c.weights[4]) * d3 : 0.0)) +
+                        0x1p-40 * mag;
+  *undecided = false;
+  if (__builtin_isfinite(sum) && __builtin_isfinite(margin) && __builtin_isfinite(a0)) {
+    if (sum - margin >= C.thr) return 1;
+    if (sum + margin < C.thr) return 0;
+  }
+  *undecided = true;
+  return 0;
+}
+
 template <typename T>
 __device__ __forceinline__ uint4 ld16(const uint8_t *row, int ch) {
   return reinterpret_cast<const uint4 *>(row)[ch];

@@ -45,9 +45,13 @@ struct DevClassifier {
 // the accumulation kernel only: rinv[i] = RN(1 / (maxs[i] - mins[i])) on the host, and
 // is_sim ? n : 1 - n == noff + nsgn * n; on = 1 when the classifier has the trainer's layout
 // and every range of features 2..4 is finite and nonzero.
+// classify_small (8-bit bins, small magnitudes) also takes range[i] = RN(maxs[i] - mins[i]) and
+// divides features 0 / 1 by it as mk_div (mk = 1 when those ranges and minima keep every operand
+// of the division normal), and rB = RN(1 / B) for the centre's PTerms (set by the launcher).
 struct FastCls {
-  double rinv[MC_MAX_SINGLE], noff[MC_MAX_SINGLE], nsgn[MC_MAX_SINGLE];
-  int on;
+  double rinv[MC_MAX_SINGLE], noff[MC_MAX_SINGLE], nsgn[MC_MAX_SINGLE], range[MC_MAX_SINGLE];
+  double rB;
+  int on, mk;
 };
 
 // Read-only view of the device histogram matrix passed to kernels by value.
