@@ -1460,8 +1460,11 @@ __device__ __forceinline__ void worker_dstream(const AccArgs &A, const DevClassi
   // (LDS- and global-typed: a buffer picked by index would otherwise be a flat access)
   MC_LDS uint32_t *lpos[2] = {(MC_LDS uint32_t *)reinterpret_cast<uint32_t *>(dyn + (rec_words + 3) / 4), nullptr};
   lpos[1] = lpos[0] + (A.fcap + 3) / 4 * 4;
-  // this worker's two row buffers (fcap entries each), as buffer resources for sc1 loads
-  const uint64_t wrow = A.fcap * (uint64_t)nch;  // uint4 per buffer
+  // this worker's two row buffers (fcap entries each), as buffer resources for sc1 loads; an
+  // entry is its nch row chunks and an info chunk {mag, len, ap, np} (classify_small's PSm,
+  // ap = ~0 when not ok), so the scan reads no per-position arrays
+  const uint32_t CH = (uint32_t)nch + 1;
+  const uint64_t wrow = A.fcap * (uint64_t)CH;  // uint4 per buffer
   MC_GLB u32x4_t *rb[2] = {(MC_GLB u32x4_t *)(A.srows + (uint64_t)w * 2 * wrow),
                            (MC_GLB u32x4_t *)(A.srows + ((uint64_t)w * 2 + 1) * wrow)};
   const __amdgpu_buffer_rsrc_t rr[2] = {__builtin_amdgcn_make_buffer_rsrc((u32x4_t *)rb[0], 0, (int)(wrow * 16), 0x00020000),
@@ -1469,8 +1472,9 @@ __device__ __forceinline__ void worker_dstream(const AccArgs &A, const DevClassi
   int cur = 0;
   const uint32_t J = (uint32_t)((A.fcap + NT - 1) / NT);  // entries per thread (<= SJ)
   auto slot = [&](uint32_t e, int k) -> uint32_t {  // uint4 index of entry e's chunk k in a buffer
-    return ((e >> 6) * (uint32_t)nch + (uint32_t)k) * 64u + (e & 63u);
+    return ((e >> 6) * CH + (uint32_t)k) * 64u + (e & 63u);
   };
+  const bool small_on = sizeof(T) == 1 && A.fc.on && A.fc.mk;
   // entry e = t + NT j: this worker's (e / DT)-th tile, offset e % DT (positions increase with
   // the entry, so the entries below N are a prefix)
   uint32_t alive = 0;  // bit j: entry t + NT j alive
@@ -1483,6 +1487,9 @@ __device__ __forceinline__ void worker_dstream(const AccArgs &A, const DevClassi
     lpos[0][e] = (uint32_t)p;
     alive |= 1u << j;
     for (int k = 0; k < nch; k++) glb_st16(rb[0] + slot(e, k), A.hs[(uint64_t)k * A.npad + p]);
+    const PInfo pi{A.mag_s[p], A.sumsq_s[p], A.len_s[p]};
+    const PSm ps = psmall(pi, pterms(pi.mag, pi.sumsq, A.B));
+    glb_st16(rb[0] + slot(e, nch), make_uint4(ps.mag, ps.len, ps.ok ? ps.ap : ~0u, ps.np));
   }
   drain();  // (the rows are read back with sc1 loads after the barrier below)
   if (t == 0) {
@@ -1575,7 +1582,10 @@ __device__ __forceinline__ void worker_dstream(const AccArgs &A, const DevClassi
     const PInfo pc{(uint64_t)hdr[4 + KINL] | ((uint64_t)hdr[5 + KINL] << 32),
                    (uint64_t)hdr[6 + KINL] | ((uint64_t)hdr[7 + KINL] << 32),
                    (uint64_t)hdr[8 + KINL] | ((uint64_t)hdr[9 + KINL] << 32)};
-    const PTerms tq = pterms(pc.mag, pc.sumsq, A.B);
+    const PTerms tq = pterms_mk(pc.mag, pc.sumsq, A.B, A.fc.rB);
+    const PSm ps_q = psmall(pc, tq);
+    const double kq = (double)((int64_t)pc.mag - (int64_t)A.B * tq.ap);
+    const bool small_q = small_on && ps_q.ok;
     const MC_LDS uint32_t *lp = lpos[cur];
     // the controller's kills since the last record, against each entry of this thread
     {
@@ -1645,16 +1655,31 @@ __device__ __forceinline__ void worker_dstream(const AccArgs &A, const DevClassi
 #pragma unroll
         for (int k = 0; k < NC; k++)
           if (k < nch) v[k] = ld_sc1_16(R, slot(e, k) * 16u);
-        const PInfo pi{A.mag_s[p], A.sumsq_s[p], A.len_s[p]};
+        const uint4 inf = ld_sc1_16(R, slot(e, nch) * 16u);
         Acc<T> acc;
 #pragma unroll
         for (int k = 0; k < NC; k++)
           if (k < nch) acc.add(v[k], clds[k]);
-        double cv;
-        const PTerms pt = pterms(pi.mag, pi.sumsq, A.B);
-        const int d = A.fc.on    ? classify_fast(C, A.fc, acc.finish(pi.mag, pc.mag), pi, pt, pc, tq, A.B, &cv)
-                      : C.layout ? classify_std(C, acc.finish(pi.mag, pc.mag), pi, pt, pc, tq, A.B, &cv)
-                                 : classify_cand<T>(acc, pi, pc, A.B, C, &cv);
+        double cv = -1.0;
+        int d = 0;
+        bool und = true;
+        if constexpr (sizeof(T) == 1) {
+          if (small_q && inf.z != ~0u) {
+            const PSm ps{inf.x, inf.y, inf.z, inf.w, true};
+            acc.fold();
+            const double dap = C.layout == 4 ? mk_div((double)inf.x, (double)A.B, A.fc.rB) : 0.0;
+            d = classify_small(C, A.fc, acc.sad, acc.dot, ps, ps_q, kq, dap, tq.da, A.B, &cv, &und);
+          }
+        }
+        if (und) {  // (classify_small undecided or not applicable: the per-position arrays)
+          const PInfo pi{A.mag_s[p], A.sumsq_s[p], A.len_s[p]};
+          const PTerms pt = pterms(pi.mag, pi.sumsq, A.B);
+          double cx;
+          d = A.fc.on    ? classify_fast(C, A.fc, acc.finish(pi.mag, pc.mag), pi, pt, pc, tq, A.B, &cx)
+              : C.layout ? classify_std(C, acc.finish(pi.mag, pc.mag), pi, pt, pc, tq, A.B, &cx)
+                         : classify_cand<T>(acc, pi, pc, A.B, C, &cx);
+          if (cv == -1.0) cv = cx;
+        }
         if (d) {
           alive &= ~(1u << j);
           const uint32_t idx = atomicAdd(&s_nfl, 1u);
@@ -1752,7 +1777,7 @@ __device__ __forceinline__ void worker_dstream(const AccArgs &A, const DevClassi
         }
         if (al) {
           const uint32_t e = t + NT * j;
-          for (int k = 0; k < nch; k++) glb_st16(rb[nxt] + slot(r, k), ld_sc1_16(rr[cur], slot(e, k) * 16u));
+          for (int k = 0; k <= nch; k++) glb_st16(rb[nxt] + slot(r, k), ld_sc1_16(rr[cur], slot(e, k) * 16u));
           lpos[nxt][r] = lp[e];
         }
         base += tot;
@@ -2940,7 +2965,7 @@ int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, 
   // compacted row copies: one region of NT rows per local chunk (this rank's chunks); or the
   // dense streaming workers' two row buffers each
   const size_t cc_bytes = pl.compact    ? (size_t)(pl.fcap / NT) * GW * NT * (size_t)nch * 16
-                          : pl.dstream ? (size_t)2 * GW * pl.fcap * (size_t)nch * 16
+                          : pl.dstream ? (size_t)2 * GW * pl.fcap * (size_t)(nch + 1) * 16
                                        : 0;
   if (cc_bytes && ensure(c->s_k, cc_bytes)) return MC_ERR_OOM;
   MInfo *d_minfo = (MInfo *)c->s_i.p;
