@@ -306,7 +306,7 @@ __device__ void mean_closest(const HistView &H, const uint32_t *ids, const uint6
 
 constexpr int FT = 1024;
 
-template <typename T>
+template <typename T, bool GM>  // GM: the mean in global scratch (B > 4096), see mean_shift_kernel
 __global__ __launch_bounds__(FT) void finalize_kernel(HistView H, const ScanPartial *__restrict__ partials, int nparts,
                                                       ScanDev *__restrict__ sd, const uint32_t *__restrict__ members,
                                                       const uint64_t *__restrict__ mkeys, double *__restrict__ gmean) {
@@ -339,7 +339,9 @@ __global__ __launch_bounds__(FT) void finalize_kernel(HistView H, const ScanPart
   const uint32_t nflag = sd->nflag;
   const uint32_t M = sd->nmembers + nflag;
   if (nflag > 0) {
-    double *mean = H.B <= 4096 ? mean_lds : gmean;
+    double *mean;
+    if constexpr (GM) mean = gmean;
+    else mean = mean_lds;
     mean_closest<T, FT>(H, members, mkeys, M, mean, &new_id);
   }
   if (threadIdx.x == 0) {
@@ -368,7 +370,9 @@ __global__ __launch_bounds__(FT) void finalize_kernel(HistView H, const ScanPart
 // One workgroup per centre j: members of clusters j-delta..j+delta (cluster order) are
 // classified against centre j (Trainer::filter, Trainer.cpp:334-349); the survivors' mean
 // and the first survivor closest to it (Trainer::closest, :351-365) give the new centre.
-template <typename T>
+// GM: the column sums / mean in global scratch (they do not fit LDS with the centre's chunks) --
+// a compile-time choice: picked at run time, the buffer's accesses would be FLAT instructions.
+template <typename T, bool GM>
 __global__ __launch_bounds__(NT) void mean_shift_kernel(HistView H, DevClassifier C, const uint32_t *__restrict__ cid,
                                                         uint32_t Cn, const uint64_t *__restrict__ off,
                                                         const uint32_t *__restrict__ mem, int delta,
@@ -442,7 +446,9 @@ __global__ __launch_bounds__(NT) void mean_shift_kernel(HistView H, DevClassifie
     return;
   }
   // (launch_mean_shift's LDS plan: the sums stay in LDS when the chunks and B doubles fit 64 KiB)
-  double *mbuf = nch * 16 + H.B * 8 <= 65536 ? mean : gmean + (uint64_t)j * H.B;
+  double *mbuf;
+  if constexpr (GM) mbuf = gmean + (uint64_t)j * H.B;
+  else mbuf = mean;
   if constexpr (sizeof(T) <= 2) {
     // integer mean + SAD closest (tests/test_identities.py); sums reuse the mean buffer
     const RowRef R{reinterpret_cast<const uint4 *>(H.hist), H.pitch / 16, 1};
@@ -569,7 +575,7 @@ int launch_finalize(mc_ctx *c, int nblocks) {
   const size_t lds = H.B <= 4096 ? (size_t)H.B * 8 : 0;
   if (H.B > 4096 && ensure(c->s_g, (size_t)H.B * 8)) return MC_ERR_OOM;
   timed_begin(c);
-  MCG_DISPATCH_T(c->width, (finalize_kernel<T><<<1, FT, lds, c->stream>>>(
+  MCG_DISPATCH_T(c->width, ((H.B > 4096 ? finalize_kernel<T, true> : finalize_kernel<T, false>)<<<1, FT, lds, c->stream>>>(
                                H, (const ScanPartial *)c->partials.p, nblocks, (ScanDev *)c->scan_dev.p,
                                (const uint32_t *)c->members.p, (const uint64_t *)c->member_keys.p,
                                (double *)c->s_g.p)));
@@ -598,7 +604,7 @@ int launch_mean_shift(mc_ctx *c, const uint32_t *d_cid, uint32_t C, const uint64
   MCG_CHECK(hipMemcpyAsync(c->s_d.p, soff.data(), (C + 1) * 8, hipMemcpyHostToDevice, c->stream));
   const size_t lds = (size_t)nch * 16 + (gm ? 0 : (size_t)H.B * 8);
   timed_begin(c);
-  MCG_DISPATCH_T(c->width, (mean_shift_kernel<T><<<j1 - j0, NT, lds, c->stream>>>(
+  MCG_DISPATCH_T(c->width, ((gm ? mean_shift_kernel<T, true> : mean_shift_kernel<T, false>)<<<j1 - j0, NT, lds, c->stream>>>(
                                H, c->cls, d_cid, C, d_off, d_mem, delta, (const uint64_t *)c->s_d.p,
                                (uint32_t *)c->s_e.p, (uint32_t *)c->s_f.p, (double *)c->s_g.p, d_keep, d_new, j0)));
   MCG_CHECK(hipGetLastError());

@@ -292,14 +292,18 @@ __device__ __forceinline__ void write_row(const KArgs &A, uint64_t s, uint32_t *
   *wmax = mx > *wmax ? mx : *wmax;
 }
 
-template <typename T>
+// GLOB: the tables in global scratch (k >= 8).  A compile-time choice: a table pointer picked
+// at run time between LDS and global memory makes every table access a FLAT instruction.
+template <typename T, bool GLOB>
 __global__ __launch_bounds__(KT) void kmer_kernel(KArgs A, bool write) {
   extern __shared__ __attribute__((aligned(16))) uint32_t ltab[];
   __shared__ uint64_t s_max[KW];
   const int B = 1 << (2 * A.k);
   const int wv = wave_id(), lane = threadIdx.x & 63;
-  const bool glob = A.gtab != nullptr;
-  uint32_t *base = glob ? A.gtab + (uint64_t)blockIdx.x * KW * (uint64_t)B : ltab;  // this workgroup's tables
+  constexpr bool glob = GLOB;
+  uint32_t *base;  // this workgroup's tables
+  if constexpr (GLOB) base = A.gtab + (uint64_t)blockIdx.x * KW * (uint64_t)B;
+  else base = ltab;
   uint32_t *mytab = base + (A.shared ? 0 : (size_t)wv * B);
   uint64_t wmax = 0;
   if (!A.shared || wv == 0)
@@ -402,11 +406,12 @@ int launch_kmer(mc_ctx *c, int k, int width, bool write, uint64_t *d_max, int *d
     A.gtab = (uint32_t *)c->s_g.p;
   }
   timed_begin(c);
+  const bool g = A.gtab != nullptr;
   switch (width) {
-    case 1: kmer_kernel<uint8_t><<<grid, KT, lds, c->stream>>>(A, write); break;
-    case 2: kmer_kernel<uint16_t><<<grid, KT, lds, c->stream>>>(A, write); break;
-    case 4: kmer_kernel<uint32_t><<<grid, KT, lds, c->stream>>>(A, write); break;
-    default: kmer_kernel<uint64_t><<<grid, KT, lds, c->stream>>>(A, write); break;
+    case 1: (g ? kmer_kernel<uint8_t, true> : kmer_kernel<uint8_t, false>)<<<grid, KT, lds, c->stream>>>(A, write); break;
+    case 2: (g ? kmer_kernel<uint16_t, true> : kmer_kernel<uint16_t, false>)<<<grid, KT, lds, c->stream>>>(A, write); break;
+    case 4: (g ? kmer_kernel<uint32_t, true> : kmer_kernel<uint32_t, false>)<<<grid, KT, lds, c->stream>>>(A, write); break;
+    default: (g ? kmer_kernel<uint64_t, true> : kmer_kernel<uint64_t, false>)<<<grid, KT, lds, c->stream>>>(A, write); break;
   }
   MCG_CHECK(hipGetLastError());
   timed_end(c, F_KMER);

@@ -123,7 +123,9 @@ __device__ __forceinline__ bool better(double v, uint64_t p, double bv, uint64_t
   return v > bv || (v == bv && p < bp);
 }
 
-template <typename T>
+// GS: the cluster's column sums in global memory (B > 4096) -- a compile-time choice, so the
+// LDS sums are not FLAT accesses
+template <typename T, bool GS>
 __global__ __launch_bounds__(ST) void fused_scan_kernel(FusedArgs A, DevClassifier C) {
   extern __shared__ __attribute__((aligned(16))) uint4 dyn[];
   uint4 *clds = dyn;          // centre chunks
@@ -259,12 +261,14 @@ __global__ __launch_bounds__(ST) void fused_scan_kernel(FusedArgs A, DevClassifi
     const RowRef R{A.hs, 1, A.npad};
     // integer column sums of the cluster: running sum from the previous step (or the new
     // cluster's first member) + this step's flagged members, folded in LDS
-    uint64_t *lsum = A.B <= 4096 ? reinterpret_cast<uint64_t *>(Fl + A.nch) : A.msum;
+    uint64_t *lsum;
+    if constexpr (GS) lsum = A.msum;
+    else lsum = reinterpret_cast<uint64_t *>(Fl + A.nch);
     for (int b = threadIdx.x; b < A.B; b += ST) lsum[b] = A.new_cluster ? elem<T>(R, A.first_pos, b) : A.msum[b];
     __syncthreads();
     add_rows<T, ST>(R, A.flags_dev, nflag, A.nch, lsum);
     __syncthreads();
-    if (lsum != A.msum)
+    if constexpr (!GS)
       for (int b = threadIdx.x; b < A.B; b += ST) A.msum[b] = lsum[b];
     STAMP(4);
     const uint64_t win = mean_closest_fast<T, ST>(R, A.mem_pos, A.mkeys, M, A.mag_s, A.B, A.nch, lsum, Fl);
@@ -301,7 +305,7 @@ __global__ __launch_bounds__(ST) void fused_scan_kernel(FusedArgs A, DevClassifi
   }
 }
 
-template <typename T>
+template <typename T, bool GS>
 __global__ __launch_bounds__(ST) void commit_kernel(CommitArgs A) {
   extern __shared__ __attribute__((aligned(16))) uint4 dyn[];
   uint4 *Fl = dyn;  // packed integer mean
@@ -321,12 +325,14 @@ __global__ __launch_bounds__(ST) void commit_kernel(CommitArgs A) {
   uint32_t new_id = 0xffffffffu;
   if (A.nflag > 0) {  // the same running integer sums + closest member as fused_scan_kernel
     const RowRef R{A.hs, 1, A.npad};
-    uint64_t *lsum = A.B <= 4096 ? reinterpret_cast<uint64_t *>(Fl + A.nch) : A.msum;
+    uint64_t *lsum;
+    if constexpr (GS) lsum = A.msum;
+    else lsum = reinterpret_cast<uint64_t *>(Fl + A.nch);
     for (int b = threadIdx.x; b < A.B; b += ST) lsum[b] = A.new_cluster ? elem<T>(R, A.first_pos, b) : A.msum[b];
     __syncthreads();
     add_rows<T, ST>(R, A.flags_dev, A.nflag, A.nch, lsum);
     __syncthreads();
-    if (lsum != A.msum)
+    if constexpr (!GS)
       for (int b = threadIdx.x; b < A.B; b += ST) A.msum[b] = lsum[b];
     const uint64_t win = mean_closest_fast<T, ST>(R, A.mem_pos, A.mkeys, M, A.mag_s, A.B, A.nch, lsum, Fl);
     new_id = A.order[win];
@@ -449,8 +455,9 @@ int launch_fused_scan(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, uint32
 #endif
   const size_t lds = (size_t)2 * nch * 16 + (c->B <= 4096 ? (size_t)c->B * 8 : 0);
   timed_begin(c);
-  if (c->width == 1) fused_scan_kernel<uint8_t><<<grid, ST, lds, c->stream>>>(A, c->cls);
-  else fused_scan_kernel<uint16_t><<<grid, ST, lds, c->stream>>>(A, c->cls);
+  const bool gs = c->B > 4096;
+  if (c->width == 1) (gs ? fused_scan_kernel<uint8_t, true> : fused_scan_kernel<uint8_t, false>)<<<grid, ST, lds, c->stream>>>(A, c->cls);
+  else (gs ? fused_scan_kernel<uint16_t, true> : fused_scan_kernel<uint16_t, false>)<<<grid, ST, lds, c->stream>>>(A, c->cls);
   MCG_CHECK(hipGetLastError());
   timed_end(c, F_SCAN);
   c->pending_kills.clear();
@@ -482,8 +489,9 @@ int launch_commit(mc_ctx *c, const uint32_t *d_flags, uint32_t nflag, uint32_t s
   A.seq = seq;
   const size_t lds = (size_t)nch * 16 + (c->B <= 4096 ? (size_t)c->B * 8 : 0);
   timed_begin(c);
-  if (c->width == 1) commit_kernel<uint8_t><<<1, ST, lds, c->stream>>>(A);
-  else commit_kernel<uint16_t><<<1, ST, lds, c->stream>>>(A);
+  const bool gs = c->B > 4096;
+  if (c->width == 1) (gs ? commit_kernel<uint8_t, true> : commit_kernel<uint8_t, false>)<<<1, ST, lds, c->stream>>>(A);
+  else (gs ? commit_kernel<uint16_t, true> : commit_kernel<uint16_t, false>)<<<1, ST, lds, c->stream>>>(A);
   MCG_CHECK(hipGetLastError());
   timed_end(c, F_SCAN);
   c->pending_begin = false;

@@ -43,7 +43,10 @@ constexpr size_t SEL_LDS = (size_t)LMAX * 8 + 2 * (size_t)LMAX * 2;
 
 __device__ __forceinline__ bool kless(uint64_t x, uint64_t y) { return (x >> 32) < (y >> 32); }
 
-__device__ void insertion_sort_1(uint64_t *f, int64_t n) {  // std::__insertion_sort (stable)
+// (FP: a global or an LDS-typed pointer -- the two paths stay apart, no FLAT accesses)
+#define SP_LDS __attribute__((address_space(3)))
+template <typename FP>
+__device__ void insertion_sort_1(FP f, int64_t n) {  // std::__insertion_sort (stable)
   for (int64_t i = 1; i < n; i++) {
     const uint64_t v = f[i];
     int64_t j = i;
@@ -56,7 +59,8 @@ __device__ void insertion_sort_1(uint64_t *f, int64_t n) {  // std::__insertion_
 }
 
 // libstdc++'s std::__adjust_heap / std::__push_heap with the key comparator
-__device__ void adjust_heap_1(uint64_t *f, int64_t hole, int64_t len, uint64_t v) {
+template <typename FP>
+__device__ void adjust_heap_1(FP f, int64_t hole, int64_t len, uint64_t v) {
   const int64_t top = hole;
   int64_t child = hole;
   while (child < (len - 1) / 2) {
@@ -81,7 +85,8 @@ __device__ void adjust_heap_1(uint64_t *f, int64_t hole, int64_t len, uint64_t v
 
 // std::__partial_sort(first, last, last) = std::__make_heap + std::__sort_heap (one thread:
 // reached only below the depth limit, i.e. on degenerate partitions)
-__device__ void heap_sort_1(uint64_t *f, int64_t n) {
+template <typename FP>
+__device__ void heap_sort_1(FP f, int64_t n) {
   if (n < 2) return;
   for (int64_t parent = (n - 2) / 2;; parent--) {
     adjust_heap_1(f, parent, n, f[parent]);
@@ -147,8 +152,8 @@ __device__ __forceinline__ void block_scan2(uint32_t a, uint32_t b, uint32_t *ea
 // One workgroup partitions f[0, n) (n > 16) exactly as std::__unguarded_partition_pivot;
 // returns the cut.  L / R: scratch for n positions each (global u32, or LDS u16 when f is the
 // LDS copy of a range of at most LMAX words).
-template <typename PT>
-__device__ int64_t partition_wg(uint64_t *f, int64_t n, PT *L, PT *R, uint32_t *s32, uint64_t *s64) {
+template <typename PT, typename FP>
+__device__ int64_t partition_wg(FP f, int64_t n, PT *L, PT *R, uint32_t *s32, uint64_t *s64) {
   const int t = threadIdx.x;
   if (t == 0) {  // std::__move_median_to_first(first, first + 1, mid, last - 1)
     const uint64_t a = f[1], b = f[n / 2], c = f[n - 1];
@@ -306,7 +311,7 @@ __global__ __launch_bounds__(ST) void select_kernel(SelArgs a) {
       const SplitNode x = s_nd;
       __syncthreads();  // (s_nd is rewritten below)
       if (x.fin) {
-        if (t == 0) a.qout[q] = in_lds ? LW[pos - lbase] : W[pos];
+        if (t == 0) a.qout[q] = in_lds ? ((SP_LDS uint64_t *)LW)[pos - lbase] : W[pos];
         break;
       }
       if (x.left >= 0) {  // (never in LDS: the nodes visited there are fresh)
@@ -325,11 +330,17 @@ __global__ __launch_bounds__(ST) void select_kernel(SelArgs a) {
         __syncthreads();
         mark(1);
       }
-      uint64_t *f = in_lds ? LW + (x.lo - lbase) : W + x.lo;
+      SP_LDS uint64_t *fl = (SP_LDS uint64_t *)LW + (x.lo - lbase);
+      uint64_t *fg = W + x.lo;
       if (n <= 16 || x.depth == 0) {  // a leaf, or the heapsort fallback below the depth limit
         if (t == 0) {
-          if (n <= 16) insertion_sort_1(f, n);
-          else heap_sort_1(f, n);
+          if (in_lds) {
+            if (n <= 16) insertion_sort_1(fl, n);
+            else heap_sort_1(fl, n);
+          } else {
+            if (n <= 16) insertion_sort_1(fg, n);
+            else heap_sort_1(fg, n);
+          }
           nd[idx].fin = 1;
           s_nd.fin = 1;
         }
@@ -337,8 +348,8 @@ __global__ __launch_bounds__(ST) void select_kernel(SelArgs a) {
         mark(2);
         continue;
       }
-      const int64_t cut = x.lo + (in_lds ? partition_wg<uint16_t>(f, n, LL, LR, s32, s64)
-                                         : partition_wg<uint32_t>(f, n, L + x.lo, R + x.lo, s32, s64));
+      const int64_t cut = x.lo + (in_lds ? partition_wg<uint16_t>(fl, n, LL, LR, s32, s64)
+                                         : partition_wg<uint32_t>(fg, n, L + x.lo, R + x.lo, s32, s64));
       if (t == 0) {
         if (s_nn + 2 > a.maxnode) {
           atomicMax(a.err, 1);
