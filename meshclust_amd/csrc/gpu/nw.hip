@@ -410,18 +410,18 @@ __global__ __launch_bounds__(64 * W) void nw_mw_kernel(NWPairs q) {
   }
 }
 
-// Waves per pair in the latency form.  Up to 1,024 rows four waves (one per SIMD, R = 4)
-// measured fastest; longer pairs (config E's 8-12 kb genomes) run eight (two waves per SIMD,
-// one wave's dependent-issue stalls filled by the other's cells): 14 % less end-to-end time
-// on the 10 kb sets, while eight waves on 1 kb pairs cost 7 % more NW time (profiles/
-// r01_v7_nw_waves.txt).  MC_NW_WAVES = 2, 4, 8 or 16 forces one width for every pair.
-inline int mw_waves(uint64_t la) {
+// Waves per pair in the latency form: four (one per SIMD) at every length.  Round 1 measured
+// eight faster for config E's 8-12 kb genomes (profiles/r01_v7_nw_waves.txt); on the round-4
+// kernels four waves are faster there too: E9100's sampler rounds 301 ms against 317-319 ms at
+// eight, 369 ms at sixteen and 577 ms at two (profiles/r04/v5/nw_width.txt).  MC_NW_WAVES = 2,
+// 4, 8 or 16 forces one width for every pair.
+inline int mw_waves(uint64_t) {
   static const int forced = [] {
     const char *e = getenv("MC_NW_WAVES");
     const int v = e ? atoi(e) : 0;
     return v == 2 || v == 4 || v == 8 || v == 16 ? v : 0;
   }();
-  return forced ? forced : la <= 1024 ? 4 : 8;
+  return forced ? forced : 4;
 }
 
 template <int R, typename P>
