@@ -306,8 +306,12 @@ def main():
                 "bytes_per_eval": eval_bytes, "evals_per_launch": round(scan_evals / fam_n["scan"], 1),
                 "avg_launch_us": round(avg_s * 1e6, 2),
                 "us_per_step": round(fam_ms["scan"] * 1e3 / sum(s["scan_steps"] for s in stats), 2),
-                "note": "priced against HBM by algorithmic bytes (SURVEY.md §8(d)); the rows stay in LDS, "
-                        "so the kernel is bound by its dependent step chain, not by HBM (DESIGN.md §3.1)"}
+                "note": ("priced against HBM by algorithmic bytes (SURVEY.md §8(d)); the rows stay in LDS, "
+                         "so the kernel is bound by its dependent step chain, not by HBM (DESIGN.md §3.1)")
+                        if a.workload == "B" else
+                        ("priced against HBM by algorithmic bytes (SURVEY.md §8(d)); on one to four GPUs "
+                         "the workers stream every window's rows from HBM (dense streaming form, DESIGN.md "
+                         "§3.1c); at eight each rank's share of the rows is LDS-resident (§6)")}
         if a.workload == "B" and not shard and world == 1:  # (the counters are of the config-B launch)
             tr = kernel_pmc(kname)
             if tr is not None:
@@ -325,7 +329,7 @@ def main():
                                  "algorithmic_bytes_per_launch": round(kb), "avg_launch_us": round(ks * 1e6, 2),
                                  "achieved": round(kb / ks / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                  "frac": round(kb / ks / 1e9 / HBM_PEAK_GBS, 4),
-                                 "traffic": kernel_pmc("kmer_kernel<unsigned char") if width == 1 else None}
+                                 "traffic": kernel_pmc("kmer_kernel<unsigned char") if width == 1 and a.workload == "B" else None}
     if fam_n["mean_shift"]:
         mb = sum(s["update_evals"] for s in stats) * (B * width + 16) / fam_n["mean_shift"] / (world if shard else 1)
         ms = fam_ms["mean_shift"] / fam_n["mean_shift"] / 1e3
@@ -333,7 +337,7 @@ def main():
                                        "algorithmic_bytes_per_launch": round(mb), "avg_launch_us": round(ms * 1e6, 2),
                                        "achieved": round(mb / ms / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                        "frac": round(mb / ms / 1e9 / HBM_PEAK_GBS, 4),
-                                       "traffic": kernel_pmc("mean_shift_kernel<unsigned char") if width == 1 else None}
+                                       "traffic": kernel_pmc("mean_shift_kernel<unsigned char") if width == 1 and a.workload == "B" else None}
     nw_cells = sum(s["nw_cells"] for s in stats)
     nw_rate = nw_cells / (fam_ms["nw"] / 1e3) if fam_ms["nw"] else None
     # NW is VALU-bound: the peak is the int32 VALU issue rate (lane-instructions
