@@ -2472,7 +2472,20 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
           uint32_t sum[per];
 #pragma unroll
           for (int e = 0; e < per; e++) sum[e] = 0;
-          for (uint32_t i = (uint32_t)sl; i < nlist; i += (uint32_t)nsl) {
+          // (eight members' chunks in flight per thread: the loads are independent)
+          uint32_t i = (uint32_t)sl;
+          for (; i + 7u * (uint32_t)nsl < nlist; i += 8u * (uint32_t)nsl) {
+            uint4 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) v[u] = A.hr[(uint64_t)s_plist[i + (uint32_t)u * (uint32_t)nsl] * nch + c];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+              const T *pv = reinterpret_cast<const T *>(&v[u]);
+#pragma unroll
+              for (int e = 0; e < per; e++) sum[e] += pv[e];
+            }
+          }
+          for (; i < nlist; i += (uint32_t)nsl) {
             const uint4 v = A.hr[(uint64_t)s_plist[i] * nch + c];
             const T *pv = reinterpret_cast<const T *>(&v);
 #pragma unroll
@@ -2532,21 +2545,12 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
       if constexpr (WIDE) {
         // one member per wave (rows from `hr`, 64 lanes over the row): every lane ends with
         // the wave's first minimum
-        for (uint64_t q = wv; q < M; q += NW) {
+        auto member_row = [&](uint64_t q) -> const uint4 * {
           const uint32_t r = q < A.mrow ? lds_u32(mc.pos + q) : ld32(A.mem_pos + cl_start + q);
-          const uint4 *row = A.hr + (uint64_t)r * nch;
-          Acc<T> acc;
-          int c = lane;
-          for (; c + 192 < nch; c += 256) {
-            const uint4 v0 = row[c], v1 = row[c + 64], v2 = row[c + 128], v3 = row[c + 192];
-            acc.add(v0, F4[c]);
-            acc.add(v1, F4[c + 64]);
-            acc.add(v2, F4[c + 128]);
-            acc.add(v3, F4[c + 192]);
-          }
-          for (; c < nch; c += 64) acc.add(row[c], F4[c]);
-          acc.wave_reduce();
-          const uint64_t mp = q < A.mrow ? lds_u64(mc.info + q * 3) : A.mag_s[r];
+          return A.hr + (uint64_t)r * nch;
+        };
+        auto score = [&](uint64_t q, Acc<T> &acc) {
+          const uint64_t mp = q < A.mrow ? lds_u64(mc.info + q * 3) : A.mag_s[ld32(A.mem_pos + cl_start + q)];
           const uint64_t key = q < A.mrow ? lds_u64(mc.key + q) : ld64(A.mkeys + cl_start + q);
           const PS s = acc.finish(mp, sumF);
           const double frac = (double)(2 * s.smin) / (double)(mp + sumF);
@@ -2555,6 +2559,60 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
             bd = d;
             bk = key;
             bq = q;
+          }
+        };
+        if (nch <= 256) {
+          // at most four chunks per lane: the next member's row is loaded while this one is
+          // reduced (two members in flight per wave; a past-the-end load re-reads a valid row,
+          // so every trip issues the same loads)
+          auto load = [&](uint64_t q, uint4 (&v)[4]) {
+            const uint4 *row = member_row(q < M ? q : (uint64_t)wv);
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+              const int c = lane + 64 * u;
+              v[u] = row[c < nch ? c : nch - 1];
+            }
+          };
+          auto reduce = [&](uint64_t q, const uint4 (&v)[4]) {
+            Acc<T> acc;
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+              const int c = lane + 64 * u;
+              if (c < nch) acc.add_sad(v[u], F4[c]);
+            }
+            acc.wave_reduce();
+            score(q, acc);
+          };
+          uint4 va[4], vb[4];
+          uint64_t q = wv;
+          if (q < M) {
+            load(q, va);
+            for (;;) {
+              load(q + NW, vb);
+              reduce(q, va);
+              q += NW;
+              if (q >= M) break;
+              load(q + NW, va);
+              reduce(q, vb);
+              q += NW;
+              if (q >= M) break;
+            }
+          }
+        } else {
+          for (uint64_t q = wv; q < M; q += NW) {
+            const uint4 *row = member_row(q);
+            Acc<T> acc;
+            int c = lane;
+            for (; c + 192 < nch; c += 256) {
+              const uint4 v0 = row[c], v1 = row[c + 64], v2 = row[c + 128], v3 = row[c + 192];
+              acc.add_sad(v0, F4[c]);
+              acc.add_sad(v1, F4[c + 64]);
+              acc.add_sad(v2, F4[c + 128]);
+              acc.add_sad(v3, F4[c + 192]);
+            }
+            for (; c < nch; c += 64) acc.add_sad(row[c], F4[c]);
+            acc.wave_reduce();
+            score(q, acc);
           }
         }
       } else if (NCH > 0 && NC % 4 == 0 && sizeof(T) == 1 && (A.dbg & 2)) {
