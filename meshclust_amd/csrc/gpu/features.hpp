@@ -549,11 +549,62 @@ __device__ __forceinline__ uint4 ld16(const uint8_t *row, int ch) {
 // Integer pair statistics for the 64 candidates of one wave, 16 lanes per histogram row so
 // every load instruction reads four whole 256-byte rows (1 KiB) contiguously.  Lane l ends up
 // with the statistics of the pair it owns (my_a vs my_b, or my_a vs the LDS-resident centre).
+// Rows of at most 16 chunks (8-bit bins up to k = 4): one chunk per lane and row, so the 16
+// passes' loads are independent -- issued CEN ? 8 : 4 passes at a time (their rows and
+// magnitudes in flight together, clamped addresses for the idle lanes) instead of one round
+// trip per pass.
+template <typename T, int BATCH, bool CEN>
+__device__ __forceinline__ PS wave_pair_stats_short(const HistView &H, uint32_t my_a, uint32_t my_b, bool valid,
+                                                    const uint4 *centre_lds, uint64_t centre_mag, int nch) {
+  const int lane = threadIdx.x & 63, group = lane >> 4, lig = lane & 15;
+  const int ch = lig < nch ? lig : 0;
+  PS mine{0, 0, 0};
+  for (int p0 = 0; p0 < 16; p0 += BATCH) {
+    uint4 ra[BATCH], rb[BATCH];
+    uint64_t ma[BATCH], mb[BATCH];
+    bool vv[BATCH];
+#pragma unroll
+    for (int u = 0; u < BATCH; u++) {
+      const int cl = (p0 + u) * 4 + group;
+      const uint32_t a = __shfl(my_a, cl, 64);
+      const int v = __shfl((int)valid, cl, 64);
+      vv[u] = v != 0;
+      const uint32_t a0 = v ? a : 0u;  // (row 0 stands in for an idle group: a valid address)
+      ra[u] = ld16<T>(H.hist + (uint64_t)a0 * H.pitch, ch);
+      ma[u] = H.mag[a0];
+      if constexpr (CEN) {
+        rb[u] = centre_lds[ch];
+        mb[u] = centre_mag;
+      } else {
+        const uint32_t b = __shfl(my_b, cl, 64), b0 = v ? b : 0u;
+        rb[u] = ld16<T>(H.hist + (uint64_t)b0 * H.pitch, ch);
+        mb[u] = H.mag[b0];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < BATCH; u++) {
+      Acc<T> acc;
+      if (vv[u] && lig < nch) acc.add(ra[u], rb[u]);
+      acc.reduce16();
+      const PS s = acc.finish(vv[u] ? ma[u] : 0, CEN ? mb[u] : (vv[u] ? mb[u] : 0));
+      // lane l takes the result of pass l/4 from the leader of group l%4
+      const int src = (lane & 3) * 16;
+      const uint64_t x0 = shfl64(s.smin, src), x1 = shfl64(s.sabs, src), x2 = shfl64(s.sdot, src);
+      if (p0 + u == (lane >> 2)) mine = PS{x0, x1, x2};
+    }
+  }
+  return mine;
+}
+
 template <typename T>
 __device__ __forceinline__ PS wave_pair_stats(const HistView &H, uint32_t my_a, uint32_t my_b, bool valid,
                                               const uint4 *centre_lds, uint64_t centre_mag) {
   const int lane = threadIdx.x & 63, group = lane >> 4, lig = lane & 15;
   const int nch = (int)((H.B * (int)sizeof(T) + 15) / 16);
+  if (nch <= 16) {
+    if (centre_lds) return wave_pair_stats_short<T, 8, true>(H, my_a, my_b, valid, centre_lds, centre_mag, nch);
+    return wave_pair_stats_short<T, 4, false>(H, my_a, my_b, valid, centre_lds, centre_mag, nch);
+  }
   PS mine{0, 0, 0};
   for (int pass = 0; pass < 16; pass++) {
     const int cl = pass * 4 + group;
@@ -702,12 +753,12 @@ __device__ uint64_t mean_closest_fast(const RowRef &R, const uint32_t *rows, con
       int c = lane;
       for (; c + 192 < nch; c += 256) {
         const uint4 v0 = R.chunk(r, c), v1 = R.chunk(r, c + 64), v2 = R.chunk(r, c + 128), v3 = R.chunk(r, c + 192);
-        acc.add(v0, Fl[c]);
-        acc.add(v1, Fl[c + 64]);
-        acc.add(v2, Fl[c + 128]);
-        acc.add(v3, Fl[c + 192]);
+        acc.add_sad(v0, Fl[c]);
+        acc.add_sad(v1, Fl[c + 64]);
+        acc.add_sad(v2, Fl[c + 128]);
+        acc.add_sad(v3, Fl[c + 192]);
       }
-      for (; c < nch; c += 64) acc.add(R.chunk(r, c), Fl[c]);
+      for (; c < nch; c += 64) acc.add_sad(R.chunk(r, c), Fl[c]);
       acc.wave_reduce();
       const uint64_t mp = mags[r];
       const PS s = acc.finish(mp, sumF);
@@ -732,10 +783,10 @@ __device__ uint64_t mean_closest_fast(const RowRef &R, const uint32_t *rows, con
         f[c] = Fl[c];
       }
 #pragma unroll
-      for (int c = 0; c < 16; c++) acc.add(v[c], f[c]);
+      for (int c = 0; c < 16; c++) acc.add_sad(v[c], f[c]);  // (distance_d needs no dot product)
     } else {
 #pragma unroll 8
-      for (int c = 0; c < nch; c++) acc.add(R.chunk(r, c), Fl[c]);
+      for (int c = 0; c < nch; c++) acc.add_sad(R.chunk(r, c), Fl[c]);
     }
     const uint64_t mp = mags[r];
     const PS s = acc.finish(mp, sumF);

@@ -51,6 +51,51 @@ __global__ __launch_bounds__(NT) void distance_keys_kernel(HistView H, const uin
                                                            uint16_t *__restrict__ keys, uint32_t ptile) {
   extern __shared__ __attribute__((aligned(16))) uint4 plds[];
   const int nch = (int)((H.B * (int)sizeof(T) + 15) / 16);
+  if constexpr (sizeof(T) == 1) {
+    if (nch <= 16) {
+      // rows of at most 16 chunks (k <= 4): a point per lane, its row in registers, the pivot
+      // tile in LDS (broadcast reads); Smin from 4 v_sad_u8 per chunk and the magnitudes, no
+      // cross-lane reduction, and each pivot's 64 keys of a wave stored as one 128-byte run
+      uint64_t *pmag = reinterpret_cast<uint64_t *>(plds + (size_t)ptile * nch);
+      for (uint32_t p0 = 0; p0 < npiv; p0 += ptile) {
+        const uint32_t pn = min(ptile, npiv - p0);
+        __syncthreads();
+        for (uint32_t t = threadIdx.x; t < pn * (uint32_t)nch; t += NT) {
+          const uint32_t pp = t / nch, ch = t % nch;
+          plds[pp * nch + ch] = reinterpret_cast<const uint4 *>(H.hist + (uint64_t)piv[p0 + pp] * H.pitch)[ch];
+        }
+        for (uint32_t t = threadIdx.x; t < pn; t += NT) pmag[t] = H.mag[piv[p0 + t]];
+        __syncthreads();
+        for (uint64_t i = (uint64_t)blockIdx.x * NT + threadIdx.x; i - threadIdx.x < m; i += (uint64_t)gridDim.x * NT) {
+          const bool valid = i < m;
+          const uint32_t id = valid ? ids[i] : 0;
+          const uint4 *row = reinterpret_cast<const uint4 *>(H.hist + (uint64_t)id * H.pitch);
+          uint4 mine[16];
+#pragma unroll
+          for (int c = 0; c < 16; c++) mine[c] = c < nch ? row[c] : make_uint4(0, 0, 0, 0);
+          const uint64_t magi = H.mag[id];
+          for (uint32_t pp = 0; pp < pn; pp++) {
+            const uint4 *pr = plds + (size_t)pp * nch;
+            uint32_t s4[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int c = 0; c < 16; c++)
+              if (c < nch) {
+                const uint4 q = pr[c];
+                s4[0] = __builtin_amdgcn_sad_u8(mine[c].x, q.x, s4[0]);
+                s4[1] = __builtin_amdgcn_sad_u8(mine[c].y, q.y, s4[1]);
+                s4[2] = __builtin_amdgcn_sad_u8(mine[c].z, q.z, s4[2]);
+                s4[3] = __builtin_amdgcn_sad_u8(mine[c].w, q.w, s4[3]);
+              }
+            const uint32_t sad = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+            const uint64_t magp = pmag[pp];
+            const uint64_t smin = (magi + magp - sad) >> 1;
+            if (valid) keys[(uint64_t)(p0 + pp) * m + i] = (uint16_t)distance_key(smin, magi, magp);
+          }
+        }
+      }
+      return;
+    }
+  }
   const int lane = threadIdx.x & 63, group = lane >> 4, lig = lane & 15, wave = wave_id();
   const int rows_per_block = 16;  // 4 waves x 4 groups
   for (uint32_t p0 = 0; p0 < npiv; p0 += ptile) {
@@ -404,17 +449,21 @@ __global__ __launch_bounds__(NT) void mean_shift_kernel(HistView H, DevClassifie
   const uint64_t lo = off[bj], hi = off[ej + 1];
   uint32_t *mine = kept + soff[j];
   // survivors are compacted in member order: a wave ballot gives each survivor its rank
+  // (the next round's member id is loaded a round ahead, and a member's magnitudes before its
+  // pair statistics: their round trips overlap the row loads)
+  uint32_t id_next = lo + threadIdx.x < hi ? mem[lo + threadIdx.x] : 0;
   for (uint64_t base = lo; base < hi; base += NT) {
     const uint64_t q = base + threadIdx.x;
     const bool valid = q < hi;
-    const uint32_t id = valid ? mem[q] : 0;
+    const uint32_t id = valid ? id_next : 0;
+    id_next = q + NT < hi ? mem[q + NT] : 0;
     int d = 0;
     if (keep) {  // filter decision supplied by the caller (alignment mode)
       d = valid ? keep[soff[j] + (q - lo)] : 0;
     } else {
+      const PInfo pi = valid ? pinfo(H, id) : PInfo{0, 0, 0};
       PS s = wave_pair_stats<T>(H, id, centre, valid, clds, pc.mag);
       if (valid) {
-        const PInfo pi = pinfo(H, id);
         double raw[MC_MAX_SINGLE];
         raw_lookup<T>(H, C.c, s, id, centre, pi, pc, raw);
         double c0;
@@ -494,10 +543,11 @@ int launch_distance_keys(mc_ctx *c, const uint32_t *d_piv, uint32_t npiv, const 
   if (m == 0 || npiv == 0) return MC_OK;
   const HistView H = hist_view(c);
   const int nch = (int)((H.B * H.width + 15) / 16);
-  uint32_t ptile = (uint32_t)std::max(1, 65536 / (nch * 16));
+  const bool lane_rows = H.width == 1 && nch <= 16;  // (distance_keys_kernel's point-per-lane form)
+  uint32_t ptile = (uint32_t)std::max(1, 65536 / (nch * 16 + (lane_rows ? 8 : 0)));
   ptile = std::min(ptile, npiv);
-  const size_t lds = (size_t)ptile * nch * 16;
-  const int grid = grid_for(m, 16, 2048);
+  const size_t lds = (size_t)ptile * nch * 16 + (lane_rows ? (size_t)ptile * 8 : 0);
+  const int grid = lane_rows ? grid_for(m, NT, 2048) : grid_for(m, 16, 2048);
   timed_begin(c);
   MCG_DISPATCH_T(c->width, (distance_keys_kernel<T><<<grid, NT, lds, c->stream>>>(H, d_piv, npiv, d_ids, m, d_keys, ptile)));
   MCG_CHECK(hipGetLastError());
