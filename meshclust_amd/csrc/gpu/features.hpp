@@ -658,6 +658,37 @@ __device__ __forceinline__ uint64_t elem(const RowRef &R, uint64_t r, int b) {
 template <typename T, int NTH>
 __device__ __forceinline__ void add_rows(const RowRef &R, const uint32_t *rows, uint32_t M, int nch, uint64_t *sum) {
   constexpr int per = 16 / (int)sizeof(T);
+  if (nch * 2 <= NTH && (uint64_t)M * (sizeof(T) == 1 ? 0xffull : 0xffffull) <= 0xffffffffull && sizeof(T) <= 2) {
+    // short rows: thread (chunk c, slice sl) adds its chunk over the rows q = sl (mod nsl) in
+    // 32-bit registers, four rows' loads in flight, then one atomic per bin and thread -- nsl
+    // per bin instead of M (every row adding to the same bins was M-way atomic contention)
+    const int nsl = NTH / nch;
+    for (int t = threadIdx.x; t < nch * nsl; t += NTH) {
+      const int c = t % nch, sl = t / nch;
+      uint32_t acc[per];
+#pragma unroll
+      for (int e = 0; e < per; e++) acc[e] = 0;
+      uint32_t q = (uint32_t)sl;
+      for (; q + 3u * (uint32_t)nsl < M; q += 4u * (uint32_t)nsl) {
+        const uint4 v0 = R.chunk(rows[q], c), v1 = R.chunk(rows[q + (uint32_t)nsl], c),
+                    v2 = R.chunk(rows[q + 2u * (uint32_t)nsl], c), v3 = R.chunk(rows[q + 3u * (uint32_t)nsl], c);
+        const T *p0 = reinterpret_cast<const T *>(&v0), *p1 = reinterpret_cast<const T *>(&v1),
+                *p2 = reinterpret_cast<const T *>(&v2), *p3 = reinterpret_cast<const T *>(&v3);
+#pragma unroll
+        for (int e = 0; e < per; e++) acc[e] += (uint32_t)p0[e] + (uint32_t)p1[e] + (uint32_t)p2[e] + (uint32_t)p3[e];
+      }
+      for (; q < M; q += (uint32_t)nsl) {
+        const uint4 v = R.chunk(rows[q], c);
+        const T *pv = reinterpret_cast<const T *>(&v);
+#pragma unroll
+        for (int e = 0; e < per; e++) acc[e] += pv[e];
+      }
+#pragma unroll
+      for (int e = 0; e < per; e++)
+        if (acc[e]) atomicAdd((unsigned long long *)&sum[c * per + e], (unsigned long long)acc[e]);
+    }
+    return;
+  }
   const uint64_t items = (uint64_t)M * nch;
   for (uint64_t it = threadIdx.x; it < items; it += NTH) {
     const uint32_t q = (uint32_t)(it / nch);
