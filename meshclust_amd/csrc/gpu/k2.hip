@@ -426,7 +426,6 @@ __global__ __launch_bounds__(NT) void mean_shift_kernel(HistView H, DevClassifie
                                                         const uint8_t *__restrict__ keep, uint32_t *__restrict__ newc,
                                                         uint32_t jbase) {
   extern __shared__ __attribute__((aligned(16))) uint4 dyn[];
-  __shared__ uint32_t cnt;
   // XCD-aware order (speed only: blocks are dealt round-robin over the 8 XCDs): the blocks one
   // XCD runs take consecutive centres, so the neighbourhoods j - delta .. j + delta they read
   // overlap in that XCD's L2 instead of being fetched by eight L2s
@@ -441,7 +440,6 @@ __global__ __launch_bounds__(NT) void mean_shift_kernel(HistView H, DevClassifie
   double *mean = reinterpret_cast<double *>(dyn + nch);
   const uint32_t centre = cid[j];
   for (int t = threadIdx.x; t < nch; t += NT) clds[t] = reinterpret_cast<const uint4 *>(H.hist + (uint64_t)centre * H.pitch)[t];
-  if (threadIdx.x == 0) cnt = 0;
   __syncthreads();
   const PInfo pc = pinfo(H, centre);
   const uint32_t bj = j >= (uint32_t)delta ? j - (uint32_t)delta : 0;
@@ -452,6 +450,8 @@ __global__ __launch_bounds__(NT) void mean_shift_kernel(HistView H, DevClassifie
   // (the next round's member id is loaded a round ahead, and a member's magnitudes before its
   // pair statistics: their round trips overlap the row loads)
   uint32_t id_next = lo + threadIdx.x < hi ? mem[lo + threadIdx.x] : 0;
+  uint32_t kept_n = 0;  // survivors so far (uniform)
+  int par = 0;
   for (uint64_t base = lo; base < hi; base += NT) {
     const uint64_t q = base + threadIdx.x;
     const bool valid = q < hi;
@@ -470,25 +470,28 @@ __global__ __launch_bounds__(NT) void mean_shift_kernel(HistView H, DevClassifie
         d = classify_raw(C, raw, &c0, nullptr);
       }
     }
-    // ordered compaction within the workgroup: wave prefix via ballot, waves in order
-    __shared__ uint32_t wcount[NT / 64];
+    // ordered compaction within the workgroup: wave prefix via ballot, waves in order; the
+    // running count in every thread's register and the wave counts double-buffered, so a round
+    // takes one barrier (a buffer is rewritten two rounds later, after the next round's barrier)
+    __shared__ uint32_t wcount[2][NT / 64];
     const uint64_t bal = __ballot(d);
     const int lane = threadIdx.x & 63, w = wave_id();
-    if (lane == 0) wcount[w] = (uint32_t)__popcll(bal);
+    if (lane == 0) wcount[par][w] = (uint32_t)__popcll(bal);
     __syncthreads();
-    uint32_t before = cnt;
-    for (int i = 0; i < w; i++) before += wcount[i];
+    uint32_t before = kept_n, tot = 0;
+#pragma unroll
+    for (int i = 0; i < NT / 64; i++) {
+      const uint32_t x = wcount[par][i];
+      if (i < w) before += x;
+      tot += x;
+    }
     const uint32_t rank = (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
     if (d) mine[before + rank] = id;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      uint32_t t = 0;
-      for (int i = 0; i < NT / 64; i++) t += wcount[i];
-      cnt += t;
-    }
-    __syncthreads();
+    kept_n += tot;
+    par ^= 1;
   }
-  const uint32_t M = cnt;
+  __syncthreads();  // (the survivors' ids are read back by every thread below)
+  const uint32_t M = kept_n;
   if (threadIdx.x == 0) nkept[j] = M;
   if (M == 0) {
     if (threadIdx.x == 0) newc[j] = centre;
