@@ -127,7 +127,7 @@ struct KArgs {
 // `tab` with this wave's lanes taking 16 consecutive starts each; `part` / `nparts` split the
 // 16-start groups between the waves that share the sequence.
 __device__ __forceinline__ void count_range(const KArgs &A, uint64_t s, int64_t p_lo, int64_t p_hi, int64_t L,
-                                            bool pure, uint32_t *tab, int part, int nparts) {
+                                            bool pure, uint32_t *tab, int part, int nparts, uint64_t pk0, uint64_t pk1) {
   const int lane = threadIdx.x & 63;
   const int k = A.k;
   const uint32_t mask = k == 16 ? 0xffffffffu : ((1u << (2 * k)) - 1u);
@@ -141,8 +141,8 @@ __device__ __forceinline__ void count_range(const KArgs &A, uint64_t s, int64_t 
     }
     if (pure) {
       // bases [p0, p0 + cnt + k - 1) from the 2-bit words: a 64-bit window at bit 2*(p0 % 16)
-      const uint32_t *w = A.pk + A.pk_off[s] + (p0 >> 4);
-      const uint64_t nw = A.pk_off[s + 1] - A.pk_off[s] - (uint64_t)(p0 >> 4);
+      const uint32_t *w = A.pk + pk0 + (p0 >> 4);
+      const uint64_t nw = pk1 - pk0 - (uint64_t)(p0 >> 4);
       const uint64_t lo = ((uint64_t)(nw > 1 ? w[1] : 0u) << 32) | w[0];
       const uint64_t hi = nw > 2 ? w[2] : 0u;
       const int sh = (int)(p0 & 15) * 2;
@@ -178,7 +178,7 @@ __device__ __forceinline__ void count_sequence(const KArgs &A, uint64_t s, uint3
   const bool pure = A.impure[s] == 0;
   for (uint64_t g = A.seg_off[s]; g < A.seg_off[s + 1]; g++) {
     const int64_t first = A.seg[2 * g], last = (int64_t)A.seg[2 * g + 1] - A.k + 1;
-    count_range(A, s, first, last < first ? first : last, L, pure, tab, part, nparts);  // a short segment still hashes at `first`
+    count_range(A, s, first, last < first ? first : last, L, pure, tab, part, nparts, A.pk_off[s], A.pk_off[s + 1]);  // a short segment still hashes at `first`
   }
 }
 
@@ -202,7 +202,8 @@ __device__ __forceinline__ void tab_drain(bool glob) {
 // 8-bit rows from one LDS table with B a multiple of 256 (k >= 4): every lane takes 32-bit
 // words of the row (four bins: one 16-byte LDS read and one zeroing write), the wave's stores
 // are 256 contiguous bytes, and the magnitude / sum of squares / maximum are DPP reductions
-__device__ __forceinline__ void write_row8(const KArgs &A, uint64_t s, uint32_t *tab, int B, bool write, uint64_t *wmax) {
+__device__ __forceinline__ void write_row8(const KArgs &A, uint64_t s, uint32_t *tab, int B, bool write, uint64_t *wmax,
+                                           uint64_t len) {
   const int lane = threadIdx.x & 63;
   uint32_t m = 0, mx = 0;  // (a magnitude is the record's k-mer count + B: 32 bits below 4 Gb)
   uint64_t sq64 = 0;
@@ -230,18 +231,18 @@ __device__ __forceinline__ void write_row8(const KArgs &A, uint64_t s, uint32_t 
   if (lane == 0 && write) {
     A.mag[s] = m64;
     A.sumsq[s] = s64;
-    A.len_out[s] = A.seq_off[s + 1] - A.seq_off[s];
+    A.len_out[s] = len;
   }
   *wmax = wm > *wmax ? wm : *wmax;
 }
 
 template <typename T>
 __device__ __forceinline__ void write_row(const KArgs &A, uint64_t s, uint32_t *tab0, int ntab, int B, bool write,
-                                          bool glob, uint64_t *wmax) {
+                                          bool glob, uint64_t *wmax, uint64_t len) {
   const int lane = threadIdx.x & 63;
   if constexpr (sizeof(T) == 1) {
     if (ntab == 1 && !glob && (B & 255) == 0) {
-      write_row8(A, s, tab0, B, write, wmax);
+      write_row8(A, s, tab0, B, write, wmax, len);
       return;
     }
   }
@@ -287,7 +288,7 @@ __device__ __forceinline__ void write_row(const KArgs &A, uint64_t s, uint32_t *
   if (lane == 0 && write) {
     A.mag[s] = m;
     A.sumsq[s] = sq;
-    A.len_out[s] = A.seq_off[s + 1] - A.seq_off[s];
+    A.len_out[s] = len;
   }
   *wmax = mx > *wmax ? mx : *wmax;
 }
@@ -310,12 +311,35 @@ __global__ __launch_bounds__(KT) void kmer_kernel(KArgs A, bool write) {
     for (int b = lane; b < B; b += 64) tab_zero(mytab + b, glob);
   tab_drain(glob);
   if (!A.coop) {
-    // one wave per sequence: the wave's own table, no workgroup barrier
-    for (uint64_t s = (uint64_t)blockIdx.x * KW + wv; s < A.n; s += (uint64_t)gridDim.x * KW) {
-      count_sequence(A, s, mytab, 0, 1);
-      tab_drain(glob);
-      write_row<T>(A, s, mytab, 1, B, write, glob, &wmax);
-      tab_drain(glob);
+    // one wave per sequence: the wave's own table, no workgroup barrier.  The metadata of the
+    // wave's next 64 sequences (offsets, purity, segment bounds) are loaded lane by lane in two
+    // round trips and handed out by readlane, instead of a chain of dependent loads per sequence
+    const uint64_t stride = (uint64_t)gridDim.x * KW;
+    for (uint64_t sb = (uint64_t)blockIdx.x * KW + wv; sb < A.n; sb += 64 * stride) {
+      const uint64_t si = sb + (uint64_t)lane * stride;
+      const bool vi = si < A.n;
+      const uint64_t s0 = vi ? si : 0;
+      const uint64_t so0 = A.seq_off[s0], so1 = A.seq_off[s0 + 1], pk0 = A.pk_off[s0], pk1 = A.pk_off[s0 + 1];
+      const uint64_t g0 = A.seg_off[s0], g1 = A.seg_off[s0 + 1];
+      const bool one = vi && A.impure[s0] == 0 && g1 == g0 + 1;  // pure, one segment: the fast form
+      const int32_t sf = one ? A.seg[2 * g0] : 0, sl = one ? A.seg[2 * g0 + 1] : 0;
+      const uint64_t left = (A.n - sb + stride - 1) / stride;
+      const int nb = left < 64 ? (int)left : 64;
+      for (int jj = 0; jj < nb; jj++) {
+        const uint64_t s = sb + (uint64_t)jj * stride;
+        const uint64_t L = readlane64(so1, jj) - readlane64(so0, jj);
+        if (__builtin_amdgcn_readlane((int)one, jj)) {
+          const int64_t first = __builtin_amdgcn_readlane(sf, jj);
+          const int64_t last = (int64_t)__builtin_amdgcn_readlane(sl, jj) - A.k + 1;
+          count_range(A, s, first, last < first ? first : last, (int64_t)L, true, mytab, 0, 1, readlane64(pk0, jj),
+                      readlane64(pk1, jj));
+        } else {
+          count_sequence(A, s, mytab, 0, 1);
+        }
+        tab_drain(glob);
+        write_row<T>(A, s, mytab, 1, B, write, glob, &wmax, L);
+        tab_drain(glob);
+      }
     }
   } else {
     // the KW waves share a sequence (per-wave tables, or one shared table); wave 0 sums the
@@ -326,7 +350,7 @@ __global__ __launch_bounds__(KT) void kmer_kernel(KArgs A, bool write) {
       tab_drain(glob);
       __syncthreads();
       if (wv == 0) {
-        write_row<T>(A, s, base, A.shared ? 1 : KW, B, write, glob, &wmax);
+        write_row<T>(A, s, base, A.shared ? 1 : KW, B, write, glob, &wmax, A.seq_off[s + 1] - A.seq_off[s]);
         tab_drain(glob);
       }
       __syncthreads();
