@@ -134,6 +134,8 @@ struct AccArgs {
   int spec;         // the record carries a superset of the window; the exact one follows (dense)
   int poll1;        // the controller polls a partial's tag granule before loading it whole
   int psleep;       // s_sleep between the controller's polls of a partial (0, 1, 2, 4)
+  int rpoll;        // dense workers: waves polling the step record (MC_ACCUM_RPOLL, 1..4)
+  int rpoll_gap;    // ... wave w starts w * rpoll_gap * 512 clocks late (MC_ACCUM_RPOLL_GAP)
   uint32_t rec_g;
   uint64_t *klog;      // static positions killed by the controller (pop / erase), append-only,
                        // entry e a granule tagged e + 1 (a reader checks the tag: no drain
@@ -1004,7 +1006,9 @@ __device__ __forceinline__ void worker_dense(const AccArgs &A, const DevClassifi
   __shared__ uint64_t s_tw[NW];  // MC_ACCUM_PROFILE=4: each wave's scores-done time
   __shared__ uint64_t s_t0[3];   // ... thread 0's record-seen, scores-done and part-B times
   __shared__ uint32_t s_arr;     // waves that have reduced this step's scores
+  __shared__ uint32_t s_rgot;    // the step whose record a polling wave has written to srec
   constexpr int NC = NCH > 0 ? NCH : DMAXCH;
+  constexpr int RPW = (4 * NC + REC_HDR + 63) / 64;  // record words per polling lane
   const uint32_t GW = gridDim.x - 1, w = blockIdx.x - 1;
   const Div32 dgw(GW);
   const int lane = threadIdx.x & 63, wv = wave_id();
@@ -1043,33 +1047,51 @@ __device__ __forceinline__ void worker_dense(const AccArgs &A, const DevClassifi
     s_abort = 0;
     s_b[0] = s_b[1] = 0;
     s_arr = 0;
+    s_rgot = 0;
   }
   __syncthreads();
   uint32_t kcur = 0, seen = 0;
   for (;;) {
-    // ---- wait for the next step's record (wave 0), as `worker` ---------------------------
-    if (wv == 0) {
+    // ---- wait for the next step's record --------------------------------------------------
+    // Waves 0 .. rpoll-1 poll it, wave w starting w gaps later, so the record is seen within a
+    // fraction of one poll round trip after it lands; the first wave with every granule tagged
+    // writes the words to LDS and marks s_rgot (the others stop at their next check).  Wave 0
+    // alone takes the path of a worker that fell RING steps behind.
+    if (wv < A.rpoll) {
       const uint64_t t0 = now();
       const uint32_t want = seen + 1;
       int state = 0;
       uint32_t got = want;
       bool late = false;
       const uint64_t *rn = A.ring + (uint64_t)(want % RING) * A.rec_g;
+      for (int g = 0; g < wv * A.rpoll_gap; g++) __builtin_amdgcn_s_sleep(8);
       for (uint32_t it = 1;; it++) {
+        if (__hip_atomic_load(&s_rgot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == want) {
+          state = 1;
+          break;
+        }
         bool ok = true, ahead = false;
-        for (int j = lane; j < rec_words; j += 64) {
-          const uint64_t x = ld64(rn + j);
+        uint32_t xv[RPW];
+#pragma unroll
+        for (int u = 0; u < RPW; u++) {
+          const int j = lane + 64 * u;
+          const uint64_t x = j < rec_words ? ld64(rn + j) : gran(want, 0);
           const uint32_t tg = (uint32_t)(x >> 32);
           ok &= tg == want;
           ahead |= (int32_t)(tg - want) > 0;
-          srec[j] = (uint32_t)x;
+          xv[u] = (uint32_t)x;
         }
         if (__ballot(!ok) == 0) {
+#pragma unroll
+          for (int u = 0; u < RPW; u++)
+            if (lane + 64 * u < rec_words) srec[lane + 64 * u] = xv[u];
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+          if (lane == 0) __hip_atomic_store(&s_rgot, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           state = 1;
           break;
         }
         if (__ballot(ahead) != 0) {
-          late = true;
+          late = wv == 0;
           break;
         }
         if ((it & 255) == 0 && timed_out(A, t0)) {
@@ -1078,6 +1100,7 @@ __device__ __forceinline__ void worker_dense(const AccArgs &A, const DevClassifi
         }
         __builtin_amdgcn_s_sleep(1);
       }
+      if (wv == 0) {
       while (late && state == 0) {
         uint32_t v = 0;
         if (lane == 0) {
@@ -1107,6 +1130,9 @@ __device__ __forceinline__ void worker_dense(const AccArgs &A, const DevClassifi
         if (state == 2) s_abort = 1;
         s_go = got;
         s_nfl = 0;
+      }
+      } else if (state == 2 && lane == 0) {
+        s_abort = 1;
       }
     }
     __syncthreads();
@@ -3062,6 +3088,12 @@ int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, 
   A.ringb = A.ring + (size_t)RING * pl.rec_g;
   A.spec = (pl.dense || pl.dstream) && !getenv("MC_ACCUM_NO_SPEC") ? 1 : 0;
   A.poll1 = getenv("MC_ACCUM_POLL1") ? 1 : 0;
+  {
+    const char *e = getenv("MC_ACCUM_RPOLL"), *g = getenv("MC_ACCUM_RPOLL_GAP");
+    const int v = e ? atoi(e) : 1, gv = g ? atoi(g) : 2;
+    A.rpoll = v < 1 ? 1 : v > 4 ? 4 : v;
+    A.rpoll_gap = gv < 0 ? 0 : gv > 16 ? 16 : gv;
+  }
   A.psleep = getenv("MC_ACCUM_POLL_SLEEP") ? atoi(getenv("MC_ACCUM_POLL_SLEEP")) : 1;
   A.rec_g = pl.rec_g;
   A.partials = (uint64_t *)c->s_b.p;
