@@ -134,6 +134,7 @@ struct AccArgs {
   int spec;         // the record carries a superset of the window; the exact one follows (dense)
   int poll1;        // the controller polls a partial's tag granule before loading it whole
   int psleep;       // s_sleep between the controller's polls of a partial (0, 1, 2, 4)
+  int etake;        // a polling thread takes its worker's flagged members as soon as it has the partial
   int rpoll;        // dense workers: waves polling the step record (MC_ACCUM_RPOLL, 1..4)
   int rpoll_gap;    // ... wave w starts w * rpoll_gap * 512 clocks late (MC_ACCUM_RPOLL_GAP)
   uint32_t rec_g;
@@ -2307,6 +2308,7 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
             st64x(mslot + (slot < (uint32_t)MBOX_INL ? 5 + slot : MBOX_HDR - MBOX_INL + slot), gran(step, p));
           } else if (slot < PLIST) {
             s_plist[slot] = p;
+            if (A.etake) take(M + slot, p, false, (int64_t)slot);  // (MC_ACCUM_EARLY_TAKE)
           } else {  // a list overflow: this thread takes the member itself (past the cache)
             take(M + slot, p, true);
             drain();
@@ -2476,8 +2478,9 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
       // remove_available: the new members, one thread each, all their loads in flight at once
       // (member i on thread i + 64: wave 0, which publishes the next record, keeps no
       // outstanding stores for that record's drain to wait on)
-      for (uint64_t i = (threadIdx.x + NT - 64) % NT; i < nflag && i < PLIST; i += NT)
-        take(M + i, s_plist[i], false, (int64_t)i);
+      if (!A.etake || mslot)
+        for (uint64_t i = (threadIdx.x + NT - 64) % NT; i < nflag && i < PLIST; i += NT)
+          take(M + i, s_plist[i], false, (int64_t)i);
       npend = nflag < PLIST ? (uint32_t)nflag : PLIST;
       if (M + nflag > A.mrow) drain();  // members past the cache are read back from mem_pos / mkeys
       __syncthreads();
@@ -3088,6 +3091,7 @@ int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, 
   A.ringb = A.ring + (size_t)RING * pl.rec_g;
   A.spec = (pl.dense || pl.dstream) && !getenv("MC_ACCUM_NO_SPEC") ? 1 : 0;
   A.poll1 = getenv("MC_ACCUM_POLL1") ? 1 : 0;
+  A.etake = getenv("MC_ACCUM_EARLY_TAKE") && atoi(getenv("MC_ACCUM_EARLY_TAKE")) ? 1 : 0;
   {
     const char *e = getenv("MC_ACCUM_RPOLL"), *g = getenv("MC_ACCUM_RPOLL_GAP");
     const int v = e ? atoi(e) : 1, gv = g ? atoi(g) : 2;
