@@ -527,18 +527,26 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
   Scope s(timer, "update+merge");
   std::vector<uint8_t> fused_sim;
   std::vector<double> fused_c0;
+  // the clusters' member lists change only when the merge pass merged something (the
+  // partition shrinks): otherwise the next iteration reuses them as they are
+  std::vector<uint32_t> members;
+  std::vector<uint64_t> off;
+  bool rebuild = true;
   for (int it = 0; it < cfg.iterations; it++) {
     bool fused = false;
     uint64_t fused_np = 0;
     // mean_shift_update for every centre, all reading the same state (ClusterFactory.cpp:744-749)
     const uint32_t C = (uint32_t)part.size();
-    std::vector<uint32_t> cids(C), members, newc(C);
-    std::vector<uint64_t> off(C + 1, 0);
-    for (uint32_t j = 0; j < C; j++) {
-      cids[j] = part[j].centre;
-      members.insert(members.end(), part[j].points.begin(), part[j].points.end());
-      off[j + 1] = members.size();
+    std::vector<uint32_t> cids(C), newc(C);
+    if (rebuild) {
+      members.clear();
+      off.assign(C + 1, 0);
+      for (uint32_t j = 0; j < C; j++) {
+        members.insert(members.end(), part[j].points.begin(), part[j].points.end());
+        off[j + 1] = members.size();
+      }
     }
+    for (uint32_t j = 0; j < C; j++) cids[j] = part[j].centre;
     for (uint32_t j = 0; j < C; j++) {
       uint32_t b = j >= (uint32_t)cfg.delta ? j - cfg.delta : 0;
       uint32_t e = std::min<uint32_t>(j + cfg.delta, C - 1);
@@ -657,6 +665,7 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
     }
     Scope sc(timer, "update.cascade");
     merge_cascade(part, poff, sim, c0);
+    rebuild = part.size() != C;
   }
   return part;
 }
