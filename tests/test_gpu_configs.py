@@ -108,12 +108,14 @@ def test_config_B100k_global_bitmap_equals_reference(product):
     assert st["accum_path"] == "device"
 
 
-@pytest.mark.parametrize("env,tag", [({"MC_ACCUM_DBG": "3"}, ".dbg3"), ({"MC_CLASSIFY_EXACT": "1"}, ".exact")])
+@pytest.mark.parametrize("env,tag", [({"MC_ACCUM_DBG": "3"}, ".dbg3"), ({"MC_CLASSIFY_EXACT": "1"}, ".exact"),
+                                     ({"MC_CLASSIFY_NO_SMALL": "1"}, ".nosmall")])
 def test_config_B100k_accum_variants_equal_reference(product, env, tag):
     """The accumulation kernel's opt-in forms (per-bin aggregated bvec kills and the
-    quad-per-member closest search, MC_ACCUM_DBG=3) and the workers' exact classifier
-    (MC_CLASSIFY_EXACT: classify_std everywhere, no division-light decision) at config B, against
-    the reference's partition."""
+    quad-per-member closest search, MC_ACCUM_DBG=3), the workers' exact classifier
+    (MC_CLASSIFY_EXACT: classify_std everywhere, no division-light decision) and the
+    division-light decision without the small-magnitude form (MC_CLASSIFY_NO_SMALL:
+    classify_fast) at config B, against the reference's partition."""
     st = _big("B100k", product, 300, env=env, tag=tag)
     assert st["accum_path"] == "device"
 
