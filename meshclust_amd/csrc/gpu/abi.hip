@@ -1122,6 +1122,8 @@ int mc_accumulate(mc_ctx *c, const uint32_t *bin_lo, const uint64_t *bounds, uin
     fprintf(stderr, "[accum] closest: members scored %.3f, reduced %.3f, winner %.3f ms\n", out[18] / 1e5, out[19] / 1e5,
             out[20] / 1e5);
     fprintf(stderr, "[accum] window: record span %.3f, record stores issued %.3f ms\n", out[21] / 1e5, out[22] / 1e5);
+    fprintf(stderr, "[accum] window: bvec kills %.3f, fast form %.3f (%llu), general form %.3f (%llu) ms\n", out[23] / 1e5,
+            out[24] / 1e5, (unsigned long long)out[26], out[25] / 1e5, (unsigned long long)out[27]);
     if (out[17])  // the controller's shader-clock ticks over its 100 MHz real-time ticks
       fprintf(stderr, "[accum] controller shader clock %.0f MHz over %.3f ms\n", (double)out[16] / ((double)out[17] / 100.0),
               out[17] / 1e5);

@@ -135,6 +135,7 @@ struct AccArgs {
   int poll1;        // the controller polls a partial's tag granule before loading it whole
   int psleep;       // s_sleep between the controller's polls of a partial (0, 1, 2, 4)
   int etake;        // a polling thread takes its worker's flagged members as soon as it has the partial
+  int xfast;        // nearest-alive window also when an edge bin is empty (off: MC_ACCUM_NO_XFAST)
   int rpoll;        // dense workers: waves polling the step record (MC_ACCUM_RPOLL, 1..4)
   int rpoll_gap;    // ... wave w starts w * rpoll_gap * 512 clocks late (MC_ACCUM_RPOLL_GAP)
   uint32_t rec_g;
@@ -349,6 +350,9 @@ struct DevBvec {
     }
     return NONE64;
   }
+  // first alive position of bin b (b < 0: none) -- with first_nonempty / last_nonempty, the
+  // position bvec::inner_index_of's empty-bin branch makes the window's front / back
+  __device__ uint64_t first_alive_of(int64_t b) const { return b < 0 ? NONE64 : next_alive(lo[b], lo[b + 1]); }
   __device__ uint64_t prev_alive(uint64_t p, uint64_t q) const {
     if (p >= q) return NONE64;
     const int lane = threadIdx.x & 63;
@@ -1894,6 +1898,7 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
   uint64_t t_ws[4] = {0, 0, 0, 0};   // window: centre window data, window, record; [3] collect's takes
   uint64_t t_cl[3] = {0, 0, 0};      // closest: members scored (wave 0), reduced + barrier, winner + barrier
   uint64_t t_pub[2] = {0, 0};        // window (spec): the record's span, the record's stores issued
+  uint64_t t_wk[5] = {0, 0, 0, 0, 0};  // window: bvec kills, fast form, general form (time); fast, general (count)
 
   auto finish_cluster = [&]() {
     if (threadIdx.x == 0) {
@@ -2155,6 +2160,8 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
         }
         if (A.trace2 && threadIdx.x == 0 && step < TRACE_STEPS) A.trace[(uint64_t)step * TRACE_W + 6] = now();
       }
+      uint64_t tk0 = 0;
+      if (A.prof && threadIdx.x == 0) tk0 = now();
       if (npend) {  // the last step's bvec kills, after the record is out
         if (!(A.dbg & 1)) {
           for (uint32_t i = threadIdx.x; i < npend; i += NT) bv.kill_in(s_plist[i], s_pbin[i]);
@@ -2166,6 +2173,11 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
         }
         npend = 0;
         __syncthreads();
+      }
+      if (A.prof && threadIdx.x == 0) {
+        const uint64_t t = now();
+        t_wk[0] += t - tk0;
+        tk0 = t;
       }
       if (A.spec && rec_exact) {  // the span of the record is the window (alive after the kills)
         S = lo[wt.fb];
@@ -2179,24 +2191,34 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
         have = true;
         break;
       }
-      const bool fast = wt.fb < A.nb && wt.bb < A.nb && cnt[wt.fb] > 0 && cnt[wt.bb] > 0;
+      const bool ef = wt.fb < A.nb && cnt[wt.fb] > 0, eb = wt.bb < A.nb && cnt[wt.bb] > 0;
+      bool fast = wt.fb < A.nb && wt.bb < A.nb && ((ef && eb) || A.xfast);
       int64_t count = 0;
       if (fast) {
-        // nearest-alive form (bv_fast_window): four one-wave queries side by side
+        // nearest-alive form (bv_fast_window): four one-wave queries side by side.  An empty
+        // edge bin sends bvec::inner_index_of to the first / last non-empty bin, offset 0
+        // (bvec.cpp:55-104): front is then the first alive position overall, back the first
+        // alive position of the last non-empty bin (tests/native/bvec_check.cpp).
         if (wv < 4) {
           const uint64_t pf = lo[wt.fb] + wt.kf, qb = lo[wt.bb] + wt.kble;
           uint64_t r;
-          if (wv == 0) r = bv.next_alive(pf, lo[wt.fb + 1]);
-          else if (wv == 1) r = bv.prev_alive(lo[wt.fb], pf);
-          else if (wv == 2) r = bv.next_alive(qb, lo[wt.bb + 1]);
-          else r = bv.prev_alive(lo[wt.bb], qb);
+          if (wv == 0) r = ef ? bv.next_alive(pf, lo[wt.fb + 1]) : bv.first_alive_of(bv.first_nonempty());
+          else if (wv == 1) r = ef ? bv.prev_alive(lo[wt.fb], pf) : NONE64;
+          else if (wv == 2) r = eb ? bv.next_alive(qb, lo[wt.bb + 1]) : bv.first_alive_of(bv.last_nonempty());
+          else r = eb ? bv.prev_alive(lo[wt.bb], qb) : NONE64;
           if (lane == 0) s_q[wv] = r;
         }
         __syncthreads();
-        bv_fast_window(s_q[0], s_q[1], s_q[2], s_q[3], lo[wt.bb] + wt.kblt, &S, &E);
-        count = (S != NONE64 && E != NONE64 && E >= S) ? 1 : 0;
+        const uint64_t q0 = s_q[0], q1 = s_q[1], q2 = s_q[2], q3 = s_q[3];
         __syncthreads();  // s_q is reused
-      } else {
+        // (no alive element at all: the general form, which reports the reference's errors)
+        fast = (ef || q0 != NONE64) && (eb || q2 != NONE64);
+        if (fast) {
+          bv_fast_window(q0, q1, q2, q3, lo[wt.bb] + wt.kblt, &S, &E);
+          count = (S != NONE64 && E != NONE64 && E >= S) ? 1 : 0;
+        }
+      }
+      if (!fast) {
         bv.h = wt;
         BPos f, b;
         bv_get_range(bv, wt.bl, wt.el, f, b);
@@ -2212,6 +2234,8 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
         const uint64_t t = now();
         t_ws[1] += t - t_mark;
         t_mark = t;
+        t_wk[fast ? 1 : 2] += t - tk0;
+        t_wk[fast ? 3 : 4]++;
       }
       if (count > 0) {
         have = true;
@@ -2833,6 +2857,7 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
     for (int i = 0; i < 4; i++) A.out[12 + i] = t_ws[i];
     for (int i = 0; i < 3; i++) A.out[18 + i] = t_cl[i];
     for (int i = 0; i < 2; i++) A.out[21 + i] = t_pub[i];
+    for (int i = 0; i < 5; i++) A.out[23 + i] = t_wk[i];
     if (A.prof) {
       A.out[16] = __builtin_amdgcn_s_memtime() - clk0;
       A.out[17] = now() - rt0;
@@ -3092,6 +3117,7 @@ int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, 
   A.spec = (pl.dense || pl.dstream) && !getenv("MC_ACCUM_NO_SPEC") ? 1 : 0;
   A.poll1 = getenv("MC_ACCUM_POLL1") ? 1 : 0;
   A.etake = getenv("MC_ACCUM_EARLY_TAKE") && atoi(getenv("MC_ACCUM_EARLY_TAKE")) ? 1 : 0;
+  A.xfast = getenv("MC_ACCUM_NO_XFAST") ? 0 : 1;
   {
     const char *e = getenv("MC_ACCUM_RPOLL"), *g = getenv("MC_ACCUM_RPOLL_GAP");
     const int v = e ? atoi(e) : 1, gv = g ? atoi(g) : 2;

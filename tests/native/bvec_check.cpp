@@ -139,7 +139,7 @@ struct FastAcc {
 
 int main() {
   std::mt19937_64 rng(777);
-  long checks = 0, fast_checks = 0;
+  long checks = 0, fast_checks = 0, empty_edge_checks = 0;
   for (int t = 0; t < 300; t++) {
     const size_t n = t < 20 ? (size_t)t + 1 : (size_t)(rng() % 6000) + 1;
     std::vector<uint64_t> len(n);
@@ -201,14 +201,25 @@ int main() {
           printf("FAST MISMATCH t=%d it=%d\n", t, it);
           return 1;
         }
-        // the device controller's nearest-alive form (both edge bins non-empty)
+        // the device controller's nearest-alive form (edge bins non-empty, or empty: then front is
+        // the first alive position overall and back the first alive position of the last
+        // non-empty bin, as bvec::inner_index_of's empty-bin branch makes them)
         {
           uint64_t lo_, hi_;
           mcg::bv_index_of_sorted(bv.begin_bounds(), fa.nbins(), bl, &lo_, &hi_);
           const uint64_t fb = lo_;
           mcg::bv_index_of_sorted(bv.begin_bounds(), fa.nbins(), el, &lo_, &hi_);
           const uint64_t bb = hi_;
-          if (fa.cnt(fb) > 0 && fa.cnt(bb) > 0) {
+          const bool ef = fa.cnt(fb) > 0, eb = fa.cnt(bb) > 0;
+          auto bin_first_alive = [&](bool last) -> uint64_t {  // first alive of the first / last non-empty bin
+            const int64_t i = last ? fa.last_nonempty() : fa.first_nonempty();
+            if (i < 0) return ~0ull;
+            for (uint64_t p = blo[i]; p < blo[i + 1]; p++)
+              if (fa.alive[p]) return p;
+            return ~0ull;
+          };
+          const uint64_t ovf = ef ? 0 : bin_first_alive(false), ovb = eb ? 0 : bin_first_alive(true);
+          if ((ef || ovf != ~0ull) && (eb || ovb != ~0ull)) {
             const auto &sl = bv.static_lengths();
             const uint64_t pf0 = std::lower_bound(sl.begin() + blo[fb], sl.begin() + blo[fb + 1], bl) - sl.begin();
             const uint64_t plt = std::lower_bound(sl.begin() + blo[bb], sl.begin() + blo[bb + 1], el) - sl.begin();
@@ -224,8 +235,9 @@ int main() {
               return ~0ull;
             };
             uint64_t S4 = 0, E4 = 0;
-            mcg::bv_fast_window(next_alive(pf0, blo[fb + 1]), prev_alive(blo[fb], pf0), next_alive(ple, blo[bb + 1]),
-                                prev_alive(blo[bb], ple), plt, &S4, &E4);
+            mcg::bv_fast_window(ef ? next_alive(pf0, blo[fb + 1]) : ovf, ef ? prev_alive(blo[fb], pf0) : ~0ull,
+                                eb ? next_alive(ple, blo[bb + 1]) : ovb, eb ? prev_alive(blo[bb], ple) : ~0ull, plt, &S4,
+                                &E4);
             const bool has = E4 != ~0ull && S4 != ~0ull && E4 >= S4;
             if (derr || has != (c2 > 0) || (has && (S4 != S2 || E4 != E2))) {
               printf("NEAREST-ALIVE MISMATCH t=%d it=%d: core err %d count %lld S %llu E %llu / fast S %llu E %llu\n", t,
@@ -234,6 +246,7 @@ int main() {
               return 1;
             }
             fast_checks++;
+            if (!ef || !eb) empty_edge_checks++;
           }
         }
         checks++;
@@ -272,6 +285,6 @@ int main() {
       }
     }
   }
-  printf("OK %ld checks (%ld nearest-alive)\n", checks, fast_checks);
+  printf("OK %ld checks (%ld nearest-alive, %ld with an empty edge bin)\n", checks, fast_checks, empty_edge_checks);
   return 0;
 }
