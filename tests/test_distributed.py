@@ -283,6 +283,12 @@ def _cli(binary, name, tmp_path, devices, env_extra=None, timeout=600):
     fa, flags = fixtures.e2e_input(name, tmp_path)
     out = str(tmp_path / (name + ".clstr"))
     st = out + ".json"
+    ids = devices.split(",")
+    if len(set(ids)) < len(ids):
+        # ranks sharing a GPU in one process: each rank's persistent accumulation kernel needs a
+        # hardware queue of its own (with HIP's default of 4 per process, a rank's launch can
+        # land behind the other rank's spinning kernel until the mailbox deadline)
+        env_extra = {"GPU_MAX_HW_QUEUES": "8", **(env_extra or {})}
     r = subprocess.run([binary, fa] + flags + ["--devices", devices, "--output", out, "--stats-json", st, "--quiet",
                         "--threads", "4"], capture_output=True, text=True, timeout=timeout,
                        env={**os.environ, "MC_SHARD_ACCUM": "1", **(env_extra or {})})
