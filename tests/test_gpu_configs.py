@@ -52,10 +52,12 @@ def product():
     return M.BIN
 
 
-@pytest.mark.parametrize("env", [{}, {"MC_ACCUM_NARROW": "1"}, {"MC_ACCUM_STEPS": "1"}])
+@pytest.mark.parametrize("env", [{}, {"MC_ACCUM_NARROW": "1"}, {"MC_ACCUM_STEPS": "1"}, {"MC_ACCUM_NO_XFAST": "1"}])
 def test_config_E91_partition_equals_reference(product, tmp_path, env):
     """k = 6 (4 KiB rows): the accumulation kernel's wide form (default), its lane-per-candidate
-    form and the host-driven get_close steps, each against the reference's partition."""
+    form, the host-driven get_close steps and the controller's general window form (no
+    nearest-alive queries for windows with an empty edge bin, MC_ACCUM_NO_XFAST), each against
+    the reference's partition."""
     fa = str(tmp_path / "E91.fa")
     synth.write_fasta(fa, synth.families(7, 13, 8000, 12000, 0.05, 0.15, 61))
     out = str(tmp_path / "E91.clstr")
@@ -209,7 +211,7 @@ def test_config_E9100_properties(product):
     gives 8 GPUs work).  No reference partition exists at this size (the reference needs hours):
     the partition must be a partition with member centres, and identical across the accumulation
     kernel's wide form, its lane-per-candidate form (MC_ACCUM_NARROW), the host-driven get_close
-    steps, and the NW kernels' forms (every batch in the throughput form / in the 8-wave latency
+    steps, the controller's general window form (MC_ACCUM_NO_XFAST), and the NW kernels' forms (every batch in the throughput form / in the 8-wave latency
     form).  E91 pins these forms against the reference (test_config_E91_partition_equals_reference)."""
     fa = _families_input("E9100", 70, 130, 8000, 12000, 0.05, 0.15, 61)
     base = fa[:-3] + ".clstr"
@@ -217,6 +219,7 @@ def test_config_E9100_properties(product):
     assert st["k"] == 6 and st["n"] == 9100 and st["accum_path"] == "device"
     want = BG.canonical_digest(_properties(base, 9100))
     for tag, env in (("narrow", {"MC_ACCUM_NARROW": "1"}), ("steps", {"MC_ACCUM_STEPS": "1"}),
+                     ("noxfast", {"MC_ACCUM_NO_XFAST": "1"}),
                      ("nwtp", {"MC_NW_MW_MAX": "0"}), ("nw8", {"MC_NW_MW_MAX": "100000000", "MC_NW_WAVES": "8"})):
         out = fa[:-3] + "." + tag + ".clstr"
         _run(fa, ["--id", "0.80"], out, 600, env)
