@@ -207,6 +207,13 @@ int build_static(mc_ctx *c);
 bool accum_supported(const mc_ctx *c, uint32_t nb);
 bool accum_plan_info(const mc_ctx *c, uint32_t nb, uint32_t info[4]);
 uint64_t mailbox_slot_granules(uint32_t world, uint64_t n);  // mailbox granules per rank slot
+// accum_kernel instantiations (accum_impl.hpp), one translation unit per worker form; width 1 / 2
+// bytes per bin, nch 16 selects the compile-time 16-chunk rows (8-bit k = 4), prof the twin with
+// the MC_ACCUM_PROFILE timers (the chunk forms have none: their profile runs carry no timers)
+const void *accum_fn_dense(int width, int nch, bool prof);
+const void *accum_fn_dstream(int width, int nch, bool prof);
+const void *accum_fn_wide(int width, bool prof);
+const void *accum_fn_chunk(int width, int nch, bool compact);
 int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, uint32_t nb, double sim,
                  uint32_t *d_mem_pos, uint64_t *d_mkeys, uint32_t *d_cl_centre, uint64_t *d_cl_off, uint64_t *d_out);
 // nparts > 0: a sharded step (mc_scan_part) over this rank's static blocks only
