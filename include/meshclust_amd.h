@@ -283,6 +283,23 @@ int mc_ctx_pci_bus_id(mc_ctx *ctx, char *buf, int len);
  */
 int mc_accum_plan_info(mc_ctx *ctx, uint32_t nbins, uint32_t info[4]);
 int mc_set_accum_grid(mc_ctx *ctx, uint32_t grid);
+/*
+ * Allocate now every device buffer mc_accumulate needs for this bvec (call after
+ * mc_set_accum_grid): mc_accumulate then allocates and frees nothing.  Ranks that share one
+ * GPU in one process call it before a common barrier, so that no rank's hipFree -- which waits
+ * for the whole device -- runs while a peer's persistent kernel spins on this rank's step
+ * records (the Trainer.cpp:81-106 loop split by record).
+ */
+int mc_accum_reserve(mc_ctx *ctx, uint32_t nbins);
+/*
+ * Confine the context to slot `slot` of `share` disjoint CU sets of its GPU (ranks sharing one
+ * GPU: the one-GPU rehearsal of the record-sharded loops, ClusterFactory.cpp:744-749 and
+ * Trainer.cpp:81-106).  The context's stream is re-created with a CU mask (a hardware queue of
+ * its own), so every kernel of the rank -- the persistent accumulation grid included, sized to
+ * the mask -- runs on those CUs only and never waits behind a peer rank's spinning kernel.
+ * share 1 restores the whole GPU.  Call while the context is idle.
+ */
+int mc_ctx_partition(mc_ctx *ctx, int slot, int share);
 
 /*
  * One mean-shift iteration over all centres (the omp parallel for of ClusterFactory.cpp:

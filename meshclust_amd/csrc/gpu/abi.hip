@@ -1030,6 +1030,51 @@ int mc_set_accum_grid(mc_ctx *c, uint32_t grid) {
   return MC_OK;
 }
 
+int mc_accum_reserve(mc_ctx *c, uint32_t nbins) {
+  if (!c || nbins == 0) return MC_ERR_ARG;
+  if (!c->has_cls || c->norder == 0) return MC_ERR_STATE;
+  if (!fused(c)) {
+    set_error("device-resident accumulation does not take this configuration");
+    return MC_ERR_UNSUPPORTED;
+  }
+  MCG_CHECK(hipSetDevice(c->device));
+  return accum_reserve(c, nbins);
+}
+
+int mc_ctx_partition(mc_ctx *c, int slot, int share) {
+  if (!c || share < 1 || share > 32 || slot < 0 || slot >= share) return MC_ERR_ARG;
+  MCG_CHECK(hipSetDevice(c->device));
+  MCG_CHECK(hipStreamSynchronize(c->stream));
+  int cus = 0;
+  MCG_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
+  hipStream_t s = nullptr;
+  int n = 0;
+  if (share == 1) {
+    MCG_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  } else {
+    // CU i joins slot (i / 8) % share: groups of eight consecutive mask bits alternate between
+    // the slots, so each slot holds the same number of CUs of every XCD whether the mask's bits
+    // are dealt to the XCDs round-robin or in contiguous runs
+    std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0u);
+    for (int i = 0; i < cus; i++)
+      if ((i / 8) % share == slot) {
+        mask[(size_t)i / 32] |= 1u << (i % 32);
+        n++;
+      }
+    if (n < 16) {
+      set_error("mc_ctx_partition: fewer than 16 CUs per slot");
+      return MC_ERR_ARG;
+    }
+    MCG_CHECK(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()));
+  }
+  (void)hipStreamDestroy(c->stream);
+  c->stream = s;
+  c->part_slot = slot;
+  c->part_share = share;
+  c->part_cus = share == 1 ? 0 : n;
+  return MC_OK;
+}
+
 int mc_accumulate(mc_ctx *c, const uint32_t *bin_lo, const uint64_t *bounds, uint32_t nbins, double sim,
                   uint32_t *centre_ids, uint64_t *member_off, uint32_t *member_ids, uint64_t *nclusters,
                   uint64_t *stats) {
@@ -1133,8 +1178,9 @@ int mc_accumulate(mc_ctx *c, const uint32_t *bin_lo, const uint64_t *bounds, uin
       // controller's all-partials time
       const int TW = 20, S2 = 256, G2 = 256, T2 = 6;  // accum.hip TRACE_W, TRACE2_STEPS, GMAX, T2W
       std::vector<uint64_t> tr(4096 * TW), t2((size_t)S2 * G2 * T2);
-      MCG_CHECK(hipMemcpy(tr.data(), c->s_h.p, tr.size() * 8, hipMemcpyDeviceToHost));
-      MCG_CHECK(hipMemcpy(t2.data(), (char *)c->s_h.p + tr.size() * 8, t2.size() * 8, hipMemcpyDeviceToHost));
+      MCG_CHECK(hipMemcpyAsync(tr.data(), c->s_h.p, tr.size() * 8, hipMemcpyDeviceToHost, c->stream));
+      MCG_CHECK(hipMemcpyAsync(t2.data(), (char *)c->s_h.p + tr.size() * 8, t2.size() * 8, hipMemcpyDeviceToHost, c->stream));
+      MCG_CHECK(hipStreamSynchronize(c->stream));
       // columns: seen, scores (wave 0), part B (wave 0), after the B barrier, after the reduce
       // barrier, partial stored
       const int col[6] = {0, 1, 3, 4, 5, 2};
@@ -1175,7 +1221,8 @@ int mc_accumulate(mc_ctx *c, const uint32_t *bin_lo, const uint64_t *bounds, uin
       // has every partial -> collect done
       const int TW = 20;  // accum.hip TRACE_W
       std::vector<uint64_t> tr(4096 * TW);
-      MCG_CHECK(hipMemcpy(tr.data(), c->s_h.p, tr.size() * 8, hipMemcpyDeviceToHost));
+      MCG_CHECK(hipMemcpyAsync(tr.data(), c->s_h.p, tr.size() * 8, hipMemcpyDeviceToHost, c->stream));
+      MCG_CHECK(hipStreamSynchronize(c->stream));
       double a[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, m[7] = {0, 0, 0, 0, 0, 0, 0};
       uint64_t cnt = 0, nact = 0, mcnt = 0, scnt = 0, bcnt = 0;
       double mb[3] = {0, 0, 0};

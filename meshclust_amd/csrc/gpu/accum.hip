@@ -92,7 +92,11 @@ uint32_t accum_grid(const mc_ctx *c) {
   // kernels are launched plainly at different times, and a workgroup the dispatcher places on
   // a busier XCD must still find a free CU there (round-robin XCD placement is observed, not
   // promised: two exactly-fitting grids once left one workgroup waiting for the other kernel)
-  if (c->mb_world > 0 && c->mb_share > 1) cus = cus / c->mb_share - 8;
+  // (mc_ctx_partition: the context's CU mask, less one CU per XCD of slack -- the dispatcher's
+  // placement of workgroups over the XCDs is observed, not promised, and every workgroup of the
+  // persistent grid must find a free CU of the mask)
+  if (c->part_cus > 0) cus = std::min(cus, c->part_cus - 8);
+  else if (c->mb_world > 0 && c->mb_share > 1) cus = cus / c->mb_share - 8;
   // mc_set_accum_grid: ranks sharing a mailbox run the smallest grid among them, so that every
   // rank derives the same tile of ownership from it (accum_plan's dense test depends on G)
   if (c->acc_grid > 0) cus = std::min<int>(cus, (int)c->acc_grid);
@@ -187,6 +191,37 @@ bool accum_plan(const mc_ctx *c, uint32_t nb, AccPlan *pl) {
   return false;
 }
 
+// s_a: go word + step ring; s_b: partials (+ global bitmap); s_c: flagged positions + kill
+// log; s_i: member info (MInfo per static position); s_j: row-major static rows; s_k: the
+// compacted / dense streaming row copies; s_d..s_g, acc_out: mc_accumulate's own inputs and
+// outputs (abi.hip)
+struct AccBytes {
+  size_t ring, part, bits, fpos, klog;
+};
+int accum_alloc(mc_ctx *c, const AccPlan &pl, uint32_t nb, AccBytes *ab) {
+  const uint32_t GW = pl.G - 1;
+  const int nch = (int)((c->B * c->width + 15) / 16);
+  ab->ring = 256 + (size_t)RING * pl.rec_g * 8 + (size_t)RING * 16;
+  ab->part = ((size_t)GW * PART_G * 8 + 255) / 256 * 256;
+  ab->bits = pl.gbits ? ((c->norder + 31) / 32 * 4 + 255) / 256 * 256 : 0;
+  ab->fpos = ((size_t)GW * pl.fcap * 4 + 255) / 256 * 256;
+  ab->klog = (c->norder * 8 + 16 + 255) / 256 * 256;
+  if (ensure(c->s_a, ab->ring) || ensure(c->s_b, ab->part + ab->bits) || ensure(c->s_c, ab->fpos + ab->klog))
+    return MC_ERR_OOM;
+  if (ensure(c->s_i, c->norder * sizeof(MInfo) + 64) || ensure(c->s_j, c->norder * (size_t)nch * 16 + 64))
+    return MC_ERR_OOM;
+  // compacted row copies: one region of NT rows per local chunk (this rank's chunks); or the
+  // dense streaming workers' two row buffers each
+  const size_t cc_bytes = pl.compact    ? (size_t)(pl.fcap / NT) * GW * NT * (size_t)nch * 16
+                          : pl.dstream ? (size_t)2 * GW * pl.fcap * (size_t)(nch + 1) * 16
+                                       : 0;
+  if (cc_bytes && ensure(c->s_k, cc_bytes)) return MC_ERR_OOM;
+  if (ensure(c->s_d, ((size_t)nb + 1) * 4 + 16) || ensure(c->s_e, (size_t)nb * 8 + 16) ||
+      ensure(c->s_f, c->norder * 4 + 16) || ensure(c->s_g, (c->norder + 1) * 8 + 16) || ensure(c->acc_out, 256))
+    return MC_ERR_OOM;
+  return MC_OK;
+}
+
 }  // namespace
 
 uint64_t mailbox_slot_granules(uint32_t world, uint64_t n) {
@@ -207,6 +242,16 @@ bool accum_plan_info(const mc_ctx *c, uint32_t nb, uint32_t info[4]) {
             (!pl.dense && !pl.wide && pl.res == 0 ? 8u : 0u) | (pl.dstream ? 16u : 0u);
   info[3] = (uint32_t)pl.lds;
   return true;
+}
+
+int accum_reserve(mc_ctx *c, uint32_t nb) {
+  AccPlan pl;
+  if (!accum_plan(c, nb, &pl)) {
+    set_error("device-resident accumulation does not take this configuration");
+    return MC_ERR_UNSUPPORTED;
+  }
+  AccBytes ab;
+  return accum_alloc(c, pl, nb, &ab);
 }
 
 int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, uint32_t nb, double sim,
@@ -235,24 +280,9 @@ int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, 
     return MC_ERR_HIP;
   }
   const uint64_t fcap = pl.fcap;
-  // s_a: go word + step ring; s_b: partials (+ global bitmap); s_c: flagged positions + kill
-  // log; s_h: trace; s_i: member info (MInfo per static position); s_j: row-major static rows
-  const size_t ring_bytes = 256 + (size_t)RING * pl.rec_g * 8 + (size_t)RING * 16;
-  const size_t part_bytes = ((size_t)GW * PART_G * 8 + 255) / 256 * 256;
-  const size_t bits_bytes = pl.gbits ? ((c->norder + 31) / 32 * 4 + 255) / 256 * 256 : 0;
-  const size_t fpos_bytes = ((size_t)GW * fcap * 4 + 255) / 256 * 256;
-  const size_t klog_bytes = (c->norder * 8 + 16 + 255) / 256 * 256;
-  if (ensure(c->s_a, ring_bytes) || ensure(c->s_b, part_bytes + bits_bytes) ||
-      ensure(c->s_c, fpos_bytes + klog_bytes))
-    return MC_ERR_OOM;
-  if (ensure(c->s_i, c->norder * sizeof(MInfo) + 64) || ensure(c->s_j, c->norder * (size_t)nch * 16 + 64))
-    return MC_ERR_OOM;
-  // compacted row copies: one region of NT rows per local chunk (this rank's chunks); or the
-  // dense streaming workers' two row buffers each
-  const size_t cc_bytes = pl.compact    ? (size_t)(pl.fcap / NT) * GW * NT * (size_t)nch * 16
-                          : pl.dstream ? (size_t)2 * GW * pl.fcap * (size_t)(nch + 1) * 16
-                                       : 0;
-  if (cc_bytes && ensure(c->s_k, cc_bytes)) return MC_ERR_OOM;
+  AccBytes ab;
+  if (int rc = accum_alloc(c, pl, nb, &ab)) return rc;
+  const size_t ring_bytes = ab.ring, part_bytes = ab.part, fpos_bytes = ab.fpos;
   MInfo *d_minfo = (MInfo *)c->s_i.p;
   uint4 *d_hr = (uint4 *)c->s_j.p;
   uint32_t *d_bits = pl.gbits ? (uint32_t *)((char *)c->s_b.p + part_bytes) : nullptr;
@@ -342,7 +372,9 @@ int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, 
   // they are all resident.  Several ranks' kernels (mailbox) may share a GPU in tests, where a
   // second cooperative launch would wait for the first; they take a plain launch (every
   // hand-off has its 20 s deadline either way).
-  if (A.mbox || getenv("MC_ACCUM_PLAIN_LAUNCH"))
+  // A context confined to a CU mask (mc_ctx_partition) launches plainly too: the cooperative
+  // check counts the whole GPU, and the grid was sized to the mask.
+  if (A.mbox || c->part_cus > 0 || getenv("MC_ACCUM_PLAIN_LAUNCH"))
     MCG_CHECK(hipLaunchKernel(pl.fn, dim3(G), dim3(NT), args, (unsigned)pl.lds, c->stream));
   else
     MCG_CHECK(hipLaunchCooperativeKernel(pl.fn, dim3(G), dim3(NT), args, (unsigned)pl.lds, c->stream));

@@ -974,6 +974,7 @@ __device__ __forceinline__ void worker_dense(const AccArgs &A, const DevClassifi
   __shared__ uint64_t s_t0[3];   // ... thread 0's record-seen, scores-done and part-B times
   __shared__ uint32_t s_arr;     // waves that have reduced this step's scores
   __shared__ uint32_t s_rgot;    // the step whose record a polling wave has written to srec
+  __shared__ SmallK s_sk;        // classify_small's constants (read with each candidate's row)
   constexpr int NC = NCH > 0 ? NCH : DMAXCH;
   constexpr int RPW = (4 * NC + REC_HDR + 63) / 64;  // record words per polling lane
   const uint32_t GW = gridDim.x - 1, w = blockIdx.x - 1;
@@ -1015,6 +1016,7 @@ __device__ __forceinline__ void worker_dense(const AccArgs &A, const DevClassifi
     s_b[0] = s_b[1] = 0;
     s_arr = 0;
     s_rgot = 0;
+    s_sk = make_smallk(C, A.fc);
   }
   __syncthreads();
   uint32_t kcur = 0, seen = 0;
@@ -1156,6 +1158,7 @@ __device__ __forceinline__ void worker_dense(const AccArgs &A, const DevClassifi
       Acc<T> acc;
       const uint4 *rr = lrow + t;
       constexpr int HB = NC >= 8 ? 8 : NC;
+      const SmallK sk = lds_smallk(&s_sk);
       if constexpr (NCH > 0) {
 #pragma unroll
         for (int k0 = 0; k0 < NC; k0 += HB) {
@@ -1175,7 +1178,7 @@ __device__ __forceinline__ void worker_dense(const AccArgs &A, const DevClassifi
       if constexpr (sizeof(T) == 1) {
         if (small_on && ps_q.ok && ps_t.ok) {
           acc.fold();
-          d_t = classify_small(C, A.fc, acc.sad, acc.dot, ps_t, ps_q, kq, pt_t.da, tq.da, A.B, &cv_t, &und);
+          d_t = classify_small(sk, acc.sad, acc.dot, ps_t, ps_q, kq, pt_t.da, tq.da, A.B, &cv_t, &und);
           if (und) {
             double cx;
             d_t = classify_std(C, acc.finish(pi_t.mag, pc.mag), pi_t, pt_t, pc, tq, A.B, &cx);

@@ -477,22 +477,49 @@ __device__ __forceinline__ PSm psmall(const PInfo &p, const PTerms &t) {
   const bool ok = p.mag < (1ull << 24) && p.len < (1ull << 31) && t.ap >= 0 && t.np >= 0 && t.np < (1ll << 26);
   return PSm{(uint32_t)p.mag, (uint32_t)p.len, (uint32_t)t.ap, (uint32_t)t.np, ok};
 }
+// classify_small's constants in one 208-byte block.  The accumulation workers keep a copy in LDS
+// and read it with the candidate's row (one LDS wait), instead of re-loading the kernel
+// arguments: the persistent kernel's loop holds too many uniform values for them all to stay in
+// scalar registers, and each reload was a scalar-memory round trip on the scoring chain.
+struct SmallK {
+  double mins[5], range[2], rinv[5], noff[3], nsgn[3], w[5], thr;  // noff / nsgn: features 2..4
+  int32_t sim0, sim1, kul, pad;
+};
+static_assert(sizeof(SmallK) % 16 == 0, "SmallK is copied as 16-byte words");
+__host__ __device__ __forceinline__ SmallK make_smallk(const DevClassifier &C, const FastCls &F) {
+  SmallK k;
+  for (int i = 0; i < 5; i++) {
+    k.mins[i] = C.c.mins[i];
+    k.rinv[i] = F.rinv[i];
+    k.w[i] = C.c.weights[i];
+  }
+  for (int i = 0; i < 2; i++) k.range[i] = F.range[i];
+  for (int i = 0; i < 3; i++) {
+    k.noff[i] = F.noff[2 + i];
+    k.nsgn[i] = F.nsgn[2 + i];
+  }
+  k.thr = C.thr;
+  k.sim0 = C.c.is_sim[0];
+  k.sim1 = C.c.is_sim[1];
+  k.kul = C.layout == 4;
+  k.pad = 0;
+  return k;
+}
+
 // classify_fast from the 8-bit sums (sad = sum |p - q|, dot = sum p q) and the PSm terms of
 // both histograms (kq = mag_q - B aq): LD, INTERSECTION and combo 0 exact (the LD / INT
 // normalisations as mk_div by the host's RN(1 / range)), MANHATTAN exact, PEARSON's integers
 // exact in doubles (every one below 2^53), the decision by classify_fast's margin.  *undecided:
 // the caller decides by classify_std.  Every value it returns or stores is classify_std's.
-__device__ __forceinline__ int classify_small(const DevClassifier &C, const FastCls &F, uint32_t sad, uint32_t dot,
-                                              const PSm &p, const PSm &q, double kq, double dap, double daq, int B,
-                                              double *c0, bool *undecided) {
-  const mc_classifier &c = C.c;
-  const bool kul = C.layout == 4;
+__device__ __forceinline__ int classify_small(const SmallK &K, uint32_t sad, uint32_t dot, const PSm &p, const PSm &q,
+                                              double kq, double dap, double daq, int B, double *c0, bool *undecided) {
+  const bool kul = K.kul != 0;
   const uint32_t dl = p.len > q.len ? p.len - q.len : q.len - p.len;
   const uint32_t ms = p.mag + q.mag, s2 = ms - sad;  // s2 = 2 Smin
-  double v0 = mk_div((double)dl - c.mins[0], F.range[0], F.rinv[0]);
-  double v1 = mk_div((double)s2 / (double)ms - c.mins[1], F.range[1], F.rinv[1]);
-  v0 = c.is_sim[0] ? v0 : 1 - v0;
-  v1 = c.is_sim[1] ? v1 : 1 - v1;
+  double v0 = mk_div((double)dl - K.mins[0], K.range[0], K.rinv[0]);
+  double v1 = mk_div((double)s2 / (double)ms - K.mins[1], K.range[1], K.rinv[1]);
+  v0 = K.sim0 ? v0 : 1 - v0;
+  v1 = K.sim1 ? v1 : 1 - v1;
   const double a0 = v0 * v1;
   *c0 = a0;
   double r[5], e[5], v[5];
@@ -511,34 +538,51 @@ __device__ __forceinline__ int classify_small(const DevClassifier &C, const Fast
       v[i] = e[i] = 0.0;
       continue;
     }
-    const double n = (r[i] - c.mins[i]) * F.rinv[i];
-    v[i] = F.noff[i] + F.nsgn[i] * n;
-    e[i] = 0x1p-40 * ((__builtin_fabs(r[i]) + __builtin_fabs(c.mins[i])) * __builtin_fabs(F.rinv[i]) +
+    const double n = (r[i] - K.mins[i]) * K.rinv[i];
+    v[i] = K.noff[i - 2] + K.nsgn[i - 2] * n;
+    e[i] = 0x1p-40 * ((__builtin_fabs(r[i]) + __builtin_fabs(K.mins[i])) * __builtin_fabs(K.rinv[i]) +
                       __builtin_fabs(v[i]) + 1.0);
   }
   const double q00 = v0 * v0;
   const double a1 = q00 * (v[2] * v[2]);
   const double a2 = v[3];
   const double a3 = q00 * (v[4] * v[4]);
-  double sum = c.weights[0];
-  sum = __builtin_fma(c.weights[1], a0, sum);
-  sum = __builtin_fma(c.weights[2], a1, sum);
-  sum = __builtin_fma(c.weights[3], a2, sum);
-  if (kul) sum = __builtin_fma(c.weights[4], a3, sum);
+  double sum = K.w[0];
+  sum = __builtin_fma(K.w[1], a0, sum);
+  sum = __builtin_fma(K.w[2], a1, sum);
+  sum = __builtin_fma(K.w[3], a2, sum);
+  if (kul) sum = __builtin_fma(K.w[4], a3, sum);
   const double d1 = q00 * (2.0 * __builtin_fabs(v[2]) + e[2]) * e[2] + 0x1p-40 * __builtin_fabs(a1);
   const double d3 = q00 * (2.0 * __builtin_fabs(v[4]) + e[4]) * e[4] + 0x1p-40 * __builtin_fabs(a3);
-  const double mag = __builtin_fabs(c.weights[0]) + __builtin_fabs(c.weights[1] * a0) + __builtin_fabs(c.weights[2] * a1) +
-                     __builtin_fabs(c.weights[3] * a2) + (kul ? __builtin_fabs(c.weights[4] * a3) : 0.0);
-  const double margin = 2.0 * (__builtin_fabs(c.weights[2]) * d1 + __builtin_fabs(c.weights[3]) * e[3] +
-                               (kul ? __builtin_fabs(c.weights[4]) * d3 : 0.0)) +
+  const double mag = __builtin_fabs(K.w[0]) + __builtin_fabs(K.w[1] * a0) + __builtin_fabs(K.w[2] * a1) +
+                     __builtin_fabs(K.w[3] * a2) + (kul ? __builtin_fabs(K.w[4] * a3) : 0.0);
+  const double margin = 2.0 * (__builtin_fabs(K.w[2]) * d1 + __builtin_fabs(K.w[3]) * e[3] +
+                               (kul ? __builtin_fabs(K.w[4]) * d3 : 0.0)) +
                         0x1p-40 * mag;
   *undecided = false;
   if (__builtin_isfinite(sum) && __builtin_isfinite(margin) && __builtin_isfinite(a0)) {
-    if (sum - margin >= C.thr) return 1;
-    if (sum + margin < C.thr) return 0;
+    if (sum - margin >= K.thr) return 1;
+    if (sum + margin < K.thr) return 0;
   }
   *undecided = true;
   return 0;
+}
+__device__ __forceinline__ int classify_small(const DevClassifier &C, const FastCls &F, uint32_t sad, uint32_t dot,
+                                              const PSm &p, const PSm &q, double kq, double dap, double daq, int B,
+                                              double *c0, bool *undecided) {
+  return classify_small(make_smallk(C, F), sad, dot, p, q, kq, dap, daq, B, c0, undecided);
+}
+// the SmallK block from LDS: volatile 16-byte reads, so they are issued where the scoring needs
+// them (beside the row's reads) and never hoisted into registers across the worker's loop
+__device__ __forceinline__ SmallK lds_smallk(const SmallK *p) {
+  typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+  const volatile __attribute__((address_space(3))) v4u *q = (const volatile __attribute__((address_space(3))) v4u *)p;
+  v4u w[sizeof(SmallK) / 16];
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(SmallK) / 16); i++) w[i] = q[i];
+  SmallK k;
+  __builtin_memcpy(&k, w, sizeof(SmallK));
+  return k;
 }
 
 template <typename T>

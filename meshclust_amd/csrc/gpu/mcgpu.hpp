@@ -152,6 +152,9 @@ struct mc_ctx {
   uint64_t mb_bytes = 0;
   int mb_rank = 0, mb_world = 0, mb_share = 1;
   uint32_t acc_grid = 0;  // mc_set_accum_grid: cap on the accumulation kernel's workgroups (0: none)
+  // mc_ctx_partition: this context's stream runs on slot `part_slot` of `part_share` disjoint CU
+  // sets of its GPU (ranks sharing one GPU); part_cus CUs in the mask (0: the whole GPU)
+  int part_slot = 0, part_share = 1, part_cus = 0;
   // scratch
   mcg::Buf s_a, s_b, s_c, s_d, s_e, s_f, s_g, s_h, s_i, s_j, s_k;
   // mc_update_iteration's member lists on the device and their host shadow: re-uploaded only
@@ -214,6 +217,9 @@ const void *accum_fn_dense(int width, int nch, bool prof);
 const void *accum_fn_dstream(int width, int nch, bool prof);
 const void *accum_fn_wide(int width, bool prof);
 const void *accum_fn_chunk(int width, int nch, bool compact);
+// every device buffer launch_accum needs for `nb` bins, allocated now (mc_accum_reserve: ranks
+// sharing a GPU allocate before any rank launches, so no hipFree waits on a spinning peer kernel)
+int accum_reserve(mc_ctx *c, uint32_t nb);
 int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, uint32_t nb, double sim,
                  uint32_t *d_mem_pos, uint64_t *d_mkeys, uint32_t *d_cl_centre, uint64_t *d_cl_off, uint64_t *d_out);
 // nparts > 0: a sharded step (mc_scan_part) over this rank's static blocks only
