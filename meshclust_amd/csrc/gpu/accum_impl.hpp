@@ -136,6 +136,9 @@ struct AccArgs {
   int poll1;        // the controller polls a partial's tag granule before loading it whole
   int psleep;       // s_sleep between the controller's polls of a partial (0, 1, 2, 4)
   int etake;        // a polling thread takes its worker's flagged members as soon as it has the partial
+  int helpers;      // the controller's waves 4-7 during the fan-in (dense form, one rank): 1 apply the
+                    // last step's deferred bvec kills there (not beside the record's publication),
+                    // 2 also take the new members as the pollers list them (MC_ACCUM_HELPERS)
   int xfast;        // nearest-alive window also when an edge bin is empty (off: MC_ACCUM_NO_XFAST)
   int rpoll;        // dense workers: waves polling the step record (MC_ACCUM_RPOLL, 1..4)
   int rpoll_gap;    // ... wave w starts w * rpoll_gap * 512 clocks late (MC_ACCUM_RPOLL_GAP)
@@ -1807,6 +1810,7 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
   __shared__ uint32_t s_new;  // members taken into the cluster this step
   __shared__ uint32_t s_plist[PLIST];  // ... their positions
   __shared__ uint32_t s_pbin[PLIST];   // ... their bvec bins (kills deferred to the next window)
+  __shared__ uint32_t s_kdone, s_pdone;  // helper waves' kill passes / pollers done (cumulative)
   __shared__ uint64_t s_q[4];
   __shared__ uint32_t s_klast[KINL];
   __shared__ int s_abort;
@@ -1845,6 +1849,8 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
   if (threadIdx.x == 0) {
     s_abort = 0;
     s_new = 0;
+    s_kdone = 0;
+    s_pdone = 0;
   }
   uint64_t lg = 1;
   while (lg * 2 <= A.nb) lg *= 2;
@@ -1863,6 +1869,10 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
   bool rec_exact = false;  // the record being published carries the exact window (no part B)
   uint32_t npend = 0;   // new members s_plist[0, npend) whose bvec kills are still to be done
   uint64_t t_wait = 0, t_coll = 0, t_mark = 0;
+  uint32_t kdef = 0;                  // deferred kills (s_plist / s_pbin [0, kdef)) for the helper waves
+  uint32_t ncoll = 0, pdone_base = 0;  // collects so far; pollers counted in s_pdone before this one
+  // (helper waves: the dense / chunk forms on one rank; the mailbox path lists members later)
+  const bool helpers = A.helpers > 0 && !WIDE && A.mbox == nullptr;
   const uint64_t clk0 = prof_on ? __builtin_amdgcn_s_memtime() : 0, rt0 = prof_on ? now() : 0;
   uint64_t t_sub[4] = {0, 0, 0, 0};  // collect: reduce (stragglers), column sums, mean, closest
   uint64_t t_ws[4] = {0, 0, 0, 0};   // window: centre window data, window, record; [3] collect's takes
@@ -2132,6 +2142,13 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
       }
       uint64_t tk0 = 0;
       if (prof_on && threadIdx.x == 0) tk0 = now();
+      // (helper waves: with the record's span the exact window, nothing reads the bvec before
+      // the collect's barrier, so the kills go to waves 4-7 while waves 0-3 poll)
+      if (npend && helpers && A.spec && rec_exact) {
+        kdef = npend;
+        npend = 0;
+        __syncthreads();  // (the barrier the kills ended with: the last collect's LDS words are free)
+      }
       if (npend) {  // the last step's bvec kills, after the record is out
         if (!(A.dbg & 1)) {
           for (uint32_t i = threadIdx.x; i < npend; i += NT) bv.kill_in(s_plist[i], s_pbin[i]);
@@ -2247,6 +2264,41 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
     double bv_ = -1.0;
     uint64_t bp_ = NONE64;
     uint32_t cnt_w = 0, scan_w = 0;
+    const bool early = helpers && A.helpers >= 2;  // helper waves take the listed members
+    ncoll++;
+    if (helpers && threadIdx.x >= NT / 2) {
+      // ---- helper waves 4-7 (nact <= 255: no poller among them) ------------------------------
+      const uint32_t h = threadIdx.x - NT / 2;
+      for (uint32_t i = h; i < kdef; i += NT / 2) bv.kill_in(s_plist[i], s_pbin[i]);
+      if (early)
+        for (uint32_t i = h; i < PLIST; i += NT / 2) s_plist[i] = NONE;  // (an entry not listed yet)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      if (lane == 0) atomicAdd(&s_kdone, 1u);
+      if (early) {
+        // entry e (e = h, h + 256, ...) is taken as soon as its poller has written it; done when
+        // every poller has finished and every listed entry below PLIST is taken
+        const uint64_t t0 = now();
+        uint32_t e = h;
+        for (uint32_t it = 1;; it++) {
+          const uint32_t pd = __hip_atomic_load(&s_pdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          const uint32_t nl = __hip_atomic_load(&s_new, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          const uint32_t lim = nl < PLIST ? nl : PLIST;
+          while (e < lim) {
+            const uint32_t p = __hip_atomic_load(&s_plist[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (p == NONE) break;
+            take(M + e, p, false, (int64_t)e);
+            e += NT / 2;
+          }
+          if (pd - pdone_base >= nact && e >= lim) break;  // (s_new is final once every poller is done)
+          if ((it & 255) == 0 && timed_out(A, t0)) {
+            s_abort = 1;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        drain();  // (take's member-list stores, read back past the member cache)
+      }
+    }
     if (threadIdx.x < nact) {  // (nact <= G - 1 < NT)
       const uint32_t wk = Div32(GW).mod((uint32_t)c0 + threadIdx.x);
       const uint64_t *q = A.partials + (uint64_t)wk * PART_G;
@@ -2294,6 +2346,15 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
         cnt_w = (uint32_t)g8[3];
         scan_w = (uint32_t)g8[4];
         // this worker's flagged positions into the step's list: cnt_w slots reserved at once
+        // (helper waves: after their kill pass has read the last step's entries)
+        if (helpers && cnt_w) {
+          const uint64_t tk = now();
+          for (uint32_t it = 1; __hip_atomic_load(&s_kdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < 4u * ncoll; it++) {
+            if ((it & 255) == 0 && timed_out(A, tk)) break;
+            __builtin_amdgcn_s_sleep(1);
+          }
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        }
         const uint32_t slot0 = cnt_w ? atomicAdd(&s_new, cnt_w) : 0u;
         for (uint32_t j = 0; j < cnt_w; j++) {
           const uint32_t p = j < (uint32_t)INL ? (uint32_t)g8[5 + j] : ld32(A.fpos + (uint64_t)wk * A.fcap + j);
@@ -2301,14 +2362,21 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
           if (mslot) {  // (several ranks: every rank takes the union, below)
             st64x(mslot + (slot < (uint32_t)MBOX_INL ? 5 + slot : MBOX_HDR - MBOX_INL + slot), gran(step, p));
           } else if (slot < PLIST) {
-            s_plist[slot] = p;
-            if (A.etake) take(M + slot, p, false, (int64_t)slot);  // (MC_ACCUM_EARLY_TAKE)
+            if (early) __hip_atomic_store(&s_plist[slot], p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            else s_plist[slot] = p;
+            if (A.etake && !early) take(M + slot, p, false, (int64_t)slot);  // (MC_ACCUM_EARLY_TAKE)
           } else {  // a list overflow: this thread takes the member itself (past the cache)
             take(M + slot, p, true);
             drain();
           }
         }
       }
+    }
+    if (helpers) {  // (every poller wave, after its last listing)
+      const uint64_t pb = __ballot(threadIdx.x < nact);
+      if (pb && lane == 0) atomicAdd(&s_pdone, (uint32_t)__popcll(pb));
+      pdone_base += nact;
+      kdef = 0;
     }
     if (prof_on && threadIdx.x == 0) {
       const uint64_t t = now();
@@ -2472,7 +2540,7 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
       // remove_available: the new members, one thread each, all their loads in flight at once
       // (member i on thread i + 64: wave 0, which publishes the next record, keeps no
       // outstanding stores for that record's drain to wait on)
-      if (!A.etake || mslot)
+      if ((!A.etake && !early) || mslot)
         for (uint64_t i = (threadIdx.x + NT - 64) % NT; i < nflag && i < PLIST; i += NT)
           take(M + i, s_plist[i], false, (int64_t)i);
       npend = nflag < PLIST ? (uint32_t)nflag : PLIST;

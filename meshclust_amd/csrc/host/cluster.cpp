@@ -227,9 +227,11 @@ struct SharedMailbox {
   }
 };
 
-static bool attach_mailbox(const ShardComm &comm, mc_ctx *ctx, uint64_t n, uint32_t nbins, SharedMailbox &mb) {
+static bool attach_mailbox(const ShardComm &comm, mc_ctx *ctx, uint64_t n, uint32_t nbins, SharedMailbox &mb,
+                           bool failed_before) {
   struct Blk {
-    char name[56];
+    char name[52];
+    int32_t failed;  // this rank's process once saw the mailbox hand-offs time out
     int32_t ok;
     uint32_t grid;  // this rank's accumulation grid (then: its plan's tile of ownership)
     char pci[64];   // this rank's GPU: ranks on one GPU split its CUs
@@ -238,6 +240,7 @@ static bool attach_mailbox(const ShardComm &comm, mc_ctx *ctx, uint64_t n, uint3
   const int W = comm.world;
   const size_t bytes = mc_mailbox_bytes(W, n);
   Blk mine{};
+  mine.failed = failed_before ? 1 : 0;
   if (mc_ctx_pci_bus_id(ctx, mine.pci, sizeof mine.pci) != MC_OK) mine.pci[0] = 0;
   int fd = -1;
   if (comm.rank == 0) {
@@ -250,6 +253,7 @@ static bool attach_mailbox(const ShardComm &comm, mc_ctx *ctx, uint64_t n, uint3
   if (comm.allgather(comm.user, &mine, sizeof mine, all.data()) != 0)
     throw PeerError("mailbox all-gather across ranks failed");
   bool ok = all[0].ok != 0;
+  for (const auto &b : all) ok &= b.failed == 0;  // (any rank's earlier timeout: none of them tries)
   if (ok && comm.rank != 0) fd = shm_open(all[0].name, O_RDWR, 0600);
   if (ok && fd >= 0) {
     void *p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
@@ -262,10 +266,14 @@ static bool attach_mailbox(const ShardComm &comm, mc_ctx *ctx, uint64_t n, uint3
   int share = 0;
   for (const auto &b : all) share += strncmp(b.pci, mine.pci, sizeof mine.pci) == 0;
   uint32_t info[4] = {0, 0, 0, 0};
-  if (mb.p && mc_set_mailbox(ctx, mb.p, bytes, comm.rank, W, std::max(share, 1)) == MC_OK &&
-      mc_accum_plan_info(ctx, nbins, info) == MC_OK)
+  // (mb.ctx: the mailbox is registered with this context, whatever the plan says -- every exit
+  // below that does not use it detaches it before the segment is unmapped)
+  bool plan = false;
+  if (ok && mb.p && mc_set_mailbox(ctx, mb.p, bytes, comm.rank, W, std::max(share, 1)) == MC_OK) {
     mb.ctx = ctx;
-  mine.ok = mb.ctx != nullptr;
+    plan = mc_accum_plan_info(ctx, nbins, info) == MC_OK;
+  }
+  mine.ok = plan;
   mine.grid = info[0];
   if (comm.allgather(comm.user, &mine, sizeof mine, all.data()) != 0)
     throw PeerError("mailbox all-gather across ranks failed");
@@ -279,7 +287,13 @@ static bool attach_mailbox(const ShardComm &comm, mc_ctx *ctx, uint64_t n, uint3
   if (ok) {
     uint32_t gmin = ~0u;
     for (const auto &b : all) gmin = std::min(gmin, b.grid);
-    mine.grid = (mc_set_accum_grid(ctx, gmin) == MC_OK && mc_accum_plan_info(ctx, nbins, info) == MC_OK) ? info[1] : 0;
+    // every device buffer of the accumulation is allocated before this all-gather, so no rank
+    // frees memory (hipFree waits for the whole device) once any rank's persistent kernel spins
+    // on the mailbox: the ranks of one process share the device
+    mine.grid = (mc_set_accum_grid(ctx, gmin) == MC_OK && mc_accum_plan_info(ctx, nbins, info) == MC_OK &&
+                 mc_accum_reserve(ctx, nbins) == MC_OK)
+                    ? info[1]
+                    : 0;
     if (comm.allgather(comm.user, &mine, sizeof mine, all.data()) != 0)
       throw PeerError("mailbox all-gather across ranks failed");
     for (const auto &b : all) ok &= b.grid != 0 && b.grid == all[0].grid;
@@ -432,14 +446,15 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
   // scans its tiles and the kernels exchange each step through the shared mailbox
   // (mc_set_mailbox); MC_SHARD_HOST_STEPS=1, or a mailbox that cannot be attached on every
   // rank, keeps the host-driven sharded steps (mc_scan_part + all-gather + mc_scan_commit).
+  comm_phase(cfg.comm, "accumulate");
   fault_point(cfg.comm, "accumulate");
   SharedMailbox mbox;
-  // (a mailbox whose hand-offs once timed out on these ranks is not tried again by this process:
-  // every clustering after the first goes straight to the host-driven sharded steps; all ranks
-  // saw the same timeout, so they agree)
+  // (a mailbox whose hand-offs once timed out in this process is not tried again: every later
+  // clustering goes to the host-driven sharded steps -- the ranks agree on it in
+  // attach_mailbox's first all-gather, so a group whose ranks have different histories agrees)
   static std::atomic<bool> mailbox_failed{false};
-  const bool dev_shard = shard && !getenv("MC_SHARD_HOST_STEPS") && !getenv("MC_ACCUM_STEPS") && !mailbox_failed.load() &&
-                         attach_mailbox(*shard, ctx, order.size(), (uint32_t)bv.bins().size(), mbox);
+  const bool dev_shard = shard && !getenv("MC_SHARD_HOST_STEPS") && !getenv("MC_ACCUM_STEPS") &&
+                         attach_mailbox(*shard, ctx, order.size(), (uint32_t)bv.bins().size(), mbox, mailbox_failed.load());
   // The device-resident loop (mc_accumulate) unless alignment mode or the configuration
   // asks for the step API; MC_ACCUM_STEPS=1 forces the host-driven loop (both are GPU paths).
   bool done = false;
@@ -502,6 +517,11 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
       stats.accum_path = dev_shard                              ? "device x" + std::to_string(shard->world)
                          : (multi && cfg.comm->world > 1) ? "device (replicated x" + std::to_string(cfg.comm->world) + ")"
                                                           : "device";
+    } else if (rc == MC_ERR_TIMEOUT && !dev_shard) {
+      // (a replicated or single-rank loop depends on no other rank: a hand-off deadline here
+      // means this GPU did not run the persistent grid together -- the step loop is exact too)
+      stats.accum_path = std::string("steps (") + mc_last_error() + ")";
+      fprintf(stderr, "meshclust: device accumulation timed out; taking the host-driven get_close steps\n");
     } else if (rc != MC_ERR_UNSUPPORTED) {
       check(rc, "mc_accumulate");
     } else if (dev_shard) {  // (every rank: the same configuration) -> the host-driven sharded steps
@@ -524,6 +544,7 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
     while (last != BVec::NONE)
       accumulate(&last, ds, ctx, bv, part, cfg, stats, flag_buf, timer, memo.get(), shard, all_flagged);
   }
+  comm_phase(cfg.comm, "update");
   Scope s(timer, "update+merge");
   std::vector<uint8_t> fused_sim;
   std::vector<double> fused_c0;

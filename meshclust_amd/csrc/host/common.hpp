@@ -33,6 +33,11 @@ struct PeerError : Error {
   explicit PeerError(const std::string &m) : Error(m, 1) {}
 };
 
+// Labels the all-gathers that follow on `comm` (run_pipeline wraps every rank's comm with a
+// timer): per phase, the time this rank waited for the last rank to arrive and the exchange
+// itself, "comm.<phase>.wait" / "comm.<phase>.xfer" in ms, with ".calls" and ".kb" beside them.
+void comm_phase(const ShardComm *comm, const char *phase);
+
 // Throws mc::Error when an ABI call fails (no fallback path exists).
 inline void check(int rc, const char *what) {
   if (rc != MC_OK) {

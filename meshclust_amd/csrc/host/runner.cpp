@@ -139,8 +139,88 @@ bool tune_host_heap() {
   return ok == 1;
 }
 
-RunResult run_pipeline(const Dataset &ds, mc_ctx *ctx, Options opt, bool upload, const ShardComm *comm) {
+// The ranks' all-gathers, timed.  Each block travels with its sender's entry time on the
+// host's monotonic clock (one clock for every process of a node), so a rank splits each
+// exchange into waiting for the last rank to arrive and the exchange after that.
+struct TimedComm {
+  ShardComm inner;
+  PhaseTimer *timer = nullptr;
+  std::string phase = "setup";
+  std::vector<uint8_t> ib, ob;
+};
+
+static double mono_us() {
+  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+static int timed_allgather(void *user, const void *in, uint64_t bytes, void *out) {
+  auto *t = (TimedComm *)user;
+  const int W = t->inner.world;
+  const uint64_t blk = 8 + bytes;
+  t->ib.resize(blk);
+  t->ob.resize(blk * (uint64_t)W);
+  const double t0 = mono_us();
+  memcpy(t->ib.data(), &t0, 8);
+  if (bytes) memcpy(t->ib.data() + 8, in, bytes);
+  const int rc = t->inner.allgather(t->inner.user, t->ib.data(), blk, t->ob.data());
+  const double t1 = mono_us();
+  if (rc) return rc;
+  double last = t0;
+  for (int r = 0; r < W; r++) {
+    double tr;
+    memcpy(&tr, t->ob.data() + blk * r, 8);
+    last = std::max(last, tr);
+    if (bytes) memcpy((char *)out + bytes * r, t->ob.data() + blk * r + 8, bytes);
+  }
+  const std::string k = "comm." + t->phase;
+  t->timer->add(k + ".wait", (last - t0) / 1000.0);
+  t->timer->add(k + ".xfer", (t1 - std::max(last, t0)) / 1000.0);
+  t->timer->add(k + ".calls", 1.0);
+  t->timer->add(k + ".kb", (double)(blk * (uint64_t)W) / 1024.0);
+  return 0;
+}
+
+void comm_phase(const ShardComm *comm, const char *phase) {
+  if (comm && comm->allgather == timed_allgather) ((TimedComm *)comm->user)->phase = phase;
+}
+
+// Ranks sharing one GPU (the one-GPU rehearsal, or --devices 0,0): each context takes a CU
+// partition of its own (mc_ctx_partition), slot = its order among the ranks with the same PCI
+// bus id.  Their kernels then never queue behind one another's persistent grids.
+static void partition_shared_gpu(const ShardComm &comm, mc_ctx *ctx, PhaseTimer &timer) {
+  struct Blk {
+    char pci[64];
+  };
+  Blk mine{};
+  if (mc_ctx_pci_bus_id(ctx, mine.pci, sizeof mine.pci) != MC_OK) mine.pci[0] = 0;
+  std::vector<Blk> all(comm.world);
+  if (comm.allgather(comm.user, &mine, sizeof mine, all.data()) != 0) throw PeerError("all-gather across ranks failed");
+  int share = 0, slot = 0;
+  for (int r = 0; r < comm.world; r++)
+    if (mine.pci[0] && strncmp(all[r].pci, mine.pci, sizeof mine.pci) == 0) {
+      if (r < comm.rank) slot++;
+      share++;
+    }
+  if (share > 1 && !getenv("MC_NO_PARTITION")) {
+    check(mc_ctx_partition(ctx, slot, share), "mc_ctx_partition");
+    timer.add("gpu_share", (double)share);
+  }
+}
+
+RunResult run_pipeline(const Dataset &ds, mc_ctx *ctx, Options opt, bool upload, const ShardComm *comm_in) {
   RunResult rr;
+  TimedComm tcomm;
+  ShardComm wrapped;
+  const ShardComm *comm = comm_in;
+  if (comm_in && comm_in->allgather) {
+    tcomm.inner = *comm_in;
+    tcomm.timer = &rr.timer;
+    wrapped = *comm_in;
+    wrapped.allgather = timed_allgather;
+    wrapped.user = &tcomm;
+    comm = &wrapped;
+    if (comm->world > 1) partition_shared_gpu(*comm, ctx, rr.timer);
+  }
   rr.n = ds.size();
   const bool verbose = !opt.quiet;
   int threads = opt.threads;
@@ -173,6 +253,7 @@ RunResult run_pipeline(const Dataset &ds, mc_ctx *ctx, Options opt, bool upload,
     if (verbose) printf("Using %d bit histograms\n", 8 * width);
     check(mc_kmer_build(ctx, opt.k, width), "mc_kmer_build");
   }
+  comm_phase(comm, "train");
   TrainerConfig tc;
   tc.n_points = opt.sample_size;
   tc.max_pts_from_one = opt.pivots;

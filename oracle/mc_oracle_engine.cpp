@@ -499,6 +499,13 @@ int mc_accum_plan_info(mc_ctx *, uint32_t, uint32_t *) {
   return fail(MC_ERR_UNSUPPORTED, "the CPU oracle engine drives accumulation step by step");
 }
 int mc_set_accum_grid(mc_ctx *, uint32_t) { return MC_OK; }
+int mc_accum_reserve(mc_ctx *, uint32_t) {
+  return fail(MC_ERR_UNSUPPORTED, "the CPU oracle engine drives accumulation step by step");
+}
+// (ranks of the CPU engine share the host's cores; there is no CU mask to split)
+int mc_ctx_partition(mc_ctx *, int slot, int share) {
+  return share < 1 || slot < 0 || slot >= share ? MC_ERR_ARG : MC_OK;
+}
 
 // RCCL is a GPU-side transport: the CPU engine's ranks exchange through the caller's callback.
 int mc_comm_unique_id(uint8_t *) { return fail(MC_ERR_UNSUPPORTED, "no RCCL in the CPU oracle engine"); }

@@ -279,19 +279,21 @@ def test_bench_two_gpus_D100k(tmp_path):
 HARNESS = os.path.join(ROOT, "oracle", "_build", "meshclust_cpu")
 
 
-def _cli(binary, name, tmp_path, devices, env_extra=None, timeout=600):
+def _cli(binary, name, tmp_path, devices, env_extra=None, timeout=600, shard_accum=True):
+    """bin/meshclust --devices.  Ranks that share a GPU run in the product's default environment:
+    each rank's context takes a CU partition of its own (mc_ctx_partition: a CU-masked stream,
+    a hardware queue per rank) and every rank allocates before any rank launches
+    (mc_accum_reserve), so no rank's work waits behind another rank's persistent kernel."""
     fa, flags = fixtures.e2e_input(name, tmp_path)
     out = str(tmp_path / (name + ".clstr"))
     st = out + ".json"
-    ids = devices.split(",")
-    if len(set(ids)) < len(ids):
-        # ranks sharing a GPU in one process: each rank's persistent accumulation kernel needs a
-        # hardware queue of its own (with HIP's default of 4 per process, a rank's launch can
-        # land behind the other rank's spinning kernel until the mailbox deadline)
-        env_extra = {"GPU_MAX_HW_QUEUES": "8", **(env_extra or {})}
+    env = dict(os.environ)
+    env.pop("GPU_MAX_HW_QUEUES", None)
+    if shard_accum:
+        env["MC_SHARD_ACCUM"] = "1"
+    env.update(env_extra or {})
     r = subprocess.run([binary, fa] + flags + ["--devices", devices, "--output", out, "--stats-json", st, "--quiet",
-                        "--threads", "4"], capture_output=True, text=True, timeout=timeout,
-                       env={**os.environ, "MC_SHARD_ACCUM": "1", **(env_extra or {})})
+                        "--threads", "4"], capture_output=True, text=True, timeout=timeout, env=env)
     return r, out, st
 
 
@@ -349,5 +351,24 @@ def test_devices_cli_gpu_byte_identical(name, devices, tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     w = len(devices.split(","))
     assert json.load(open(st))["accum_path"] == ("device x%d" % w if w > 1 else "device")
+    with gzip.open(fixtures.golden("e2e_%s.clstr.gz" % name), "rb") as f:
+        assert open(out, "rb").read() == f.read()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["fam2k", "big2_3k"])
+def test_devices_cli_gpu_default_env_replicated(name, tmp_path):
+    """--devices 0,0 with the product's defaults (no MC_SHARD_ACCUM): inputs this small fit one
+    rank's CU partition in the dense resident form, so every rank runs the whole accumulation
+    chain itself ("device (replicated x2)"), each on its own CUs; the comm timers are in the
+    stats."""
+    import meshclust_amd as M
+    M.build()
+    r, out, st = _cli(M.BIN, name, tmp_path, "0,0", shard_accum=False)
+    assert r.returncode == 0, r.stderr[-3000:]
+    stats = json.load(open(st))
+    assert stats["accum_path"] == "device (replicated x2)", stats["accum_path"]
+    assert stats["phases_ms"].get("gpu_share") == 2.0
+    assert stats["phases_ms"]["comm.update.calls"] >= 1
     with gzip.open(fixtures.golden("e2e_%s.clstr.gz" % name), "rb") as f:
         assert open(out, "rb").read() == f.read()
