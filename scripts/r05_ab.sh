@@ -10,4 +10,4 @@ if [ -n "${K:-}" ]; then
     || { echo "parity rc=$?"; tail -n 30 gpurun_out/ab_parity.log; exit 1; }
   tail -n 2 gpurun_out/ab_parity.log
 fi
-exec bash scripts/r04_ab.sh
+bash scripts/r04_ab.sh
