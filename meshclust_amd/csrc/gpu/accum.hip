@@ -320,7 +320,6 @@ int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, 
   A.spec = (pl.dense || pl.dstream) && !getenv("MC_ACCUM_NO_SPEC") ? 1 : 0;
   A.poll1 = getenv("MC_ACCUM_POLL1") ? 1 : 0;
   A.etake = getenv("MC_ACCUM_EARLY_TAKE") && atoi(getenv("MC_ACCUM_EARLY_TAKE")) ? 1 : 0;
-  A.helpers = getenv("MC_ACCUM_HELPERS") ? atoi(getenv("MC_ACCUM_HELPERS")) : 0;
   A.xfast = getenv("MC_ACCUM_NO_XFAST") ? 0 : 1;
   {
     const char *e = getenv("MC_ACCUM_RPOLL"), *g = getenv("MC_ACCUM_RPOLL_GAP");

@@ -136,9 +136,6 @@ struct AccArgs {
   int poll1;        // the controller polls a partial's tag granule before loading it whole
   int psleep;       // s_sleep between the controller's polls of a partial (0, 1, 2, 4)
   int etake;        // a polling thread takes its worker's flagged members as soon as it has the partial
-  int helpers;      // the controller's waves 4-7 during the fan-in (dense form, one rank): 1 apply the
-                    // last step's deferred bvec kills there (not beside the record's publication),
-                    // 2 also take the new members as the pollers list them (MC_ACCUM_HELPERS)
   int xfast;        // nearest-alive window also when an edge bin is empty (off: MC_ACCUM_NO_XFAST)
   int rpoll;        // dense workers: waves polling the step record (MC_ACCUM_RPOLL, 1..4)
   int rpoll_gap;    // ... wave w starts w * rpoll_gap * 512 clocks late (MC_ACCUM_RPOLL_GAP)
@@ -1810,7 +1807,6 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
   __shared__ uint32_t s_new;  // members taken into the cluster this step
   __shared__ uint32_t s_plist[PLIST];  // ... their positions
   __shared__ uint32_t s_pbin[PLIST];   // ... their bvec bins (kills deferred to the next window)
-  __shared__ uint32_t s_kdone, s_pdone;  // helper waves' kill passes / pollers done (cumulative)
   __shared__ uint64_t s_q[4];
   __shared__ uint32_t s_klast[KINL];
   __shared__ int s_abort;
@@ -1849,8 +1845,6 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
   if (threadIdx.x == 0) {
     s_abort = 0;
     s_new = 0;
-    s_kdone = 0;
-    s_pdone = 0;
   }
   uint64_t lg = 1;
   while (lg * 2 <= A.nb) lg *= 2;
@@ -1869,10 +1863,6 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
   bool rec_exact = false;  // the record being published carries the exact window (no part B)
   uint32_t npend = 0;   // new members s_plist[0, npend) whose bvec kills are still to be done
   uint64_t t_wait = 0, t_coll = 0, t_mark = 0;
-  uint32_t kdef = 0;                  // deferred kills (s_plist / s_pbin [0, kdef)) for the helper waves
-  uint32_t ncoll = 0, pdone_base = 0;  // collects so far; pollers counted in s_pdone before this one
-  // (helper waves: the dense / chunk forms on one rank; the mailbox path lists members later)
-  const bool helpers = A.helpers > 0 && !WIDE && A.mbox == nullptr;
   const uint64_t clk0 = prof_on ? __builtin_amdgcn_s_memtime() : 0, rt0 = prof_on ? now() : 0;
   uint64_t t_sub[4] = {0, 0, 0, 0};  // collect: reduce (stragglers), column sums, mean, closest
   uint64_t t_ws[4] = {0, 0, 0, 0};   // window: centre window data, window, record; [3] collect's takes
@@ -1880,8 +1870,15 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
   uint64_t t_pub[2] = {0, 0};        // window (spec): the record's span, the record's stores issued
   uint64_t t_wk[5] = {0, 0, 0, 0, 0};  // window: bvec kills, fast form, general form (time); fast, general (count)
 
+  // The controller's global stores of cluster bookkeeping (cluster table, member list, kill
+  // log) come from thread 64, never from wave 0: wave 0 publishes the next step record, and
+  // the compiler waits for every outstanding vector-memory operation of that wave before the
+  // record's first store (its words come from LDS or, for an uncached centre, global loads: one
+  // merged register, one conservative vmcnt(0)) -- a write-through store still in flight there
+  // held the record back by a memory round trip at every cluster change.
+  constexpr uint32_t BK = 64;
   auto finish_cluster = [&]() {
-    if (threadIdx.x == 0) {
+    if (threadIdx.x == BK) {
       A.cl_centre[ncl] = last;
       A.cl_off[ncl + 1] = cl_start + M;
     }
@@ -1892,9 +1889,9 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
   // accumulate's `current = {last}`: member 0 of a new cluster, its row, sums and window data
   // (kill: the seed also leaves the bvec here -- bvec::erase of get_close's best candidate --
   // with its bin from the member info, no search for it)
-  auto log_kill = [&](uint64_t p) {  // thread 0: a pop / erase, for the workers
-    st64(A.klog + kn, gran(kn + 1, (uint32_t)p));
-    s_klast[kn % KINL] = (uint32_t)p;
+  auto log_kill = [&](uint64_t p) {  // a pop / erase, for the workers (thread 0: LDS, thread BK: global)
+    if (threadIdx.x == BK) st64(A.klog + kn, gran(kn + 1, (uint32_t)p));
+    if (threadIdx.x == 0) s_klast[kn % KINL] = (uint32_t)p;
   };
   // (thread 0's global stores come after every load of the seed: a load behind a store waits
   // for the store, see publish)
@@ -1902,15 +1899,13 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
     if (A.mrow && !WIDE)
       for (int c = threadIdx.x; c < nch; c += NT) mc.row[c] = A.hr[pos * nch + c];
     for (int b = threadIdx.x; b < A.B; b += NT) msum[b] = reinterpret_cast<const T *>(A.hr + pos * nch)[b];
+    if (kill) log_kill(pos);
     if (threadIdx.x == 0) {
       if (A.mrow) {
         uint2 w[MINFO_W];
         minfo_issue(A.minfo + pos, w);
         const MInfo mi = minfo_take(w);
-        if (kill) {
-          bv.kill_in(pos, mi.bin);
-          log_kill(pos);
-        }
+        if (kill) bv.kill_in(pos, mi.bin);
         mc.pos[0] = (uint32_t)pos;
         mc.key[0] = 0;
         mc.info[0] = mi.mag;
@@ -1919,8 +1914,9 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
         mc.wt[0] = mi.wt;
       } else if (kill) {
         bv.kill_one(pos);
-        log_kill(pos);
       }
+    }
+    if (threadIdx.x == BK) {
       st32(A.mem_pos + cl_start, (uint32_t)pos);
       st64(A.mkeys + cl_start, 0);
     }
@@ -1936,10 +1932,8 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
     const int64_t b = bv.first_nonempty();
     if (b < 0) return NONE64;
     const uint64_t p = bv.select((uint64_t)b, 0);
-    if (threadIdx.x == 0) {
-      bv.kill_in(p, (uint64_t)b);
-      log_kill(p);
-    }
+    if (threadIdx.x == 0) bv.kill_in(p, (uint64_t)b);
+    log_kill(p);
     kn++;
     __syncthreads();
     return p;
@@ -2142,13 +2136,6 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
       }
       uint64_t tk0 = 0;
       if (prof_on && threadIdx.x == 0) tk0 = now();
-      // (helper waves: with the record's span the exact window, nothing reads the bvec before
-      // the collect's barrier, so the kills go to waves 4-7 while waves 0-3 poll)
-      if (npend && helpers && A.spec && rec_exact) {
-        kdef = npend;
-        npend = 0;
-        __syncthreads();  // (the barrier the kills ended with: the last collect's LDS words are free)
-      }
       if (npend) {  // the last step's bvec kills, after the record is out
         if (!(A.dbg & 1)) {
           for (uint32_t i = threadIdx.x; i < npend; i += NT) bv.kill_in(s_plist[i], s_pbin[i]);
@@ -2258,49 +2245,18 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
                               : 0u;
     // mailbox: this rank's slot of the step's parity; the local flagged positions go there
     uint64_t *mslot = A.mbox ? A.mbox + ((uint64_t)(step & 1) * A.W + A.rank) * A.slot_g : nullptr;
-    // thread t polls the partial of the t-th active worker until its granules carry the step,
-    // then lists that worker's flagged positions (a slot from an LDS counter: member order is
-    // irrelevant, the keys step << 32 | position order them like the bvec walk)
+    // thread P0 + t polls the partial of the t-th active worker until its granules carry the
+    // step, then lists that worker's flagged positions (a slot from an LDS counter: member order
+    // is irrelevant, the keys step << 32 | position order them like the bvec walk).  Wave 0 polls
+    // nothing: it publishes the next record, and anything it leaves in flight (a mailbox store
+    // to host memory) would hold that record's first store back (see BK).
+    constexpr uint32_t P0 = 64;
+    const uint32_t pt = threadIdx.x - P0;
     double bv_ = -1.0;
     uint64_t bp_ = NONE64;
     uint32_t cnt_w = 0, scan_w = 0;
-    const bool early = helpers && A.helpers >= 2;  // helper waves take the listed members
-    ncoll++;
-    if (helpers && threadIdx.x >= NT / 2) {
-      // ---- helper waves 4-7 (nact <= 255: no poller among them) ------------------------------
-      const uint32_t h = threadIdx.x - NT / 2;
-      for (uint32_t i = h; i < kdef; i += NT / 2) bv.kill_in(s_plist[i], s_pbin[i]);
-      if (early)
-        for (uint32_t i = h; i < PLIST; i += NT / 2) s_plist[i] = NONE;  // (an entry not listed yet)
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      if (lane == 0) atomicAdd(&s_kdone, 1u);
-      if (early) {
-        // entry e (e = h, h + 256, ...) is taken as soon as its poller has written it; done when
-        // every poller has finished and every listed entry below PLIST is taken
-        const uint64_t t0 = now();
-        uint32_t e = h;
-        for (uint32_t it = 1;; it++) {
-          const uint32_t pd = __hip_atomic_load(&s_pdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          const uint32_t nl = __hip_atomic_load(&s_new, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          const uint32_t lim = nl < PLIST ? nl : PLIST;
-          while (e < lim) {
-            const uint32_t p = __hip_atomic_load(&s_plist[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (p == NONE) break;
-            take(M + e, p, false, (int64_t)e);
-            e += NT / 2;
-          }
-          if (pd - pdone_base >= nact && e >= lim) break;  // (s_new is final once every poller is done)
-          if ((it & 255) == 0 && timed_out(A, t0)) {
-            s_abort = 1;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-        }
-        drain();  // (take's member-list stores, read back past the member cache)
-      }
-    }
-    if (threadIdx.x < nact) {  // (nact <= G - 1 < NT)
-      const uint32_t wk = Div32(GW).mod((uint32_t)c0 + threadIdx.x);
+    if (threadIdx.x >= P0 && pt < nact) {  // (nact <= G - 1 < NT - P0)
+      const uint32_t wk = Div32(GW).mod((uint32_t)c0 + pt);
       const uint64_t *q = A.partials + (uint64_t)wk * PART_G;
       const uint32_t poff = wk * PART_G * 8;
       const uint64_t t0 = now();
@@ -2346,15 +2302,6 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
         cnt_w = (uint32_t)g8[3];
         scan_w = (uint32_t)g8[4];
         // this worker's flagged positions into the step's list: cnt_w slots reserved at once
-        // (helper waves: after their kill pass has read the last step's entries)
-        if (helpers && cnt_w) {
-          const uint64_t tk = now();
-          for (uint32_t it = 1; __hip_atomic_load(&s_kdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < 4u * ncoll; it++) {
-            if ((it & 255) == 0 && timed_out(A, tk)) break;
-            __builtin_amdgcn_s_sleep(1);
-          }
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        }
         const uint32_t slot0 = cnt_w ? atomicAdd(&s_new, cnt_w) : 0u;
         for (uint32_t j = 0; j < cnt_w; j++) {
           const uint32_t p = j < (uint32_t)INL ? (uint32_t)g8[5 + j] : ld32(A.fpos + (uint64_t)wk * A.fcap + j);
@@ -2362,21 +2309,14 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
           if (mslot) {  // (several ranks: every rank takes the union, below)
             st64x(mslot + (slot < (uint32_t)MBOX_INL ? 5 + slot : MBOX_HDR - MBOX_INL + slot), gran(step, p));
           } else if (slot < PLIST) {
-            if (early) __hip_atomic_store(&s_plist[slot], p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            else s_plist[slot] = p;
-            if (A.etake && !early) take(M + slot, p, false, (int64_t)slot);  // (MC_ACCUM_EARLY_TAKE)
+            s_plist[slot] = p;
+            if (A.etake) take(M + slot, p, false, (int64_t)slot);  // (MC_ACCUM_EARLY_TAKE)
           } else {  // a list overflow: this thread takes the member itself (past the cache)
             take(M + slot, p, true);
             drain();
           }
         }
       }
-    }
-    if (helpers) {  // (every poller wave, after its last listing)
-      const uint64_t pb = __ballot(threadIdx.x < nact);
-      if (pb && lane == 0) atomicAdd(&s_pdone, (uint32_t)__popcll(pb));
-      pdone_base += nact;
-      kdef = 0;
     }
     if (prof_on && threadIdx.x == 0) {
       const uint64_t t = now();
@@ -2446,9 +2386,9 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
       // ---- the ranks' exchange: publish this rank's header, take every rank's ----------
       // get_close over the union is the serial loop's: is_min = nothing flagged anywhere, the
       // result the first maximum by (value, static position), every flagged candidate joins
-      if (threadIdx.x < MBOX_HDR) {
+      if (threadIdx.x >= BK && threadIdx.x < BK + MBOX_HDR) {  // (not wave 0, see BK)
         const uint64_t vb = (uint64_t)__double_as_longlong(best_val);
-        const int j = threadIdx.x;
+        const int j = threadIdx.x - BK;
         const uint32_t data = j == 0   ? (uint32_t)(vb >> 32)
                               : j == 1 ? (uint32_t)vb
                               : j == 2 ? (best_pos == NONE64 ? NONE : (uint32_t)best_pos)
@@ -2540,7 +2480,7 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
       // remove_available: the new members, one thread each, all their loads in flight at once
       // (member i on thread i + 64: wave 0, which publishes the next record, keeps no
       // outstanding stores for that record's drain to wait on)
-      if ((!A.etake && !early) || mslot)
+      if (!A.etake || mslot)
         for (uint64_t i = (threadIdx.x + NT - 64) % NT; i < nflag && i < PLIST; i += NT)
           take(M + i, s_plist[i], false, (int64_t)i);
       npend = nflag < PLIST ? (uint32_t)nflag : PLIST;

@@ -111,9 +111,7 @@ def test_config_B100k_global_bitmap_equals_reference(product):
 
 
 @pytest.mark.parametrize("env,tag", [({"MC_ACCUM_DBG": "3"}, ".dbg3"), ({"MC_CLASSIFY_EXACT": "1"}, ".exact"),
-                                     ({"MC_CLASSIFY_NO_SMALL": "1"}, ".nosmall"),
-                                     ({"MC_ACCUM_HELPERS": "1"}, ".help1"), ({"MC_ACCUM_HELPERS": "2"}, ".help2"),
-                                     ({"MC_ACCUM_HELPERS": "0"}, ".help0")])
+                                     ({"MC_CLASSIFY_NO_SMALL": "1"}, ".nosmall")])
 def test_config_B100k_accum_variants_equal_reference(product, env, tag):
     """The accumulation kernel's opt-in forms (per-bin aggregated bvec kills and the
     quad-per-member closest search, MC_ACCUM_DBG=3), the workers' exact classifier
