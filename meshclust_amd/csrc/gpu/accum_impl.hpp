@@ -1443,6 +1443,7 @@ __device__ __forceinline__ void worker_dstream(const AccArgs &A, const DevClassi
   __shared__ uint32_t s_nfl, s_go, s_inl[INL], s_wc[NW], s_cnt;
   __shared__ int s_abort;
   __shared__ uint32_t s_arr;
+  __shared__ SmallK s_sk;  // classify_small's constants (read with each candidate's row)
   constexpr int NC = NCH > 0 ? NCH : DMAXCH;
   const uint32_t GW = gridDim.x - 1, w = blockIdx.x - 1;
   const Div32 dgw(GW);
@@ -1492,6 +1493,7 @@ __device__ __forceinline__ void worker_dstream(const AccArgs &A, const DevClassi
     s_cnt = 0;
     s_abort = 0;
     s_arr = 0;
+    s_sk = make_smallk(C, A.fc);
   }
   __syncthreads();
   {
@@ -1652,6 +1654,7 @@ __device__ __forceinline__ void worker_dstream(const AccArgs &A, const DevClassi
         for (int k = 0; k < NC; k++)
           if (k < nch) v[k] = ld_sc1_16(R, slot(e, k) * 16u);
         const uint4 inf = ld_sc1_16(R, slot(e, nch) * 16u);
+        const SmallK sk = lds_smallk(&s_sk);
         Acc<T> acc;
 #pragma unroll
         for (int k = 0; k < NC; k++)
@@ -1664,7 +1667,7 @@ __device__ __forceinline__ void worker_dstream(const AccArgs &A, const DevClassi
             const PSm ps{inf.x, inf.y, inf.z, inf.w, true};
             acc.fold();
             const double dap = C.layout == 4 ? mk_div((double)inf.x, (double)A.B, A.fc.rB) : 0.0;
-            d = classify_small(C, A.fc, acc.sad, acc.dot, ps, ps_q, kq, dap, tq.da, A.B, &cv, &und);
+            d = classify_small(sk, acc.sad, acc.dot, ps, ps_q, kq, dap, tq.da, A.B, &cv, &und);
           }
         }
         if (und) {  // (classify_small undecided or not applicable: the per-position arrays)
