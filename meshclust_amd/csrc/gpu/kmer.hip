@@ -115,6 +115,7 @@ struct KArgs {
   int k;
   int coop;          // 1: the waves of a workgroup share one sequence
   int shared;        // 1: ... and one table (k = 7: 4^7 u32 = 64 KiB of LDS)
+  int stream8;       // the streaming form (kmer_stream8) for 8-bit rows with k = 4..6
   uint32_t *gtab;    // k >= 8: per-wave tables in global memory (gridDim * KW * B)
   uint8_t *hist;
   uint64_t pitch;
@@ -293,9 +294,148 @@ __device__ __forceinline__ void write_row(const KArgs &A, uint64_t s, uint32_t *
   *wmax = mx > *wmax ? mx : *wmax;
 }
 
+// ---- the streaming form (8-bit rows, k = 4..6, one wave per sequence): configs B and D --------
+// A wave takes 64 sequences at a time (their metadata loaded lane by lane); for each one it
+// holds this lane's three packed words of its first 16-start group, and issues the NEXT
+// sequence's words before it counts the current one, so a sequence's load latency is covered by
+// the previous one's LDS work instead of stalling the wave.  The per-sequence row statistics
+// stay in registers (lane j keeps sequence j's) and go out as three coalesced 512-byte stores
+// per 64 sequences; the row maximum is a per-lane running maximum, reduced once per wave.
+struct Pre {
+  uint32_t w0, w1, w2;
+};
+__device__ __forceinline__ Pre pre_load(const KArgs &A, uint64_t pk0, uint64_t pk1, int64_t p0, bool act) {
+  Pre r{0u, 0u, 0u};
+  if (act) {
+    const uint32_t *w = A.pk + pk0 + (p0 >> 4);
+    const uint64_t nw = pk1 - pk0 - (uint64_t)(p0 >> 4);
+    r.w0 = w[0];
+    if (nw > 1) r.w1 = w[1];
+    if (nw > 2) r.w2 = w[2];
+  }
+  return r;
+}
+// the 16 (or fewer) k-mers of starts [p0, p0 + cnt) from this lane's words
+__device__ __forceinline__ void count_words(const Pre &w, int64_t p0, int cnt, int k, uint32_t mask, uint32_t *tab) {
+  const uint64_t lo = ((uint64_t)w.w1 << 32) | w.w0, hi = w.w2;
+  const int sh = (int)(p0 & 15) * 2;
+  const uint64_t win = sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+  uint32_t h = 0;
+  for (int i = 0; i < k - 1; i++) h = (h << 2) | (uint32_t)((win >> (2 * i)) & 3u);
+  for (int j = 0; j < cnt; j++) {
+    h = ((h << 2) | (uint32_t)((win >> (2 * (j + k - 1))) & 3u)) & mask;
+    atomicAdd(&tab[h], 1u);
+  }
+}
+
+__device__ __forceinline__ void kmer_stream8(const KArgs &A, uint32_t *tab, int B, bool write, uint64_t *wmax_out) {
+  const int wv = wave_id(), lane = threadIdx.x & 63;
+  const int k = A.k;
+  const uint32_t mask = (1u << (2 * k)) - 1u;
+  const uint64_t stride = (uint64_t)gridDim.x * KW;
+  uint32_t lmax = 0;  // this lane's largest bin (+ pseudocount) over every row it wrote
+  for (uint64_t sb = (uint64_t)blockIdx.x * KW + wv; sb < A.n; sb += 64 * stride) {
+    const uint64_t si = sb + (uint64_t)lane * stride;
+    const bool vi = si < A.n;
+    const uint64_t s0 = vi ? si : 0;
+    const uint64_t so0 = A.seq_off[s0], so1 = A.seq_off[s0 + 1], pk0 = A.pk_off[s0], pk1 = A.pk_off[s0 + 1];
+    const uint64_t g0 = A.seg_off[s0], g1 = A.seg_off[s0 + 1];
+    const bool one = vi && A.impure[s0] == 0 && g1 == g0 + 1;  // pure, one segment
+    const int32_t sf = one ? A.seg[2 * g0] : 0, sl = one ? A.seg[2 * g0 + 1] : 0;
+    const uint64_t left = (A.n - sb + stride - 1) / stride;
+    const int nb = left < 64 ? (int)left : 64;
+    uint64_t my_m = 0, my_sq = 0, my_len = 0;  // lane j: sequence j's statistics
+    // the first group's words of sequence jj (lane = group index), issued one sequence ahead
+    auto issue = [&](int jj) -> Pre {
+      const bool o = __builtin_amdgcn_readlane((int)one, jj) != 0;
+      if (!o) return Pre{0u, 0u, 0u};
+      const int64_t first = __builtin_amdgcn_readlane(sf, jj);
+      const int64_t last0 = (int64_t)__builtin_amdgcn_readlane(sl, jj) - k + 1;
+      const int64_t last = last0 < first ? first : last0;
+      const int64_t ng = (last - first) / 16 + 1;
+      return pre_load(A, readlane64(pk0, jj), readlane64(pk1, jj), first + (int64_t)lane * 16, lane < ng);
+    };
+    Pre cur = issue(0);
+    for (int jj = 0; jj < nb; jj++) {
+      const uint64_t s = sb + (uint64_t)jj * stride;
+      const uint64_t L = readlane64(so1, jj) - readlane64(so0, jj);
+      const Pre nxt = jj + 1 < nb ? issue(jj + 1) : Pre{0u, 0u, 0u};
+      if (__builtin_amdgcn_readlane((int)one, jj)) {
+        const int64_t first = __builtin_amdgcn_readlane(sf, jj);
+        const int64_t last0 = (int64_t)__builtin_amdgcn_readlane(sl, jj) - k + 1;
+        const int64_t p_lo = first, p_hi = last0 < first ? first : last0;
+        const uint64_t q0 = readlane64(pk0, jj), q1 = readlane64(pk1, jj);
+        const int64_t ngroups = (p_hi - p_lo) / 16 + 1;
+        for (int64_t g = lane; g < ngroups; g += 64) {
+          const int64_t p0 = p_lo + g * 16;
+          const int cnt = (int)(p_hi - p0 + 1 < 16 ? p_hi - p0 + 1 : 16);
+          if (p0 + cnt - 1 + k > (int64_t)L) {  // a k-mer past the sequence end (a segment shorter than k)
+            atomicOr(A.err, 1);
+            continue;
+          }
+          count_words(g == lane ? cur : pre_load(A, q0, q1, p0, true), p0, cnt, k, mask, tab);
+        }
+      } else {
+        count_sequence(A, s, tab, 0, 1);
+      }
+      cur = nxt;
+      tab_drain(false);
+      // the row: bins + pseudocount, written as bytes; magnitude and sum of squares reduced over
+      // the wave, the maximum kept per lane
+      uint32_t m = 0, sq = 0;  // (32 bits: a row of L < 2^16 - B k-mers has sum (c + 1)^2 < 2^32)
+      uint64_t m64 = 0, sq64 = 0;
+      const bool small = L + (uint64_t)B < 65536;
+      uint8_t *row = A.hist + s * A.pitch;
+      for (int q = lane; q < B / 4; q += 64) {
+        uint4 c = reinterpret_cast<const uint4 *>(tab)[q];
+        reinterpret_cast<uint4 *>(tab)[q] = make_uint4(0, 0, 0, 0);
+        c.x += 1;  // pseudocount (ClusterFactory.cpp:995)
+        c.y += 1;
+        c.z += 1;
+        c.w += 1;
+        m += c.x + c.y + c.z + c.w;
+        if (small) sq += c.x * c.x + c.y * c.y + c.z * c.z + c.w * c.w;
+        else sq64 += (uint64_t)c.x * c.x + (uint64_t)c.y * c.y + (uint64_t)c.z * c.z + (uint64_t)c.w * c.w;
+        lmax = max(max(c.x, c.y), max(max(c.z, c.w), lmax));
+        if (write) reinterpret_cast<uint32_t *>(row)[q] = (c.x & 0xffu) | (c.y & 0xffu) << 8 | (c.z & 0xffu) << 16 | (c.w & 0xffu) << 24;
+      }
+      if (write)  // the row's padding up to the pitch
+        for (uint64_t b = (uint64_t)B + lane; b < A.pitch; b += 64) row[b] = 0;
+      if (small) {
+        m = wave_sum32_all(m);
+        sq = wave_sum32_all(sq);
+        m64 = m;
+        sq64 = sq;
+      } else {
+        m64 = wave_sum64_all(m);
+        sq64 = wave_sum64_all(sq64);
+      }
+      if (lane == jj) {
+        my_m = m64;
+        my_sq = sq64;
+        my_len = L;
+      }
+      tab_drain(false);
+    }
+    if (write && lane < nb) {
+      const uint64_t s = sb + (uint64_t)lane * stride;
+      A.mag[s] = my_m;
+      A.sumsq[s] = my_sq;
+      A.len_out[s] = my_len;
+    }
+  }
+  uint32_t wm = lmax;
+#define MCG_MAX_STEP(C, R) wm = max(wm, dpp_mv<C, R>(wm, wm));
+  MCG_DPP_STEPS(MCG_MAX_STEP)
+#undef MCG_MAX_STEP
+  *wmax_out = (uint32_t)__builtin_amdgcn_readlane((int)wm, 63);
+}
+
 // GLOB: the tables in global scratch (k >= 8).  A compile-time choice: a table pointer picked
 // at run time between LDS and global memory makes every table access a FLAT instruction.
-template <typename T, bool GLOB>
+// STREAM: kmer_stream8 alone (a kernel of its own: its register allocation, not the general
+// form's, sets the occupancy).
+template <typename T, bool GLOB, bool STREAM = false>
 __global__ __launch_bounds__(KT) void kmer_kernel(KArgs A, bool write) {
   extern __shared__ __attribute__((aligned(16))) uint32_t ltab[];
   __shared__ uint64_t s_max[KW];
@@ -310,7 +450,9 @@ __global__ __launch_bounds__(KT) void kmer_kernel(KArgs A, bool write) {
   if (!A.shared || wv == 0)
     for (int b = lane; b < B; b += 64) tab_zero(mytab + b, glob);
   tab_drain(glob);
-  if (!A.coop) {
+  if constexpr (STREAM) {
+    kmer_stream8(A, mytab, B, write, &wmax);
+  } else if (!A.coop) {
     // one wave per sequence: the wave's own table, no workgroup barrier.  The metadata of the
     // wave's next 64 sequences (offsets, purity, segment bounds) are loaded lane by lane in two
     // round trips and handed out by readlane, instead of a chain of dependent loads per sequence
@@ -361,7 +503,9 @@ __global__ __launch_bounds__(KT) void kmer_kernel(KArgs A, bool write) {
   if (threadIdx.x == 0) {
     uint64_t t = 0;
     for (int i = 0; i < KW; i++) t = s_max[i] > t ? s_max[i] : t;
-    atomicMax(A.gmax, (unsigned long long)t);
+    // (one device-scope atomic per workgroup only when it raises the maximum: thousands of
+    // same-address atomics serialise at one L2 channel)
+    if (t > __hip_atomic_load(A.gmax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(A.gmax, (unsigned long long)t);
   }
 }
 
@@ -406,6 +550,7 @@ int launch_kmer(mc_ctx *c, int k, int width, bool write, uint64_t *d_max, int *d
   const bool per_wave_lds = (size_t)KW * B * 4 <= 64 * 1024, shared_lds = !per_wave_lds && (size_t)B * 4 <= 64 * 1024;
   A.shared = shared_lds ? 1 : 0;
   A.coop = (c->n && c->h_seq_off[c->n] / c->n >= 4096) || shared_lds ? 1 : 0;
+  A.stream8 = getenv("MC_KMER_NO_STREAM") ? 0 : 1;
   A.hist = (uint8_t *)c->hist.p;
   A.pitch = c->pitch;
   A.mag = (uint64_t *)c->mag.p;
@@ -432,7 +577,12 @@ int launch_kmer(mc_ctx *c, int k, int width, bool write, uint64_t *d_max, int *d
   timed_begin(c);
   const bool g = A.gtab != nullptr;
   switch (width) {
-    case 1: (g ? kmer_kernel<uint8_t, true> : kmer_kernel<uint8_t, false>)<<<grid, KT, lds, c->stream>>>(A, write); break;
+    case 1:
+      if (!g && !A.coop && !A.shared && (B & 255) == 0 && A.stream8)
+        kmer_kernel<uint8_t, false, true><<<grid, KT, lds, c->stream>>>(A, write);
+      else
+        (g ? kmer_kernel<uint8_t, true> : kmer_kernel<uint8_t, false>)<<<grid, KT, lds, c->stream>>>(A, write);
+      break;
     case 2: (g ? kmer_kernel<uint16_t, true> : kmer_kernel<uint16_t, false>)<<<grid, KT, lds, c->stream>>>(A, write); break;
     case 4: (g ? kmer_kernel<uint32_t, true> : kmer_kernel<uint32_t, false>)<<<grid, KT, lds, c->stream>>>(A, write); break;
     default: (g ? kmer_kernel<uint64_t, true> : kmer_kernel<uint64_t, false>)<<<grid, KT, lds, c->stream>>>(A, write); break;

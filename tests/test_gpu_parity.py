@@ -95,6 +95,43 @@ def test_kmer_all_k_and_table_modes_vs_oracle(eng, mean_len):
         assert np.array_equal(mags, want.sum(axis=1)), k
 
 
+@pytest.mark.parametrize("k", [4, 5, 6])
+def test_kmer_stream_equals_general(eng, k, monkeypatch):
+    """K1's streaming form (8-bit rows, k = 4..6: the next sequence's words in flight while the
+    current one is counted, statistics stored per 64 sequences) against the general form
+    (MC_KMER_NO_STREAM) and the oracle: several 64-sequence batches per wave, sequences longer
+    than 64 16-start groups, several segments, 'N' bytes (impure), segments shorter than k.
+    The PEARSON feature checks the sums of squares, the histograms and magnitudes the rest."""
+    rng = np.random.default_rng(40 + k)
+    recs = []
+    for i in range(1500):
+        L = int(rng.integers(20, 2600)) if i % 50 else int(rng.integers(1, 8))
+        c = rng.integers(0, 4, size=L).astype(np.uint8)
+        if i % 7 == 0 and L > 60:
+            a = L // 2
+            c[a:a + 9] = 78
+            recs.append((c, [[0, a - 1], [a + 9, L - 1]]))
+        else:
+            recs.append((c, [[0, L - 1]]))
+    recs = [r for r in recs if all(e - s + 1 >= k for s, e in r[1])]
+    load_records(eng, recs)
+    want = np.array([O.kmer_hist(c, s, k) for c, s in recs])
+    assert want.max() <= 255
+    ij = np.array([(i, (i * 7 + 3) % len(recs)) for i in range(len(recs))], np.uint32)
+    flags = [(1 << 5), (1 << 4), (1 << 2)]  # PEARSON, INTERSECTION, MANHATTAN
+    out = {}
+    for mode in ("stream", "general"):
+        if mode == "general":
+            monkeypatch.setenv("MC_KMER_NO_STREAM", "1")
+        assert eng.kmer_max(k) == int(want.max())
+        eng.kmer_build(k, 1)
+        h, mags = eng.histograms()
+        assert np.array_equal(h.astype(np.uint64), want), mode
+        assert np.array_equal(mags, want.sum(axis=1)), mode
+        out[mode] = eng.pair_features(ij[:, 0], ij[:, 1], flags)
+    assert np.array_equal(out["stream"], out["general"])
+
+
 def test_load_packed_equals_bytes(eng):
     """mc_load_packed (2-bit words + exception bytes, the host parser's form) leaves the same
     sequences on the device as mc_load_sequences: same histograms, same NW identities."""
