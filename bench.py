@@ -137,6 +137,45 @@ def spawn_ranks(n):
     return rc
 
 
+NW_STEADY_INSTS_PER_CELL = 19.9
+# The accumulation's step-latency floor ("The floor"): a get_close step cannot
+# take less than two cross-CU hand-offs (the step record out to the workers, their partials
+# back; MI355X_MICROARCH.md price list, handoff-1to1, idle, 8 B: 0.8 us each), one candidate
+# wave's scoring chain at the VALU issue interval of one wave per SIMD (the ISA's instructions
+# per candidate wave, scripts/isa_count.py -> profiles/r05/accum_isa_counts.json; 5.7 clocks per
+# wave instruction at one wave per SIMD, profiles/r04/valu_peak.json, 2.4 GHz), and in a member
+# step one dependent memory round trip for the new members' rows (half a hand-off, 0.4 us).
+HOP_US = 0.8
+SCORE_WAVE_INSTS = 324  # profiles/r05/accum_isa_counts.json "valu"
+CLK_PER_WAVE_INST = 5.7
+MEMBER_LOAD_US = 0.4
+
+
+def latency_floor(achieved_us, stats):
+    steps = sum(s["scan_steps"] for s in stats)
+    clusters = sum(s["clusters"] for s in stats)
+    member_frac = max(0.0, 1.0 - clusters / steps) if steps else 0.0  # (one is_min step per cluster)
+    score = SCORE_WAVE_INSTS * CLK_PER_WAVE_INST / 2.4e3
+    floor = 2 * HOP_US + score + member_frac * MEMBER_LOAD_US
+    return {"floor_us_per_step": round(floor, 3), "achieved_us_per_step": achieved_us,
+            "frac": round(floor / achieved_us, 4) if achieved_us else None,
+            "hops_us": 2 * HOP_US, "score_us": round(score, 3), "member_load_us": round(member_frac * MEMBER_LOAD_US, 3),
+            "member_step_frac": round(member_frac, 3),
+            "model": "2 hand-offs (handoff-1to1 idle) + one candidate wave's VALU chain at 1 wave/SIMD + "
+                     "a member step's dependent row load"}
+
+
+def comm_summary(stats):
+    """Per phase, ms per step of waiting for the last rank and of the exchange itself (the
+    ranks' all-gathers are timed in C++, runner.cpp TimedComm), calls and KB."""
+    out = {}
+    for s in stats:
+        for k, v in s["phases_ms"].items():
+            if k.startswith("comm."):
+                out[k[5:]] = out.get(k[5:], 0.0) + v / len(stats)
+    return {k: round(v, 3) for k, v in sorted(out.items())} or None
+
+
 def kernel_pmc(kname):
     """The FETCH_SIZE / WRITE_SIZE passes of a kernel (rocprofv3 --pmc, separate passes,
     scripts/pmc_summary.py): HBM bytes per launch, FETCH doubled per the gfx950 note."""
@@ -312,6 +351,8 @@ def main():
                         ("priced against HBM by algorithmic bytes (SURVEY.md §8(d)); on one to four GPUs "
                          "the workers stream every window's rows from HBM (dense streaming form, DESIGN.md "
                          "§3.1c); at eight each rank's share of the rows is LDS-resident (§6)")}
+        if device_loop and a.workload == "B":
+            roof["latency_floor"] = latency_floor(roof["us_per_step"], stats)
         if a.workload == "B" and not shard and world == 1:  # (the counters are of the config-B launch)
             tr = kernel_pmc(kname)
             if tr is not None:
@@ -346,11 +387,15 @@ def main():
     nwc_path = os.path.join(ROOT, "profiles", "nw_counters.json")
     nwc = json.load(open(nwc_path)) if os.path.exists(nwc_path) else {}
     lane_ops = nwc.get("valu_lane_ops_per_s", 256 * 4 * 16 * 2.4e9)
-    ipc = nwc.get("lane_insts_per_cell", 20.0)
+    # priced at the throughput form's steady-state step, 19.9 lane-instructions per cell (the ISA
+    # count): the latency form's hand-offs, ramps and barriers are overhead, not
+    # work, so they count against the fraction (the kernels' own counter ratio is kept beside it)
+    ipc = NW_STEADY_INSTS_PER_CELL
     nw_peak = lane_ops / ipc
     nw_roof = {"bound": "valu", "achieved": nw_rate, "peak": nw_peak, "unit": "cells/s",
                "frac": round(nw_rate / nw_peak, 4) if nw_rate else None,
-               "lane_insts_per_cell": ipc, "valu_lane_ops_per_s": lane_ops,
+               "lane_insts_per_cell": ipc, "kernel_lane_insts_per_cell": nwc.get("lane_insts_per_cell"),
+               "valu_lane_ops_per_s": lane_ops,
                "cells_per_step": nw_cells / a.steps, "ms_per_step": round(fam_ms["nw"] / a.steps, 3)}
     if nwc:
         nw_roof["counters"] = nwc
@@ -401,6 +446,7 @@ def main():
                   "device_ms_per_step": {f: round(v / a.steps, 3) for f, v in fam_ms.items()},
                   "launches_per_step": {f: round(v / a.steps, 1) for f, v in fam_n.items()},
                   "host_phases_ms": s0["phases_ms"], "accum_path": s0.get("accum_path"),
+                  "comm_ms_per_step": comm_summary(stats),
                   "warmup_s": round(first_s, 3), "scan_steps": s0["scan_steps"],
                   "rehearsal_one_gpu": one_gpu},
     }

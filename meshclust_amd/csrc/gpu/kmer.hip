@@ -328,8 +328,13 @@ __device__ __forceinline__ void count_words(const Pre &w, int64_t p0, int cnt, i
   }
 }
 
-__device__ __forceinline__ void kmer_stream8(const KArgs &A, uint32_t *tab, int B, bool write, uint64_t *wmax_out) {
+// S sub-tables per wave (lanes l*64/S .. (l+1)*64/S - 1 count into sub-table l): a k-mer
+// increment is an LDS atomic, and lanes of one instruction that hit the same bin serialise;
+// S tables take those collisions apart (k = 4: S = 4, 4 KiB per wave).  The row sums them.
+template <int S>
+__device__ __forceinline__ void kmer_stream8(const KArgs &A, uint32_t *tab0, int B, bool write, uint64_t *wmax_out) {
   const int wv = wave_id(), lane = threadIdx.x & 63;
+  uint32_t *tab = tab0 + (size_t)(lane / (64 / S)) * B;
   const int k = A.k;
   const uint32_t mask = (1u << (2 * k)) - 1u;
   const uint64_t stride = (uint64_t)gridDim.x * KW;
@@ -338,13 +343,15 @@ __device__ __forceinline__ void kmer_stream8(const KArgs &A, uint32_t *tab, int 
     const uint64_t si = sb + (uint64_t)lane * stride;
     const bool vi = si < A.n;
     const uint64_t s0 = vi ? si : 0;
-    const uint64_t so0 = A.seq_off[s0], so1 = A.seq_off[s0 + 1], pk0 = A.pk_off[s0], pk1 = A.pk_off[s0 + 1];
+    // (sequence lengths and packed word counts below 2^32: the loader's limits)
+    const uint64_t pk0 = A.pk_off[s0];
+    const uint32_t Ls = (uint32_t)(A.seq_off[s0 + 1] - A.seq_off[s0]), npk = (uint32_t)(A.pk_off[s0 + 1] - pk0);
     const uint64_t g0 = A.seg_off[s0], g1 = A.seg_off[s0 + 1];
     const bool one = vi && A.impure[s0] == 0 && g1 == g0 + 1;  // pure, one segment
     const int32_t sf = one ? A.seg[2 * g0] : 0, sl = one ? A.seg[2 * g0 + 1] : 0;
     const uint64_t left = (A.n - sb + stride - 1) / stride;
     const int nb = left < 64 ? (int)left : 64;
-    uint64_t my_m = 0, my_sq = 0, my_len = 0;  // lane j: sequence j's statistics
+    uint64_t my_m = 0, my_sq = 0;  // lane j: sequence j's statistics (its length is Ls)
     // the first group's words of sequence jj (lane = group index), issued one sequence ahead
     auto issue = [&](int jj) -> Pre {
       const bool o = __builtin_amdgcn_readlane((int)one, jj) != 0;
@@ -353,18 +360,19 @@ __device__ __forceinline__ void kmer_stream8(const KArgs &A, uint32_t *tab, int 
       const int64_t last0 = (int64_t)__builtin_amdgcn_readlane(sl, jj) - k + 1;
       const int64_t last = last0 < first ? first : last0;
       const int64_t ng = (last - first) / 16 + 1;
-      return pre_load(A, readlane64(pk0, jj), readlane64(pk1, jj), first + (int64_t)lane * 16, lane < ng);
+      const uint64_t q0 = readlane64(pk0, jj);
+      return pre_load(A, q0, q0 + (uint32_t)__builtin_amdgcn_readlane((int)npk, jj), first + (int64_t)lane * 16, lane < ng);
     };
     Pre cur = issue(0);
     for (int jj = 0; jj < nb; jj++) {
       const uint64_t s = sb + (uint64_t)jj * stride;
-      const uint64_t L = readlane64(so1, jj) - readlane64(so0, jj);
+      const uint64_t L = (uint32_t)__builtin_amdgcn_readlane((int)Ls, jj);
       const Pre nxt = jj + 1 < nb ? issue(jj + 1) : Pre{0u, 0u, 0u};
       if (__builtin_amdgcn_readlane((int)one, jj)) {
         const int64_t first = __builtin_amdgcn_readlane(sf, jj);
         const int64_t last0 = (int64_t)__builtin_amdgcn_readlane(sl, jj) - k + 1;
         const int64_t p_lo = first, p_hi = last0 < first ? first : last0;
-        const uint64_t q0 = readlane64(pk0, jj), q1 = readlane64(pk1, jj);
+        const uint64_t q0 = readlane64(pk0, jj), q1 = q0 + (uint32_t)__builtin_amdgcn_readlane((int)npk, jj);
         const int64_t ngroups = (p_hi - p_lo) / 16 + 1;
         for (int64_t g = lane; g < ngroups; g += 64) {
           const int64_t p0 = p_lo + g * 16;
@@ -387,8 +395,17 @@ __device__ __forceinline__ void kmer_stream8(const KArgs &A, uint32_t *tab, int 
       const bool small = L + (uint64_t)B < 65536;
       uint8_t *row = A.hist + s * A.pitch;
       for (int q = lane; q < B / 4; q += 64) {
-        uint4 c = reinterpret_cast<const uint4 *>(tab)[q];
-        reinterpret_cast<uint4 *>(tab)[q] = make_uint4(0, 0, 0, 0);
+        uint4 c = reinterpret_cast<const uint4 *>(tab0)[q];
+        reinterpret_cast<uint4 *>(tab0)[q] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int u = 1; u < S; u++) {
+          const uint4 d = reinterpret_cast<const uint4 *>(tab0 + (size_t)u * B)[q];
+          reinterpret_cast<uint4 *>(tab0 + (size_t)u * B)[q] = make_uint4(0, 0, 0, 0);
+          c.x += d.x;
+          c.y += d.y;
+          c.z += d.z;
+          c.w += d.w;
+        }
         c.x += 1;  // pseudocount (ClusterFactory.cpp:995)
         c.y += 1;
         c.z += 1;
@@ -413,7 +430,6 @@ __device__ __forceinline__ void kmer_stream8(const KArgs &A, uint32_t *tab, int 
       if (lane == jj) {
         my_m = m64;
         my_sq = sq64;
-        my_len = L;
       }
       tab_drain(false);
     }
@@ -421,7 +437,7 @@ __device__ __forceinline__ void kmer_stream8(const KArgs &A, uint32_t *tab, int 
       const uint64_t s = sb + (uint64_t)lane * stride;
       A.mag[s] = my_m;
       A.sumsq[s] = my_sq;
-      A.len_out[s] = my_len;
+      A.len_out[s] = Ls;
     }
   }
   uint32_t wm = lmax;
@@ -435,7 +451,7 @@ __device__ __forceinline__ void kmer_stream8(const KArgs &A, uint32_t *tab, int 
 // at run time between LDS and global memory makes every table access a FLAT instruction.
 // STREAM: kmer_stream8 alone (a kernel of its own: its register allocation, not the general
 // form's, sets the occupancy).
-template <typename T, bool GLOB, bool STREAM = false>
+template <typename T, bool GLOB, bool STREAM = false, int S = 1>
 __global__ __launch_bounds__(KT) void kmer_kernel(KArgs A, bool write) {
   extern __shared__ __attribute__((aligned(16))) uint32_t ltab[];
   __shared__ uint64_t s_max[KW];
@@ -445,13 +461,13 @@ __global__ __launch_bounds__(KT) void kmer_kernel(KArgs A, bool write) {
   uint32_t *base;  // this workgroup's tables
   if constexpr (GLOB) base = A.gtab + (uint64_t)blockIdx.x * KW * (uint64_t)B;
   else base = ltab;
-  uint32_t *mytab = base + (A.shared ? 0 : (size_t)wv * B);
+  uint32_t *mytab = base + (A.shared ? 0 : (size_t)wv * S * B);
   uint64_t wmax = 0;
   if (!A.shared || wv == 0)
-    for (int b = lane; b < B; b += 64) tab_zero(mytab + b, glob);
+    for (int b = lane; b < S * B; b += 64) tab_zero(mytab + b, glob);
   tab_drain(glob);
   if constexpr (STREAM) {
-    kmer_stream8(A, mytab, B, write, &wmax);
+    kmer_stream8<S>(A, mytab, B, write, &wmax);
   } else if (!A.coop) {
     // one wave per sequence: the wave's own table, no workgroup barrier.  The metadata of the
     // wave's next 64 sequences (offsets, purity, segment bounds) are loaded lane by lane in two
@@ -578,8 +594,14 @@ int launch_kmer(mc_ctx *c, int k, int width, bool write, uint64_t *d_max, int *d
   const bool g = A.gtab != nullptr;
   switch (width) {
     case 1:
-      if (!g && !A.coop && !A.shared && (B & 255) == 0 && A.stream8)
-        kmer_kernel<uint8_t, false, true><<<grid, KT, lds, c->stream>>>(A, write);
+      if (!g && !A.coop && !A.shared && (B & 255) == 0 && A.stream8) {
+        // sub-tables per wave: k = 4 four (16 KiB per workgroup), k = 5 two (32 KiB), else one
+        const int S = k == 4 ? 4 : k == 5 ? 2 : 1;
+        const size_t sl = (size_t)KW * S * B * 4;
+        if (S == 4) kmer_kernel<uint8_t, false, true, 4><<<grid, KT, sl, c->stream>>>(A, write);
+        else if (S == 2) kmer_kernel<uint8_t, false, true, 2><<<grid, KT, sl, c->stream>>>(A, write);
+        else kmer_kernel<uint8_t, false, true, 1><<<grid, KT, sl, c->stream>>>(A, write);
+      }
       else
         (g ? kmer_kernel<uint8_t, true> : kmer_kernel<uint8_t, false>)<<<grid, KT, lds, c->stream>>>(A, write);
       break;

@@ -553,9 +553,38 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
   std::vector<uint32_t> members;
   std::vector<uint64_t> off;
   bool rebuild = true;
+  // Several ranks: the iterations are split over them by centre (centre all-gather) only when
+  // that pays.  Every rank runs the first iteration whole (one device round trip, identical
+  // everywhere); then the ranks exchange its time and the time of one exchange, and split the
+  // remaining iterations if a rank's share of an iteration saves more than the exchange and
+  // the separate merge-pair call cost (MC_SHARD_UPDATE=0/1 forces the choice; MC_SHARD_FORCE,
+  // the one-rank test of the sharded path, splits from the first iteration).
+  int split_update = (multi && !memo) ? -1 : 0;
+  if (split_update < 0 && getenv("MC_SHARD_FORCE")) split_update = 1;
+  if (split_update < 0 && getenv("MC_SHARD_UPDATE")) split_update = atoi(getenv("MC_SHARD_UPDATE")) ? 1 : 0;
+  double t_first = 0;
   for (int it = 0; it < cfg.iterations; it++) {
     bool fused = false;
     uint64_t fused_np = 0;
+    if (split_update < 0 && it == 1) {
+      const auto t0 = std::chrono::steady_clock::now();
+      double probe = 0, got[64];
+      if (cfg.comm->allgather(cfg.comm->user, &probe, 8, got) != 0) throw PeerError("all-gather across ranks failed");
+      const double t_ag = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+      double mine2[2] = {t_first, t_ag}, all2[2 * 64];
+      if (cfg.comm->allgather(cfg.comm->user, mine2, 16, all2) != 0) throw PeerError("all-gather across ranks failed");
+      double it_ms = 0, ag_ms = 0;
+      for (int r = 0; r < cfg.comm->world; r++) {
+        it_ms = std::max(it_ms, all2[2 * r]);
+        ag_ms = std::max(ag_ms, all2[2 * r + 1]);
+      }
+      const double W = (double)cfg.comm->world;
+      split_update = it_ms * (1.0 - 1.0 / W) > 2.0 * ag_ms + 0.1 ? 1 : 0;
+      timer.add("update.decision.iteration_ms", it_ms);
+      timer.add("update.decision.exchange_ms", ag_ms);
+    }
+    if (multi && !memo && it == 0) fault_point(cfg.comm, "update");
+    const auto t_it0 = std::chrono::steady_clock::now();
     // mean_shift_update for every centre, all reading the same state (ClusterFactory.cpp:744-749)
     const uint32_t C = (uint32_t)part.size();
     std::vector<uint32_t> cids(C), newc(C);
@@ -573,7 +602,7 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
       uint32_t e = std::min<uint32_t>(j + cfg.delta, C - 1);
       stats.update_evals += off[e + 1] - off[b];
     }
-    if (C && !memo && multi) {
+    if (C && !memo && multi && split_update == 1) {
       // this rank's share of the centres, then the centre-reassignment all-gather
       const uint32_t W = (uint32_t)cfg.comm->world, per = (C + W - 1) / W;
       const uint32_t j0 = std::min<uint32_t>(C, per * (uint32_t)cfg.comm->rank), j1 = std::min<uint32_t>(C, j0 + per);
@@ -687,7 +716,10 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
     Scope sc(timer, "update.cascade");
     merge_cascade(part, poff, sim, c0);
     rebuild = part.size() != C;
+    if (it == 0) t_first = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_it0).count();
   }
+  if (multi && !memo)
+    stats.update_path = split_update == 1 ? "split x" + std::to_string(cfg.comm->world) : "replicated";
   return part;
 }
 

@@ -49,6 +49,7 @@ struct ClusterStats {
   // which accumulation loop ran: "device" (mc_accumulate, one persistent kernel) or "steps"
   // (host-driven mc_scan per get_close step) with the reason
   std::string accum_path;
+  std::string update_path;  // several ranks: the mean-shift iterations split by centre or replicated
 };
 
 // Runs accumulation + `iterations` rounds of mean-shift update and merge.

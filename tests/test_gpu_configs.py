@@ -248,3 +248,25 @@ def test_config_C20k_align_properties(product):
         out = fa[:-3] + "." + tag + ".clstr"
         _run(fa, flags, out, 600, env)
         assert BG.canonical_digest(_properties(out, gen[0])) == want, tag
+
+
+@pytest.mark.timeout(1200)
+def test_config_C100k_align_properties(product):
+    """Config C at its BASELINE size (100k x 1 kb, 1,000 templates, --id 0.55 --align; the
+    reference would need days on the CPU): every read in exactly one cluster,
+    every centre a member of its cluster, and the same canonical partition whether the
+    window scans' NW batches run in the one-wave throughput form (MC_NW_MW_MAX=0) or in the
+    default mix of throughput and latency forms."""
+    gen = (100000, 1000, 1000, 0.03, 41)
+    fa = os.path.join(_cache_dir(), "C100k.fa")
+    if not os.path.exists(fa):
+        synth.generate(fa + ".tmp", *gen)
+        os.replace(fa + ".tmp", fa)
+    flags = ["--id", "0.55", "--align"]
+    base = fa[:-3] + ".clstr"
+    st = _run(fa, flags, base, 900)
+    assert st["accum_path"] == "steps (alignment mode)" and st["align_nw_pairs"] > 0
+    want = BG.canonical_digest(_properties(base, gen[0]))
+    out = fa[:-3] + ".tp.clstr"
+    _run(fa, flags, out, 900, {"MC_NW_MW_MAX": "0"})
+    assert BG.canonical_digest(_properties(out, gen[0])) == want
