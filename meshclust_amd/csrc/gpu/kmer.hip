@@ -363,11 +363,13 @@ __device__ __forceinline__ void kmer_stream8(const KArgs &A, uint32_t *tab0, int
       const uint64_t q0 = readlane64(pk0, jj);
       return pre_load(A, q0, q0 + (uint32_t)__builtin_amdgcn_readlane((int)npk, jj), first + (int64_t)lane * 16, lane < ng);
     };
+    // two sequences' words in flight ahead of the one being counted
     Pre cur = issue(0);
+    Pre nx1 = nb > 1 ? issue(1) : Pre{0u, 0u, 0u};
     for (int jj = 0; jj < nb; jj++) {
       const uint64_t s = sb + (uint64_t)jj * stride;
       const uint64_t L = (uint32_t)__builtin_amdgcn_readlane((int)Ls, jj);
-      const Pre nxt = jj + 1 < nb ? issue(jj + 1) : Pre{0u, 0u, 0u};
+      const Pre nxt = jj + 2 < nb ? issue(jj + 2) : Pre{0u, 0u, 0u};
       if (__builtin_amdgcn_readlane((int)one, jj)) {
         const int64_t first = __builtin_amdgcn_readlane(sf, jj);
         const int64_t last0 = (int64_t)__builtin_amdgcn_readlane(sl, jj) - k + 1;
@@ -386,7 +388,8 @@ __device__ __forceinline__ void kmer_stream8(const KArgs &A, uint32_t *tab0, int
       } else {
         count_sequence(A, s, tab, 0, 1);
       }
-      cur = nxt;
+      cur = nx1;
+      nx1 = nxt;
       tab_drain(false);
       // the row: bins + pseudocount, written as bytes; magnitude and sum of squares reduced over
       // the wave, the maximum kept per lane
@@ -596,7 +599,9 @@ int launch_kmer(mc_ctx *c, int k, int width, bool write, uint64_t *d_max, int *d
     case 1:
       if (!g && !A.coop && !A.shared && (B & 255) == 0 && A.stream8) {
         // sub-tables per wave: k = 4 four (16 KiB per workgroup), k = 5 two (32 KiB), else one
-        const int S = k == 4 ? 4 : k == 5 ? 2 : 1;
+        // (S > 1 measured slower: 76 vs 68 us at config B, 531 vs 507 us at D1M -- the table
+        // atomics are not what bounds the kernel; MC_KMER_SUB=1 keeps the sub-tables for tests)
+        const int S = getenv("MC_KMER_SUB") ? (k == 4 ? 4 : k == 5 ? 2 : 1) : 1;
         const size_t sl = (size_t)KW * S * B * 4;
         if (S == 4) kmer_kernel<uint8_t, false, true, 4><<<grid, KT, sl, c->stream>>>(A, write);
         else if (S == 2) kmer_kernel<uint8_t, false, true, 2><<<grid, KT, sl, c->stream>>>(A, write);
