@@ -201,7 +201,7 @@ int mc_ctx_destroy(mc_ctx *c) {
                  &c->alive, &c->members, &c->member_keys, &c->partials, &c->scan_dev, &c->flags_out, &c->s_a, &c->s_b,
                  &c->s_c, &c->s_d, &c->s_e, &c->s_f, &c->s_g, &c->s_h, &c->s_i, &c->s_j, &c->s_k, &c->hs, &c->mag_s, &c->sumsq_s, &c->len_s, &c->ticket,
                  &c->msum, &c->ident_s, &c->al_a, &c->al_b, &c->al_out, &c->acc_out, &c->sp_words, &c->sp_keys,
-                 &c->sp_scr, &c->sp_nodes, &c->sp_nn, &c->sp_q, &c->sp_err, &c->u_off, &c->u_mem})
+                 &c->sp_scr, &c->sp_nodes, &c->sp_nn, &c->sp_q, &c->sp_err, &c->u_off, &c->u_mem, &c->nw_items, &c->nw_gran})
     release(*b);
   if (c->h_scan) (void)hipHostFree(c->h_scan);
   if (c->h_stage) (void)hipHostFree(c->h_stage);

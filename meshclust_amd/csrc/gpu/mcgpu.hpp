@@ -157,6 +157,7 @@ struct mc_ctx {
   int part_slot = 0, part_share = 1, part_cus = 0;
   // scratch
   mcg::Buf s_a, s_b, s_c, s_d, s_e, s_f, s_g, s_h, s_i, s_j, s_k;
+  mcg::Buf nw_items, nw_gran;  // NW chained row blocks: work items, bottom-row granules
   // mc_update_iteration's member lists on the device and their host shadow: re-uploaded only
   // when a merge changed them (cleared when sequences are loaded: the ids were checked against n)
   mcg::Buf u_off, u_mem;

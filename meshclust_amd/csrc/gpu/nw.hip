@@ -78,6 +78,15 @@ struct NWPairs {
   int32_t *ids;
   int32_t *score;
   const uint32_t *out;  // optional result slot per pair (else the pair index)
+  // chained row blocks (latency form, CH): one workgroup per (pair, row block); work item i is
+  // pair pidx[i], block pblk[i], items of a pair consecutive in block order; a workgroup takes
+  // the next item from *ctr, so every block's predecessor was dispatched before it
+  const uint16_t *pblk;
+  uint32_t *ctr;
+  uint64_t *cbuf;        // tagged granules: per column j of a block's bottom row, 6 x {j, value}
+  const uint64_t *cin;   // per item: granule offset of the block above's bottom row (~0: none)
+  const uint64_t *cout;  // per item: granule offset of this block's bottom row (~0: last block)
+  int *err;              // a hand-off that never arrived (20 s)
 };
 
 // ---------------------------------------------------------------------------------------
@@ -104,21 +113,32 @@ struct SteadyStep {
 };
 
 
-template <int R, typename P, int W>
-__global__ __launch_bounds__(64 * W) void nw_mw_kernel(NWPairs q) {
+// CH (chained row blocks): the workgroup computes ONE row block of its pair, concurrently with
+// the pair's other blocks in other workgroups.  Wave 0 is a receiver: it polls the block above's
+// bottom row (tagged granules in global memory, written by that block's last wave) one barrier
+// interval ahead and stages it in the LDS ring slot of the first compute wave, which reads it
+// exactly as waves 1.. read the ring of the wave above them.  Waves 1..W compute.
+template <int R, typename P, int W, bool CH = false>
+__global__ __launch_bounds__(64 * (W + (CH ? 1 : 0))) void nw_mw_kernel(NWPairs q) {
   constexpr int SH = Pack<P>::SH;
   constexpr P LEN1 = (P)1 << SH;
   constexpr int ROWS = 64 * R * W;  // rows per block
   __shared__ int rM[RING_C][W], rX[RING_C][W], rY[RING_C][W];
   __shared__ P rMP[RING_C][W], rXP[RING_C][W], rYP[RING_C][W];
-  const uint32_t slot = blockIdx.x;
+  __shared__ uint32_t s_slot;
+  uint32_t slot = blockIdx.x;
+  if constexpr (CH) {
+    if (threadIdx.x == 0) s_slot = atomicAdd(q.ctr, 1u);
+    __syncthreads();
+    slot = s_slot;
+  }
   if (slot >= q.npairs) return;
   const uint32_t p = q.pidx[slot];
   const uint8_t *a = q.A + q.aoff[q.ai[p]];
   const int la = (int)(q.aoff[q.ai[p] + 1] - q.aoff[q.ai[p]]);
   const uint8_t *b = q.Bq + q.boff[q.bi[p]];
   const int lb = (int)(q.boff[q.bi[p] + 1] - q.boff[q.bi[p]]);
-  const int lane = threadIdx.x & 63, w = wave_id(), gl = threadIdx.x;
+  const int lane = threadIdx.x & 63, w = wave_id() - (CH ? 1 : 0), gl = (int)threadIdx.x - (CH ? 64 : 0);
   const int len1 = la + 1, len2 = lb + 1;
   const int shorter = (len2 < len1 ? len2 : len1) - 1;
   const int lenDiff = len2 > len1 ? len2 - len1 : len1 - len2;
@@ -130,7 +150,69 @@ __global__ __launch_bounds__(64 * W) void nw_mw_kernel(NWPairs q) {
   const int nblk = (la + ROWS - 1) / ROWS;
   int fin_score = 0;
   P fin_pay = 0;
-  for (int blk = 0; blk < (nblk > 0 ? nblk : 1); blk++) {
+  const int blk_first = CH ? (int)q.pblk[slot] : 0, blk_end = CH ? blk_first + 1 : (nblk > 0 ? nblk : 1);
+  if constexpr (CH) {
+    if (w < 0) {
+      // ---- receiver wave: the block above's bottom row into ring slot [.][0] --------------
+      const int steps = lb + 63 + (W - 1) * (64 + KLAG);
+      const uint64_t *in = q.cin[slot] == ~0ull ? nullptr : q.cbuf + q.cin[slot];
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      bool failed = false;
+      // columns [c0, c1] into the ring: lane l takes granules 2 (l % 3), +1 of column c0 + l / 3
+      auto stage = [&](int c0, int c1) {
+        if (!in) return;
+        for (int cb = c0; cb <= c1; cb += 21) {
+          const int c = cb + lane / 3, part = lane % 3;
+          const bool act = lane < 63 && c <= c1 && c >= 1 && c <= lb;
+          uint64_t g0 = 0, g1 = 0;
+          for (uint32_t it = 1;; it++) {
+            bool ok = true;
+            if (act) {
+              g0 = __hip_atomic_load(const_cast<uint64_t *>(in + 6 * (uint64_t)c + 2 * part), __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+              g1 = __hip_atomic_load(const_cast<uint64_t *>(in + 6 * (uint64_t)c + 2 * part + 1), __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+              ok = (uint32_t)(g0 >> 32) == (uint32_t)c && (uint32_t)(g1 >> 32) == (uint32_t)c;
+            }
+            if (__ballot(!ok) == 0) break;
+            if (failed || ((it & 255) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > 2000000000ull)) {
+              failed = true;  // (the values are garbage; the launch reports the error)
+              break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+          }
+          if (act) {
+            const int sl = c % RING_C;
+            const uint32_t v0 = (uint32_t)g0, v1 = (uint32_t)g1;
+            if (part == 0) {
+              rM[sl][0] = (int)v0;
+              rX[sl][0] = (int)v1;
+            } else if (part == 1) {
+              rY[sl][0] = (int)v0;
+              rMP[sl][0] = (P)v1;
+            } else {
+              rXP[sl][0] = (P)v0;
+              rYP[sl][0] = (P)v1;
+            }
+          }
+        }
+      };
+      // the first compute wave reads column t + 2 at step t (and column 1 before its first
+      // step): columns 1..17 before the first barrier, then during barrier interval m the
+      // columns of interval m + 1
+      stage(1, 17);
+      __syncthreads();
+      for (int m = 0; m < steps / KLAG; m++) {
+        stage(KLAG * m + 18, KLAG * m + 33);
+        __syncthreads();
+      }
+      __syncthreads();  // (the block's closing barrier)
+      if (failed && lane == 0) atomicOr(q.err, 1);
+      return;
+    }
+    __syncthreads();  // (the receiver's first columns are in the ring)
+  }
+  for (int blk = blk_first; blk < blk_end; blk++) {
     const int itop = blk * ROWS + gl * R + 1;  // first row of this lane
     uint8_t ac[R];
     int M[R], X[R], Y[R];
@@ -173,7 +255,7 @@ __global__ __launch_bounds__(64 * W) void nw_mw_kernel(NWPairs q) {
     P nMP = 0, nXP = 0, nYP = 0;
     auto fetch = [&](int jn) {
       if (lane != 0 || jn < 1 || jn > lb) return;
-      if (w > 0) {
+      if (w > 0 || (CH && blk > 0)) {
         const int sl = jn % RING_C;
         nM = rM[sl][w];
         nX = rX[sl][w];
@@ -247,7 +329,7 @@ __global__ __launch_bounds__(64 * W) void nw_mw_kernel(NWPairs q) {
         uXP = l0 ? hXP : uXP;
         uYP = l0 ? hYP : uYP;
         const int jn = idx + 2;  // lane 0's next column (uniform)
-        if (w > 0) {
+        if (w > 0 || (CH && blk > 0)) {
           const int sl = jn % RING_C;
           nM = rM[sl][w];
           nX = rX[sl][w];
@@ -332,7 +414,16 @@ __global__ __launch_bounds__(64 * W) void nw_mw_kernel(NWPairs q) {
             rMP[sl][w + 1] = oMP;
             rXP[sl][w + 1] = oXP;
             rYP[sl][w + 1] = oYP;
-          } else if (blk + 1 < nblk) {
+          } else if (CH && blk + 1 < nblk) {
+            uint64_t *o = q.cbuf + q.cout[slot] + 6 * (uint64_t)j;
+            const uint64_t tg = (uint64_t)(uint32_t)j << 32;
+            __hip_atomic_store(o + 0, tg | (uint32_t)oM, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(o + 1, tg | (uint32_t)oX, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(o + 2, tg | (uint32_t)oY, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(o + 3, tg | (uint32_t)oMP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(o + 4, tg | (uint32_t)oXP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(o + 5, tg | (uint32_t)oYP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          } else if (!CH && blk + 1 < nblk) {
             int *sb = bnd + 6 * j;
             sb[0] = oM;
             sb[1] = oX;
@@ -351,7 +442,7 @@ __global__ __launch_bounds__(64 * W) void nw_mw_kernel(NWPairs q) {
       } else {
         ob = bc;
       }
-      if (W > 1 && (t % KLAG) == KLAG - 1) __syncthreads();
+      if ((W > 1 || CH) && (t % KLAG) == KLAG - 1) __syncthreads();
     };
     // steady state: lane 63's column >= 1 and lane 0's <= lb, i.e. lagw + 63 <= t < lagw + lb
     const int ts0 = lb >= 64 ? lagw + 63 : steps, ts1 = lb >= 64 ? lagw + lb : steps;
@@ -388,7 +479,7 @@ __global__ __launch_bounds__(64 * W) void nw_mw_kernel(NWPairs q) {
   }
   const int fl = la - (nblk - 1) * ROWS - 1;
   const int owner = la == 0 ? 0 : fl / R;
-  if (gl == owner) {
+  if (gl == owner && (!CH || blk_first == nblk - 1)) {
     int L, I;
     if (la == 0) {
       // no rows (len1 == 1): only cell 0 of each state row exists.  With columns (lb > 0)
@@ -432,6 +523,14 @@ int launch_bucket(mc_ctx *c, NWPairs q) {
   return MC_OK;
 }
 
+template <int R>
+int launch_bucket_ch(mc_ctx *c, NWPairs q) {
+  if (q.npairs == 0) return MC_OK;
+  nw_mw_kernel<R, uint32_t, 4, true><<<q.npairs, 64 * 5, 0, c->stream>>>(q);
+  MCG_CHECK(hipGetLastError());
+  return MC_OK;
+}
+
 template <int R, typename P>
 int launch_bucket_mw(mc_ctx *c, NWPairs q, int waves) {
   if (q.npairs == 0) return MC_OK;
@@ -460,6 +559,13 @@ int launch_nw(mc_ctx *c, const uint8_t *d_A, const uint64_t *d_aoff, const uint3
     return e ? (uint64_t)atoll(e) : (uint64_t)1024;
   }();
   const bool mw = m < mw_max;
+  // chained row blocks (MC_NW_CHAIN=0 turns them off): a latency-form pair longer than one row
+  // block gets a workgroup per block, the blocks running concurrently one pipeline lag apart
+  static const bool chain_on = !getenv("MC_NW_CHAIN") || atoi(getenv("MC_NW_CHAIN")) != 0;
+  std::vector<uint32_t> ch_pair[4];   // per R (1, 2, 4, 8): work items' pairs
+  std::vector<uint16_t> ch_blk[4];
+  std::vector<uint64_t> ch_in[4], ch_out[4];
+  uint64_t ch_gran = 0;               // granules of every chained pair's block bottom rows
   enum { NB = 32 };  // latency form: (R, payload) x waves 2 / 4 / 8 / 16
   int bucket_waves[NB] = {0};
   std::vector<uint32_t> bucket[NB];
@@ -485,6 +591,17 @@ int launch_nw(mc_ctx *c, const uint8_t *d_A, const uint64_t *d_aoff, const uint3
       bk = r + (wide ? 4 : 0) + (wv == 2 ? 24 : wv == 4 ? 0 : wv == 8 ? 8 : 16);
       bucket_waves[bk] = wv;
       rows = w64 << r;
+      if (chain_on && wv == 4 && !wide && la > rows && lb >= 1) {
+        const uint64_t nblk = (la + rows - 1) / rows;
+        for (uint64_t b = 0; b < nblk; b++) {
+          ch_pair[r].push_back((uint32_t)i);
+          ch_blk[r].push_back((uint16_t)b);
+          ch_in[r].push_back(b == 0 ? ~0ull : ch_gran + (b - 1) * 6 * (lb + 1));
+          ch_out[r].push_back(b + 1 == nblk ? ~0ull : ch_gran + b * 6 * (lb + 1));
+        }
+        ch_gran += (nblk - 1) * 6 * (lb + 1);
+        continue;
+      }
     } else {
       r = la <= 256 ? 0 : la <= 512 ? 1 : 2;  // R = 4, 8, 16
       bk = r + (wide ? 3 : 0);
@@ -495,14 +612,53 @@ int launch_nw(mc_ctx *c, const uint8_t *d_A, const uint64_t *d_aoff, const uint3
     if (la > rows) scratch[bk] += 12 * (lb + 1);
   }
   timed_begin(c);
-  uint64_t total_idx = 0, total_scr = 0;
+  uint64_t total_idx = 0, total_scr = 0, total_ch = 0;
   for (int k = 0; k < NB; k++) {
     total_idx += bucket[k].size();
     total_scr += scratch[k];
   }
+  for (int k = 0; k < 4; k++) total_ch += ch_pair[k].size();
   if (ensure(c->s_a, total_idx * 4 + 16) || ensure(c->s_b, total_idx * 8 + 16) ||
       ensure(c->s_c, std::max<uint64_t>(total_scr, 1) * 4))
     return MC_ERR_OOM;
+  if (total_ch) {
+    // items: pair (4 B) | block (2 B, padded) | in, out offsets (8 B each); 4 counters and an
+    // error word; the granule buffer zeroed (no stale tag survives from an earlier launch)
+    const size_t ib = (total_ch * 4 + 255) / 256 * 256, bb = (total_ch * 2 + 255) / 256 * 256,
+                 ob = (total_ch * 8 + 255) / 256 * 256;
+    if (ensure(c->nw_items, ib + bb + 2 * ob + 256) || ensure(c->nw_gran, ch_gran * 8 + 64)) return MC_ERR_OOM;
+    MCG_CHECK(hipMemsetAsync(c->nw_gran.p, 0, ch_gran * 8 + 64, c->stream));
+    char *base = (char *)c->nw_items.p;
+    MCG_CHECK(hipMemsetAsync(base + ib + bb + 2 * ob, 0, 256, c->stream));
+    uint64_t at = 0;
+    int *d_err = (int *)(base + ib + bb + 2 * ob + 32);
+    for (int r = 0; r < 4; r++) {
+      const size_t n = ch_pair[r].size();
+      if (!n) continue;
+      MCG_CHECK(hipMemcpyAsync((uint32_t *)base + at, ch_pair[r].data(), n * 4, hipMemcpyHostToDevice, c->stream));
+      MCG_CHECK(hipMemcpyAsync((uint16_t *)(base + ib) + at, ch_blk[r].data(), n * 2, hipMemcpyHostToDevice, c->stream));
+      MCG_CHECK(hipMemcpyAsync((uint64_t *)(base + ib + bb) + at, ch_in[r].data(), n * 8, hipMemcpyHostToDevice, c->stream));
+      MCG_CHECK(hipMemcpyAsync((uint64_t *)(base + ib + bb + ob) + at, ch_out[r].data(), n * 8, hipMemcpyHostToDevice,
+                               c->stream));
+      NWPairs q{d_A, d_aoff, d_ai, d_B, d_boff, d_bi, (uint32_t *)base + at, (uint32_t)n, nullptr, nullptr,
+                d_ident, d_len, d_ids, d_score, d_out};
+      q.pblk = (const uint16_t *)(base + ib) + at;
+      q.ctr = (uint32_t *)(base + ib + bb + 2 * ob) + r;
+      q.cbuf = (uint64_t *)c->nw_gran.p;
+      q.cin = (const uint64_t *)(base + ib + bb) + at;
+      q.cout = (const uint64_t *)(base + ib + bb + ob) + at;
+      q.err = d_err;
+      int rc = MC_OK;
+      switch (r) {
+        case 0: rc = launch_bucket_ch<1>(c, q); break;
+        case 1: rc = launch_bucket_ch<2>(c, q); break;
+        case 2: rc = launch_bucket_ch<4>(c, q); break;
+        default: rc = launch_bucket_ch<8>(c, q); break;
+      }
+      if (rc) return rc;
+      at += n;
+    }
+  }
   uint64_t io = 0, so = 0;
   for (int k = 0; k < NB; k++) {
     if (bucket[k].empty()) continue;
@@ -541,6 +697,17 @@ int launch_nw(mc_ctx *c, const uint8_t *d_A, const uint64_t *d_aoff, const uint3
   // keep the host vectors alive until the async copies have run
   timed_end(c, F_NW);
   MCG_CHECK(hipStreamSynchronize(c->stream));
+  if (total_ch) {
+    const size_t ib = (total_ch * 4 + 255) / 256 * 256, bb = (total_ch * 2 + 255) / 256 * 256,
+                 ob = (total_ch * 8 + 255) / 256 * 256;
+    int herr = 0;
+    MCG_CHECK(hipMemcpyAsync(&herr, (char *)c->nw_items.p + ib + bb + 2 * ob + 32, 4, hipMemcpyDeviceToHost, c->stream));
+    MCG_CHECK(hipStreamSynchronize(c->stream));
+    if (herr) {
+      set_error("NW chained row blocks: a block's hand-off never arrived");
+      return MC_ERR_TIMEOUT;
+    }
+  }
   return MC_OK;
 }
 
