@@ -562,6 +562,11 @@ int launch_nw(mc_ctx *c, const uint8_t *d_A, const uint64_t *d_aoff, const uint3
   // chained row blocks (MC_NW_CHAIN=0 turns them off): a latency-form pair longer than one row
   // block gets a workgroup per block, the blocks running concurrently one pipeline lag apart
   static const bool chain_on = !getenv("MC_NW_CHAIN") || atoi(getenv("MC_NW_CHAIN")) != 0;
+  static const int chain_r = [] {  // index of R in (1, 2, 4, 8)
+    const char *e = getenv("MC_NW_CHAIN_R");
+    const int v = e ? atoi(e) : 4;
+    return v == 1 ? 0 : v == 2 ? 1 : v == 8 ? 3 : 2;
+  }();
   std::vector<uint32_t> ch_pair[4];   // per R (1, 2, 4, 8): work items' pairs
   std::vector<uint16_t> ch_blk[4];
   std::vector<uint64_t> ch_in[4], ch_out[4];
@@ -592,12 +597,16 @@ int launch_nw(mc_ctx *c, const uint8_t *d_A, const uint64_t *d_aoff, const uint3
       bucket_waves[bk] = wv;
       rows = w64 << r;
       if (chain_on && wv == 4 && !wide && la > rows && lb >= 1) {
-        const uint64_t nblk = (la + rows - 1) / rows;
+        // (blocks of R = 4 rows per lane, MC_NW_CHAIN_R = 1 / 2 / 4 / 8: short enough blocks that
+        // enough workgroups are resident to keep every SIMD issuing -- at R = 8 the 139-register
+        // kernel fits two per CU, which was slower than the sequential blocks)
+        const int rc = chain_r;
+        const uint64_t rows_c = 256ull << rc, nblk = (la + rows_c - 1) / rows_c;
         for (uint64_t b = 0; b < nblk; b++) {
-          ch_pair[r].push_back((uint32_t)i);
-          ch_blk[r].push_back((uint16_t)b);
-          ch_in[r].push_back(b == 0 ? ~0ull : ch_gran + (b - 1) * 6 * (lb + 1));
-          ch_out[r].push_back(b + 1 == nblk ? ~0ull : ch_gran + b * 6 * (lb + 1));
+          ch_pair[rc].push_back((uint32_t)i);
+          ch_blk[rc].push_back((uint16_t)b);
+          ch_in[rc].push_back(b == 0 ? ~0ull : ch_gran + (b - 1) * 6 * (lb + 1));
+          ch_out[rc].push_back(b + 1 == nblk ? ~0ull : ch_gran + b * 6 * (lb + 1));
         }
         ch_gran += (nblk - 1) * 6 * (lb + 1);
         continue;

@@ -269,12 +269,18 @@ __device__ int64_t partition_wg(FP f, int64_t n, PT *L, PT *R, uint32_t *s32, ui
   return lk1 < rK ? lk1 : rK;
 }
 
+// The array's tree of partitioned ranges is mirrored in LDS (its first NCACHE nodes): a query's
+// walk down the levels earlier calls have partitioned reads one LDS node per level instead of
+// a global one (a dependent memory round trip per level, ~17 levels per query at n = 100k).
+constexpr int NCACHE = 512;
+
 __global__ __launch_bounds__(ST) void select_kernel(SelArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint64_t s_dyn[];
   __shared__ uint32_t s32[2 * SW];
   __shared__ uint64_t s64[2];
   __shared__ SplitNode s_nd;
   __shared__ int32_t s_nn, s_idx;
+  __shared__ SplitNode s_cache[NCACHE];
   uint64_t *LW = s_dyn;                                       // LMAX words
   uint16_t *LL = reinterpret_cast<uint16_t *>(s_dyn + LMAX);  // LMAX + LMAX stopper positions
   uint16_t *LR = LL + LMAX;
@@ -287,10 +293,19 @@ __global__ __launch_bounds__(ST) void select_kernel(SelArgs a) {
     s_nn = a.nnodes[arr];
     if (s_nn == 0) {  // the root: the whole array
       nd[0] = SplitNode{0, (int64_t)a.n, 0, a.depth0, -1, 0, 0};
+      s_cache[0] = nd[0];
       s_nn = 1;
     }
   }
   __syncthreads();
+  {
+    const int32_t nc = s_nn < NCACHE ? s_nn : NCACHE;
+    for (int32_t i = t; i < nc; i += ST)
+      if (i > 0 || a.nnodes[arr] != 0) s_cache[i] = nd[i];
+  }
+  __syncthreads();
+  // node i (thread 0): from the LDS mirror when cached
+  auto node = [&](int32_t i) -> SplitNode { return i < NCACHE ? s_cache[i] : nd[i]; };
   for (uint64_t q = a.qoff[blockIdx.x]; q < a.qoff[blockIdx.x + 1]; q++) {
     const int64_t pos = (int64_t)a.qpos[q];
     int32_t idx = 0;
@@ -304,7 +319,7 @@ __global__ __launch_bounds__(ST) void select_kernel(SelArgs a) {
         tm = u;
       }
     };
-    if (t == 0) s_nd = nd[0];
+    if (t == 0) s_nd = node(0);
     __syncthreads();
     mark(0);
     for (;;) {
@@ -316,7 +331,7 @@ __global__ __launch_bounds__(ST) void select_kernel(SelArgs a) {
       }
       if (x.left >= 0) {  // (never in LDS: the nodes visited there are fresh)
         idx = pos < x.cut ? x.left : x.left + 1;
-        if (t == 0) s_nd = nd[idx];
+        if (t == 0) s_nd = node(idx);
         __syncthreads();
         mark(0);
         continue;
@@ -342,6 +357,7 @@ __global__ __launch_bounds__(ST) void select_kernel(SelArgs a) {
             else heap_sort_1(fg, n);
           }
           nd[idx].fin = 1;
+          if (idx < NCACHE) s_cache[idx].fin = 1;
           s_nd.fin = 1;
         }
         __syncthreads();
@@ -354,6 +370,7 @@ __global__ __launch_bounds__(ST) void select_kernel(SelArgs a) {
         if (s_nn + 2 > a.maxnode) {
           atomicMax(a.err, 1);
           nd[idx].fin = 1;  // (ends this query's walk; the call reports the error)
+          if (idx < NCACHE) s_cache[idx].fin = 1;
           s_nd.fin = 1;
           s_idx = idx;
         } else {
@@ -362,6 +379,12 @@ __global__ __launch_bounds__(ST) void select_kernel(SelArgs a) {
           nd[s_nn + 1] = rc;
           nd[idx].left = s_nn;
           nd[idx].cut = cut;
+          if (s_nn < NCACHE) s_cache[s_nn] = lc;
+          if (s_nn + 1 < NCACHE) s_cache[s_nn + 1] = rc;
+          if (idx < NCACHE) {
+            s_cache[idx].left = s_nn;
+            s_cache[idx].cut = cut;
+          }
           s_idx = pos < cut ? s_nn : s_nn + 1;
           s_nd = pos < cut ? lc : rc;
           s_nn += 2;
