@@ -114,6 +114,7 @@ struct SelArgs {
   uint64_t *qout;        // the word std::sort puts at each queried position
   int *err;
   unsigned long long *prof;  // MC_SPLIT_PROFILE: thread 0's realtime ticks per phase (8 counters)
+  int nowave;                // MC_SPLIT_NO_WAVE: every LDS partition by the whole workgroup
 };
 
 // Workgroup-wide exclusive scan of two counters (every thread gets its offsets and the totals).
@@ -274,6 +275,72 @@ __device__ int64_t partition_wg(FP f, int64_t n, PT *L, PT *R, uint32_t *s32, ui
 // a global one (a dependent memory round trip per level, ~17 levels per query at n = 100k).
 constexpr int NCACHE = 512;
 
+// partition_wg's algorithm by wave 0 alone, for an LDS range of at most WMAX words (the lower
+// levels of every query's walk): a lane takes ceil(n / 64) consecutive positions, the stopper
+// offsets are a wave scan, K a 64-probe bisection by ballot, the swaps 64 at a time -- no
+// workgroup barrier inside (LDS operations of one wave are performed in order).  Returns the
+// cut in every lane.  (The same stoppers, K, swaps and cut as partition_wg: the swaps are
+// disjoint, so their order does not matter.)
+constexpr int64_t WMAX = 2048;
+__device__ int64_t partition_wave(SP_LDS uint64_t *f, int64_t n, SP_LDS uint16_t *L, SP_LDS uint16_t *R) {
+  const int lane = threadIdx.x & 63;
+  if (lane == 0) {  // std::__move_median_to_first(first, first + 1, mid, last - 1)
+    const uint64_t a = f[1], b = f[n / 2], c = f[n - 1];
+    int64_t m;
+    if (kless(a, b)) m = kless(b, c) ? n / 2 : kless(a, c) ? n - 1 : 1;
+    else m = kless(a, c) ? 1 : kless(b, c) ? n - 1 : n / 2;
+    const uint64_t x = f[0];
+    f[0] = f[m];
+    f[m] = x;
+  }
+  const uint64_t pk = f[0] >> 32;
+  const int64_t S = (n + 63) / 64;
+  const int64_t i0 = (int64_t)lane * S < n ? (int64_t)lane * S : n, i1 = i0 + S < n ? i0 + S : n;
+  uint32_t cg = 0, cl = 0;
+  for (int64_t i = i0; i < i1; i++) {
+    const uint64_t k = f[i] >> 32;
+    cg += (i >= 1 && k >= pk) ? 1u : 0u;
+    cl += k <= pk ? 1u : 0u;
+  }
+  uint32_t ig = cg, il = cl;  // inclusive wave scans
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t ug = (uint32_t)__shfl_up((int)ig, o, 64), ul = (uint32_t)__shfl_up((int)il, o, 64);
+    if (lane >= o) {
+      ig += ug;
+      il += ul;
+    }
+  }
+  const uint32_t CL = (uint32_t)__builtin_amdgcn_readlane((int)ig, 63), TL = (uint32_t)__builtin_amdgcn_readlane((int)il, 63);
+  uint32_t og = ig - cg, ol = il - cl;
+  for (int64_t i = i0; i < i1; i++) {
+    const uint64_t k = f[i] >> 32;
+    if (i >= 1 && k >= pk) L[og++] = (uint16_t)i;
+    if (k <= pk) R[ol++] = (uint16_t)i;
+  }
+  // K = the last k with L[k - 1] < R[TL - k]: bracket (lo, hi), 64 probes per round
+  const int64_t m = CL < TL ? CL : TL;
+  int64_t lo = 0, hi = m + 1;
+  while (hi - lo > 1) {
+    const int64_t span = hi - lo;
+    const int64_t k = lo + 1 + ((span - 1) * (int64_t)lane) / 64;  // in (lo, hi), nondecreasing in lane
+    const bool pr = L[k - 1] < R[TL - k];
+    const int c = (int)__popcll(__ballot(pr));  // the true probes are lanes 0 .. c - 1
+    const int64_t nlo = c > 0 ? (int64_t)__builtin_amdgcn_readlane((int)k, c - 1) : lo;
+    const int64_t nhi = c < 64 ? (int64_t)__builtin_amdgcn_readlane((int)k, c) : hi;
+    lo = nlo;
+    hi = nhi;
+  }
+  const int64_t K = lo;
+  for (int64_t k = 1 + lane; k <= K; k += 64) {
+    const uint32_t pa = L[k - 1], pb = R[TL - k];
+    const uint64_t x = f[pa], y = f[pb];
+    f[pa] = y;
+    f[pb] = x;
+  }
+  const int64_t lk1 = K < (int64_t)CL ? (int64_t)L[K] : n, rK = K >= 1 ? (int64_t)R[TL - K] : n;
+  return lk1 < rK ? lk1 : rK;
+}
+
 __global__ __launch_bounds__(ST) void select_kernel(SelArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint64_t s_dyn[];
   __shared__ uint32_t s32[2 * SW];
@@ -364,8 +431,19 @@ __global__ __launch_bounds__(ST) void select_kernel(SelArgs a) {
         mark(2);
         continue;
       }
-      const int64_t cut = x.lo + (in_lds ? partition_wg<uint16_t>(fl, n, LL, LR, s32, s64)
-                                         : partition_wg<uint32_t>(fg, n, L + x.lo, R + x.lo, s32, s64));
+      int64_t cut;
+      if (in_lds && n <= WMAX && !a.nowave) {
+        if (t < 64) {
+          const int64_t c = partition_wave(fl, n, (SP_LDS uint16_t *)LL, (SP_LDS uint16_t *)LR);
+          if (t == 0) s64[0] = (uint64_t)c;
+        }
+        __syncthreads();
+        cut = x.lo + (int64_t)s64[0];
+        __syncthreads();  // (s64 is partition_wg's scratch too)
+      } else {
+        cut = x.lo + (in_lds ? partition_wg<uint16_t>(fl, n, LL, LR, s32, s64)
+                             : partition_wg<uint32_t>(fg, n, L + x.lo, R + x.lo, s32, s64));
+      }
       if (t == 0) {
         if (s_nn + 2 > a.maxnode) {
           atomicMax(a.err, 1);
@@ -447,6 +525,7 @@ int launch_select(mc_ctx *c, uint64_t *d_words, uint64_t n, uint32_t *d_scr, Spl
   a.qout = d_qout;
   a.err = d_err;
   a.prof = prof ? d_prof : nullptr;
+  a.nowave = getenv("MC_SPLIT_NO_WAVE") ? 1 : 0;
   MCG_CHECK(hipFuncSetAttribute(reinterpret_cast<const void *>(&select_kernel),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)SEL_LDS));
   select_kernel<<<ngroups, ST, SEL_LDS, c->stream>>>(a);
