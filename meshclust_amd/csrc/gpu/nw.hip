@@ -161,6 +161,25 @@ __global__ __launch_bounds__(64 * (W + (CH ? 1 : 0))) void nw_mw_kernel(NWPairs 
       // columns [c0, c1] into the ring: lane l takes granules 2 (l % 3), +1 of column c0 + l / 3
       auto stage = [&](int c0, int c1) {
         if (!in) return;
+        // wait on ONE granule first -- the last column's last granule (the block above writes
+        // its columns in order) -- one lane, a long sleep between polls: a whole wave sweeping
+        // every granule of the interval while the block above is still far behind was enough
+        // polling traffic, over a thousand resident workgroups, to slow every block down
+        const int cl = c1 < lb ? c1 : lb;
+        if (cl >= (c0 > 1 ? c0 : 1)) {
+          for (uint32_t it = 1;; it++) {
+            uint64_t g = 0;
+            if (lane == 0)
+              g = __hip_atomic_load(const_cast<uint64_t *>(in + 6 * (uint64_t)cl + 5), __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT);
+            if ((uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(g >> 32), 0) == (uint32_t)cl) break;
+            if (failed || ((it & 63) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > 2000000000ull)) {
+              failed = true;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(16);
+          }
+        }
         for (int cb = c0; cb <= c1; cb += 21) {
           const int c = cb + lane / 3, part = lane % 3;
           const bool act = lane < 63 && c <= c1 && c >= 1 && c <= lb;
