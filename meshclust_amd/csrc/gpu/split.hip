@@ -276,8 +276,8 @@ __device__ int64_t partition_wg(FP f, int64_t n, PT *L, PT *R, uint32_t *s32, ui
 constexpr int NCACHE = 512;
 
 // partition_wg's algorithm by wave 0 alone, for an LDS range of at most WMAX words (the lower
-// levels of every query's walk): a lane takes ceil(n / 64) consecutive positions, the stopper
-// offsets are a wave scan, K a 64-probe bisection by ballot, the swaps 64 at a time -- no
+// levels of every query's walk): the stoppers are compacted 64 positions per ballot, K is a
+// 64-probe bisection by ballot, the swaps go 64 at a time -- no
 // workgroup barrier inside (LDS operations of one wave are performed in order).  Returns the
 // cut in every lane.  (The same stoppers, K, swaps and cut as partition_wg: the swaps are
 // disjoint, so their order does not matter.)
@@ -294,28 +294,27 @@ __device__ int64_t partition_wave(SP_LDS uint64_t *f, int64_t n, SP_LDS uint16_t
     f[m] = x;
   }
   const uint64_t pk = f[0] >> 32;
-  const int64_t S = (n + 63) / 64;
-  const int64_t i0 = (int64_t)lane * S < n ? (int64_t)lane * S : n, i1 = i0 + S < n ? i0 + S : n;
-  uint32_t cg = 0, cl = 0;
-  for (int64_t i = i0; i < i1; i++) {
-    const uint64_t k = f[i] >> 32;
-    cg += (i >= 1 && k >= pk) ? 1u : 0u;
-    cl += k <= pk ? 1u : 0u;
-  }
-  uint32_t ig = cg, il = cl;  // inclusive wave scans
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t ug = (uint32_t)__shfl_up((int)ig, o, 64), ul = (uint32_t)__shfl_up((int)il, o, 64);
-    if (lane >= o) {
-      ig += ug;
-      il += ul;
+  // the stoppers in position order: 64 consecutive positions per ballot (a lane each), four
+  // such groups' LDS reads in flight
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;  // lanes below this one
+  uint32_t CL = 0, TL = 0;
+  for (int64_t c0 = 0; c0 < n; c0 += 256) {
+    uint64_t kk[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int64_t i = c0 + u * 64 + lane;
+      kk[u] = i < n ? f[i] >> 32 : 0;
     }
-  }
-  const uint32_t CL = (uint32_t)__builtin_amdgcn_readlane((int)ig, 63), TL = (uint32_t)__builtin_amdgcn_readlane((int)il, 63);
-  uint32_t og = ig - cg, ol = il - cl;
-  for (int64_t i = i0; i < i1; i++) {
-    const uint64_t k = f[i] >> 32;
-    if (i >= 1 && k >= pk) L[og++] = (uint16_t)i;
-    if (k <= pk) R[ol++] = (uint16_t)i;
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int64_t i = c0 + u * 64 + lane;
+      const bool gl = i < n && i >= 1 && kk[u] >= pk, gr = i < n && kk[u] <= pk;
+      const uint64_t bl = __ballot(gl), br = __ballot(gr);
+      if (gl) L[CL + (uint32_t)__popcll(bl & lt)] = (uint16_t)i;
+      if (gr) R[TL + (uint32_t)__popcll(br & lt)] = (uint16_t)i;
+      CL += (uint32_t)__popcll(bl);
+      TL += (uint32_t)__popcll(br);
+    }
   }
   // K = the last k with L[k - 1] < R[TL - k]: bracket (lo, hi), 64 probes per round
   const int64_t m = CL < TL ? CL : TL;
@@ -371,8 +370,6 @@ __global__ __launch_bounds__(ST) void select_kernel(SelArgs a) {
       if (i > 0 || a.nnodes[arr] != 0) s_cache[i] = nd[i];
   }
   __syncthreads();
-  // node i (thread 0): from the LDS mirror when cached
-  auto node = [&](int32_t i) -> SplitNode { return i < NCACHE ? s_cache[i] : nd[i]; };
   for (uint64_t q = a.qoff[blockIdx.x]; q < a.qoff[blockIdx.x + 1]; q++) {
     const int64_t pos = (int64_t)a.qpos[q];
     int32_t idx = 0;
@@ -386,20 +383,27 @@ __global__ __launch_bounds__(ST) void select_kernel(SelArgs a) {
         tm = u;
       }
     };
-    if (t == 0) s_nd = node(0);
-    __syncthreads();
+    // node i in every thread: a cached node straight from the LDS mirror (a uniform read, no
+    // barrier: every mirrored node was written before a barrier all threads have passed), any
+    // other through thread 0 -- so the levels earlier calls partitioned cost no barrier at all
+    auto fetch_node = [&](int32_t i) -> SplitNode {
+      if (i < NCACHE) return s_cache[i];
+      if (t == 0) s_nd = nd[i];
+      __syncthreads();
+      const SplitNode r = s_nd;
+      __syncthreads();
+      return r;
+    };
+    SplitNode x = fetch_node(0);
     mark(0);
     for (;;) {
-      const SplitNode x = s_nd;
-      __syncthreads();  // (s_nd is rewritten below)
       if (x.fin) {
         if (t == 0) a.qout[q] = in_lds ? ((SP_LDS uint64_t *)LW)[pos - lbase] : W[pos];
         break;
       }
       if (x.left >= 0) {  // (never in LDS: the nodes visited there are fresh)
         idx = pos < x.cut ? x.left : x.left + 1;
-        if (t == 0) s_nd = node(idx);
-        __syncthreads();
+        x = fetch_node(idx);
         mark(0);
         continue;
       }
@@ -425,9 +429,9 @@ __global__ __launch_bounds__(ST) void select_kernel(SelArgs a) {
           }
           nd[idx].fin = 1;
           if (idx < NCACHE) s_cache[idx].fin = 1;
-          s_nd.fin = 1;
         }
         __syncthreads();
+        x.fin = 1;
         mark(2);
         continue;
       }
@@ -470,6 +474,8 @@ __global__ __launch_bounds__(ST) void select_kernel(SelArgs a) {
       }
       __syncthreads();
       idx = s_idx;
+      x = s_nd;
+      __syncthreads();  // (s_nd is rewritten by the next uncached fetch or partition)
       mark(in_lds ? 4 : 3);
       if (a.prof && t == 0) atomicAdd(&a.prof[in_lds ? 7 : 6], 1ull);
     }
