@@ -427,10 +427,15 @@ __global__ __launch_bounds__(ST) void select_kernel(SelArgs a) {
             if (n <= 16) insertion_sort_1(fg, n);
             else heap_sort_1(fg, n);
           }
+        }
+        // the node is marked finished only after the barrier: a wave still reading this node
+        // from the mirror (no barrier on that read) must see it unfinished, or it would leave
+        // the walk and skip this barrier
+        __syncthreads();
+        if (t == 0) {
           nd[idx].fin = 1;
           if (idx < NCACHE) s_cache[idx].fin = 1;
         }
-        __syncthreads();
         x.fin = 1;
         mark(2);
         continue;
