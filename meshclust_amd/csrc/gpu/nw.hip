@@ -78,12 +78,13 @@ struct NWPairs {
   int32_t *ids;
   int32_t *score;
   const uint32_t *out;  // optional result slot per pair (else the pair index)
-  // chained row blocks (latency form, CH): one workgroup per (pair, row block); work item i is
+  // chained row blocks (CH): one single-wave workgroup per (pair, row block); work item i is
   // pair pidx[i], block pblk[i], items of a pair consecutive in block order; a workgroup takes
   // the next item from *ctr, so every block's predecessor was dispatched before it
   const uint16_t *pblk;
   uint32_t *ctr;
-  uint64_t *cbuf;        // tagged granules: per column j of a block's bottom row, 6 x {j, value}
+  uint64_t *cbuf;        // tagged granules: column j of a block's bottom row at 6 j .. 6 j + 5,
+                         // {j << 32 | value} for M, X, Y and their payloads
   const uint64_t *cin;   // per item: granule offset of the block above's bottom row (~0: none)
   const uint64_t *cout;  // per item: granule offset of this block's bottom row (~0: last block)
   int *err;              // a hand-off that never arrived (20 s)
@@ -113,24 +114,28 @@ struct SteadyStep {
 };
 
 
-// CH (chained row blocks): the workgroup computes ONE row block of its pair, concurrently with
-// the pair's other blocks in other workgroups.  Wave 0 is a receiver: it polls the block above's
-// bottom row (tagged granules in global memory, written by that block's last wave) one barrier
-// interval ahead and stages it in the LDS ring slot of the first compute wave, which reads it
-// exactly as waves 1.. read the ring of the wave above them.  Waves 1..W compute.
+// CH (chained row blocks): a single-wave workgroup computes ONE row block of its pair (64 R
+// rows), concurrently with the pair's other blocks in other workgroups.  The block above's
+// bottom row arrives as tagged granules in global memory, 64 columns per batch: lane l loads
+// column 64 m + 1 + l of batch m one batch ahead, checks the tags when the batch comes due
+// (spinning only if the block above is behind) and lane 0 takes column t + 1 at step t with a
+// readlane -- where the seq2 codes come from too -- so the hand-in costs no LDS, no barrier and
+// no per-step load.  Lane 63 leaves this block's bottom row in LDS, a column per step; every
+// 64 columns the wave stores them as granules, a column per lane.
 template <int R, typename P, int W, bool CH = false>
-__global__ __launch_bounds__(64 * (W + (CH ? 1 : 0))) void nw_mw_kernel(NWPairs q) {
+__global__ __launch_bounds__(64 * W) void nw_mw_kernel(NWPairs q) {
+  static_assert(!CH || (W == 1 && sizeof(P) == 4), "chained blocks: one wave, 32-bit payloads");
   constexpr int SH = Pack<P>::SH;
   constexpr P LEN1 = (P)1 << SH;
   constexpr int ROWS = 64 * R * W;  // rows per block
   __shared__ int rM[RING_C][W], rX[RING_C][W], rY[RING_C][W];
   __shared__ P rMP[RING_C][W], rXP[RING_C][W], rYP[RING_C][W];
-  __shared__ uint32_t s_slot;
+  __shared__ int s_out[CH ? 6 : 1][64];  // CH: this block's bottom row, the current 64 columns
   uint32_t slot = blockIdx.x;
   if constexpr (CH) {
-    if (threadIdx.x == 0) s_slot = atomicAdd(q.ctr, 1u);
-    __syncthreads();
-    slot = s_slot;
+    uint32_t v = 0;
+    if (threadIdx.x == 0) v = atomicAdd(q.ctr, 1u);
+    slot = (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
   }
   if (slot >= q.npairs) return;
   const uint32_t p = q.pidx[slot];
@@ -138,7 +143,7 @@ __global__ __launch_bounds__(64 * (W + (CH ? 1 : 0))) void nw_mw_kernel(NWPairs 
   const int la = (int)(q.aoff[q.ai[p] + 1] - q.aoff[q.ai[p]]);
   const uint8_t *b = q.Bq + q.boff[q.bi[p]];
   const int lb = (int)(q.boff[q.bi[p] + 1] - q.boff[q.bi[p]]);
-  const int lane = threadIdx.x & 63, w = wave_id() - (CH ? 1 : 0), gl = (int)threadIdx.x - (CH ? 64 : 0);
+  const int lane = threadIdx.x & 63, w = wave_id(), gl = (int)threadIdx.x;
   const int len1 = la + 1, len2 = lb + 1;
   const int shorter = (len2 < len1 ? len2 : len1) - 1;
   const int lenDiff = len2 > len1 ? len2 - len1 : len1 - len2;
@@ -151,86 +156,6 @@ __global__ __launch_bounds__(64 * (W + (CH ? 1 : 0))) void nw_mw_kernel(NWPairs 
   int fin_score = 0;
   P fin_pay = 0;
   const int blk_first = CH ? (int)q.pblk[slot] : 0, blk_end = CH ? blk_first + 1 : (nblk > 0 ? nblk : 1);
-  if constexpr (CH) {
-    if (w < 0) {
-      // ---- receiver wave: the block above's bottom row into ring slot [.][0] --------------
-      const int steps = lb + 63 + (W - 1) * (64 + KLAG);
-      const uint64_t *in = q.cin[slot] == ~0ull ? nullptr : q.cbuf + q.cin[slot];
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      bool failed = false;
-      // columns [c0, c1] into the ring: lane l takes granules 2 (l % 3), +1 of column c0 + l / 3
-      auto stage = [&](int c0, int c1) {
-        if (!in) return;
-        // wait on ONE granule first -- the last column's last granule (the block above writes
-        // its columns in order) -- one lane, a long sleep between polls: a whole wave sweeping
-        // every granule of the interval while the block above is still far behind was enough
-        // polling traffic, over a thousand resident workgroups, to slow every block down
-        const int cl = c1 < lb ? c1 : lb;
-        if (cl >= (c0 > 1 ? c0 : 1)) {
-          for (uint32_t it = 1;; it++) {
-            uint64_t g = 0;
-            if (lane == 0)
-              g = __hip_atomic_load(const_cast<uint64_t *>(in + 6 * (uint64_t)cl + 5), __ATOMIC_RELAXED,
-                                    __HIP_MEMORY_SCOPE_AGENT);
-            if ((uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(g >> 32), 0) == (uint32_t)cl) break;
-            if (failed || ((it & 63) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > 2000000000ull)) {
-              failed = true;
-              break;
-            }
-            __builtin_amdgcn_s_sleep(16);
-          }
-        }
-        for (int cb = c0; cb <= c1; cb += 21) {
-          const int c = cb + lane / 3, part = lane % 3;
-          const bool act = lane < 63 && c <= c1 && c >= 1 && c <= lb;
-          uint64_t g0 = 0, g1 = 0;
-          for (uint32_t it = 1;; it++) {
-            bool ok = true;
-            if (act) {
-              g0 = __hip_atomic_load(const_cast<uint64_t *>(in + 6 * (uint64_t)c + 2 * part), __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_AGENT);
-              g1 = __hip_atomic_load(const_cast<uint64_t *>(in + 6 * (uint64_t)c + 2 * part + 1), __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_AGENT);
-              ok = (uint32_t)(g0 >> 32) == (uint32_t)c && (uint32_t)(g1 >> 32) == (uint32_t)c;
-            }
-            if (__ballot(!ok) == 0) break;
-            if (failed || ((it & 255) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > 2000000000ull)) {
-              failed = true;  // (the values are garbage; the launch reports the error)
-              break;
-            }
-            __builtin_amdgcn_s_sleep(2);
-          }
-          if (act) {
-            const int sl = c % RING_C;
-            const uint32_t v0 = (uint32_t)g0, v1 = (uint32_t)g1;
-            if (part == 0) {
-              rM[sl][0] = (int)v0;
-              rX[sl][0] = (int)v1;
-            } else if (part == 1) {
-              rY[sl][0] = (int)v0;
-              rMP[sl][0] = (P)v1;
-            } else {
-              rXP[sl][0] = (P)v0;
-              rYP[sl][0] = (P)v1;
-            }
-          }
-        }
-      };
-      // the first compute wave reads column t + 2 at step t (and column 1 before its first
-      // step): columns 1..17 before the first barrier, then during barrier interval m the
-      // columns of interval m + 1
-      stage(1, 17);
-      __syncthreads();
-      for (int m = 0; m < steps / KLAG; m++) {
-        stage(KLAG * m + 18, KLAG * m + 33);
-        __syncthreads();
-      }
-      __syncthreads();  // (the block's closing barrier)
-      if (failed && lane == 0) atomicOr(q.err, 1);
-      return;
-    }
-    __syncthreads();  // (the receiver's first columns are in the ring)
-  }
   for (int blk = blk_first; blk < blk_end; blk++) {
     const int itop = blk * ROWS + gl * R + 1;  // first row of this lane
     uint8_t ac[R];
@@ -273,8 +198,8 @@ __global__ __launch_bounds__(64 * (W + (CH ? 1 : 0))) void nw_mw_kernel(NWPairs 
     int nM = NINF, nX = NINF, nY = NINF;
     P nMP = 0, nXP = 0, nYP = 0;
     auto fetch = [&](int jn) {
-      if (lane != 0 || jn < 1 || jn > lb) return;
-      if (w > 0 || (CH && blk > 0)) {
+      if (CH || lane != 0 || jn < 1 || jn > lb) return;
+      if (w > 0) {
         const int sl = jn % RING_C;
         nM = rM[sl][w];
         nX = rX[sl][w];
@@ -299,6 +224,55 @@ __global__ __launch_bounds__(64 * (W + (CH ? 1 : 0))) void nw_mw_kernel(NWPairs 
       }
     };
     fetch(1 - lagw);
+    // CH: the block above's bottom row in batches of 64 columns (see the kernel's comment):
+    // hv = the current batch's values (lane l: column 64 m + 1 + l), gn = the next batch's
+    // granules in flight
+    const uint64_t *cin = nullptr;
+    // (this block's bottom row out: the pointer formed once -- read from q inside the loop, the
+    // atomic stores beside it, which may alias q's arrays, would make it a global load per step)
+    uint64_t *cout = nullptr;
+    uint32_t hv[6] = {0, 0, 0, 0, 0, 0};
+    uint64_t gn[6] = {0, 0, 0, 0, 0, 0};
+    bool failed = false;
+    uint64_t t0 = 0;
+    auto gload = [&](int c) {
+#pragma unroll
+      for (int v = 0; v < 6; v++)
+        gn[v] = __hip_atomic_load(const_cast<uint64_t *>(cin + 6 * (uint64_t)c + v), __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
+    };
+    if constexpr (CH) {
+      if (q.cout[slot] != ~0ull) cout = q.cbuf + q.cout[slot];
+      if (q.cin[slot] != ~0ull) {
+        cin = q.cbuf + q.cin[slot];
+        t0 = __builtin_amdgcn_s_memrealtime();
+        if (1 + lane <= lb) gload(1 + lane);
+      }
+    }
+    // batch m comes due at step 64 m: its tags checked (a lane whose column the block above has
+    // not written yet reloads it, a short sleep between tries; 20 s without it: the launch's
+    // error word, garbage values), then batch m + 1's loads issued
+    auto take_batch = [&](int idx) {
+      const int c = idx + 1 + lane;
+      const bool need = c <= lb;
+      for (uint32_t it = 1;; it++) {
+        bool ok = true;
+#pragma unroll
+        for (int v = 0; v < 6; v++) ok = ok && (uint32_t)(gn[v] >> 32) == (uint32_t)c;
+        ok = ok || !need;
+        if (__ballot(!ok) == 0) break;
+        if (failed || ((it & 255) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > 2000000000ull)) {
+          if (!failed && lane == 0) atomicOr(q.err, 1);
+          failed = true;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+        if (!ok) gload(c);
+      }
+#pragma unroll
+      for (int v = 0; v < 6; v++) hv[v] = (uint32_t)gn[v];
+      if (c + 64 <= lb) gload(c + 64);
+    };
     const bool row0 = w == 0 && blk == 0;  // lane 0's upper neighbour is GlobAlignE's row 0
     // One step of this wave.  GEN: the general form (ramp-up / ramp-down: lanes outside
     // 1 <= j <= lb idle).  Steady state (every lane inside, lb >= 64): no per-lane branches --
@@ -313,6 +287,17 @@ __global__ __launch_bounds__(64 * (W + (CH ? 1 : 0))) void nw_mw_kernel(NWPairs 
         bnext = nx < lb ? b[nx] : 0;
       }
       const int b0 = __builtin_amdgcn_readlane(bcur, idx & 63);
+      if constexpr (CH) {
+        if (cin) {  // lane 0's hand-in for column idx + 1 (uniform: cin, idx)
+          if ((idx & 63) == 0) take_batch(idx);
+          nM = __builtin_amdgcn_readlane((int)hv[0], idx & 63);
+          nX = __builtin_amdgcn_readlane((int)hv[1], idx & 63);
+          nY = __builtin_amdgcn_readlane((int)hv[2], idx & 63);
+          nMP = (P)(uint32_t)__builtin_amdgcn_readlane((int)hv[3], idx & 63);
+          nXP = (P)(uint32_t)__builtin_amdgcn_readlane((int)hv[4], idx & 63);
+          nYP = (P)(uint32_t)__builtin_amdgcn_readlane((int)hv[5], idx & 63);
+        }
+      }
       int uM = dpp_shr1(oM), uX = dpp_shr1(oX), uY = dpp_shr1(oY);
       P uMP = dshr<P>(oMP), uXP = dshr<P>(oXP), uYP = dshr<P>(oYP);
       int bc = dpp_shr1(ob);
@@ -348,7 +333,8 @@ __global__ __launch_bounds__(64 * (W + (CH ? 1 : 0))) void nw_mw_kernel(NWPairs 
         uXP = l0 ? hXP : uXP;
         uYP = l0 ? hYP : uYP;
         const int jn = idx + 2;  // lane 0's next column (uniform)
-        if (w > 0 || (CH && blk > 0)) {
+        if (CH) {
+        } else if (w > 0) {
           const int sl = jn % RING_C;
           nM = rM[sl][w];
           nX = rX[sl][w];
@@ -433,15 +419,14 @@ __global__ __launch_bounds__(64 * (W + (CH ? 1 : 0))) void nw_mw_kernel(NWPairs 
             rMP[sl][w + 1] = oMP;
             rXP[sl][w + 1] = oXP;
             rYP[sl][w + 1] = oYP;
-          } else if (CH && blk + 1 < nblk) {
-            uint64_t *o = q.cbuf + q.cout[slot] + 6 * (uint64_t)j;
-            const uint64_t tg = (uint64_t)(uint32_t)j << 32;
-            __hip_atomic_store(o + 0, tg | (uint32_t)oM, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(o + 1, tg | (uint32_t)oX, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(o + 2, tg | (uint32_t)oY, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(o + 3, tg | (uint32_t)oMP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(o + 4, tg | (uint32_t)oXP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(o + 5, tg | (uint32_t)oYP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          } else if (CH && cout) {  // staged in LDS, flushed 64 columns at a time (below)
+            const int sl = (j - 1) & 63;
+            s_out[0][sl] = oM;
+            s_out[1][sl] = oX;
+            s_out[2][sl] = oY;
+            s_out[3][sl] = (int)(uint32_t)oMP;
+            s_out[4][sl] = (int)(uint32_t)oXP;
+            s_out[5][sl] = (int)(uint32_t)oYP;
           } else if (!CH && blk + 1 < nblk) {
             int *sb = bnd + 6 * j;
             sb[0] = oM;
@@ -461,7 +446,24 @@ __global__ __launch_bounds__(64 * (W + (CH ? 1 : 0))) void nw_mw_kernel(NWPairs 
       } else {
         ob = bc;
       }
-      if ((W > 1 || CH) && (t % KLAG) == KLAG - 1) __syncthreads();
+      if constexpr (CH) {
+        // lane 63 finished column t - 62: at the end of a 64-column batch (or the row) every
+        // lane stores its column's six granules from LDS.  (Stored straight from lane 63 each
+        // step, the stores' source registers -- the next step's state -- made every step wait
+        // for the previous step's stores to complete.)
+        const int jl = t - 62;
+        if (cout && jl >= 1 && jl <= lb && ((jl & 63) == 0 || jl == lb)) {
+          const int c = ((jl - 1) & ~63) + 1 + lane;
+          if (c <= jl) {
+            uint64_t *o = cout + 6 * (uint64_t)c;
+            const uint64_t tg = (uint64_t)(uint32_t)c << 32;
+#pragma unroll
+            for (int v = 0; v < 6; v++)
+              __hip_atomic_store(o + v, tg | (uint32_t)s_out[v][lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+        }
+      }
+      if (W > 1 && (t % KLAG) == KLAG - 1) __syncthreads();
     };
     // steady state: lane 63's column >= 1 and lane 0's <= lb, i.e. lagw + 63 <= t < lagw + lb
     const int ts0 = lb >= 64 ? lagw + 63 : steps, ts1 = lb >= 64 ? lagw + lb : steps;
@@ -542,10 +544,10 @@ int launch_bucket(mc_ctx *c, NWPairs q) {
   return MC_OK;
 }
 
-template <int R>
-int launch_bucket_ch(mc_ctx *c, NWPairs q) {
+int launch_bucket_ch(mc_ctx *c, NWPairs q, int r) {
   if (q.npairs == 0) return MC_OK;
-  nw_mw_kernel<R, uint32_t, 4, true><<<q.npairs, 64 * 5, 0, c->stream>>>(q);
+  if (r == 16) nw_mw_kernel<16, uint32_t, 1, true><<<q.npairs, 64, 0, c->stream>>>(q);
+  else nw_mw_kernel<8, uint32_t, 1, true><<<q.npairs, 64, 0, c->stream>>>(q);
   MCG_CHECK(hipGetLastError());
   return MC_OK;
 }
@@ -578,18 +580,22 @@ int launch_nw(mc_ctx *c, const uint8_t *d_A, const uint64_t *d_aoff, const uint3
     return e ? (uint64_t)atoll(e) : (uint64_t)1024;
   }();
   const bool mw = m < mw_max;
-  // chained row blocks (MC_NW_CHAIN=0 turns them off): a latency-form pair longer than one row
-  // block gets a workgroup per block, the blocks running concurrently one pipeline lag apart
-  static const bool chain_on = !getenv("MC_NW_CHAIN") || atoi(getenv("MC_NW_CHAIN")) != 0;
-  static const int chain_r = [] {  // index of R in (1, 2, 4, 8)
-    const char *e = getenv("MC_NW_CHAIN_R");
-    const int v = e ? atoi(e) : 4;
-    return v == 1 ? 0 : v == 2 ? 1 : v == 8 ? 3 : 2;
+  // chained row blocks (MC_NW_CHAIN=0 turns them off): a pair longer than one block of 64 x R
+  // rows gets a single-wave workgroup per block, the blocks running concurrently a pipeline lag
+  // (~130 steps) apart -- in the latency form, where few pairs leave SIMDs idle; MC_NW_CHAIN=2
+  // chains the throughput form's long pairs too
+  static const int chain_mode = [] {
+    const char *e = getenv("MC_NW_CHAIN");
+    return e ? atoi(e) : 1;
   }();
-  std::vector<uint32_t> ch_pair[4];   // per R (1, 2, 4, 8): work items' pairs
-  std::vector<uint16_t> ch_blk[4];
-  std::vector<uint64_t> ch_in[4], ch_out[4];
-  uint64_t ch_gran = 0;               // granules of every chained pair's block bottom rows
+  // rows per lane of a chained block: 16 (the throughput form's step, 256 registers, two waves
+  // per SIMD) or 8 (MC_NW_CHAIN_R=8: 154 registers, three waves per SIMD, but ~10% more
+  // instructions per cell and twice the blocks; E9100's sampler rounds 269 ms against 239)
+  static const int chain_r = getenv("MC_NW_CHAIN_R") && atoi(getenv("MC_NW_CHAIN_R")) == 8 ? 8 : 16;
+  std::vector<uint32_t> ch_pair;  // work items: pair, block, granule offsets in / out
+  std::vector<uint16_t> ch_blk;
+  std::vector<uint64_t> ch_in, ch_out;
+  uint64_t ch_gran = 0;           // granules of every chained pair's block bottom rows
   enum { NB = 32 };  // latency form: (R, payload) x waves 2 / 4 / 8 / 16
   int bucket_waves[NB] = {0};
   std::vector<uint32_t> bucket[NB];
@@ -606,6 +612,18 @@ int launch_nw(mc_ctx *c, const uint8_t *d_A, const uint64_t *d_aoff, const uint3
     const uint64_t i = order[oi];
     const uint64_t la = alen[i], lb = blen[i];
     const bool wide = la + lb >= 65535;
+    const uint64_t rows_c = 64ull * chain_r;
+    if ((chain_mode >= 2 || (chain_mode == 1 && mw)) && !wide && la > rows_c && lb >= 1) {
+      const uint64_t nblk = (la + rows_c - 1) / rows_c;
+      for (uint64_t b = 0; b < nblk; b++) {
+        ch_pair.push_back((uint32_t)i);
+        ch_blk.push_back((uint16_t)b);
+        ch_in.push_back(b == 0 ? ~0ull : ch_gran + (b - 1) * 6 * (lb + 1));
+        ch_out.push_back(b + 1 == nblk ? ~0ull : ch_gran + b * 6 * (lb + 1));
+      }
+      ch_gran += (nblk - 1) * 6 * (lb + 1);
+      continue;
+    }
     int r, bk;
     uint64_t rows;
     if (mw) {
@@ -615,21 +633,6 @@ int launch_nw(mc_ctx *c, const uint8_t *d_A, const uint64_t *d_aoff, const uint3
       bk = r + (wide ? 4 : 0) + (wv == 2 ? 24 : wv == 4 ? 0 : wv == 8 ? 8 : 16);
       bucket_waves[bk] = wv;
       rows = w64 << r;
-      if (chain_on && wv == 4 && !wide && la > rows && lb >= 1) {
-        // (blocks of R = 4 rows per lane, MC_NW_CHAIN_R = 1 / 2 / 4 / 8: short enough blocks that
-        // enough workgroups are resident to keep every SIMD issuing -- at R = 8 the 139-register
-        // kernel fits two per CU, which was slower than the sequential blocks)
-        const int rc = chain_r;
-        const uint64_t rows_c = 256ull << rc, nblk = (la + rows_c - 1) / rows_c;
-        for (uint64_t b = 0; b < nblk; b++) {
-          ch_pair[rc].push_back((uint32_t)i);
-          ch_blk[rc].push_back((uint16_t)b);
-          ch_in[rc].push_back(b == 0 ? ~0ull : ch_gran + (b - 1) * 6 * (lb + 1));
-          ch_out[rc].push_back(b + 1 == nblk ? ~0ull : ch_gran + b * 6 * (lb + 1));
-        }
-        ch_gran += (nblk - 1) * 6 * (lb + 1);
-        continue;
-      }
     } else {
       r = la <= 256 ? 0 : la <= 512 ? 1 : 2;  // R = 4, 8, 16
       bk = r + (wide ? 3 : 0);
@@ -645,7 +648,7 @@ int launch_nw(mc_ctx *c, const uint8_t *d_A, const uint64_t *d_aoff, const uint3
     total_idx += bucket[k].size();
     total_scr += scratch[k];
   }
-  for (int k = 0; k < 4; k++) total_ch += ch_pair[k].size();
+  total_ch = ch_pair.size();
   if (ensure(c->s_a, total_idx * 4 + 16) || ensure(c->s_b, total_idx * 8 + 16) ||
       ensure(c->s_c, std::max<uint64_t>(total_scr, 1) * 4))
     return MC_ERR_OOM;
@@ -658,34 +661,20 @@ int launch_nw(mc_ctx *c, const uint8_t *d_A, const uint64_t *d_aoff, const uint3
     MCG_CHECK(hipMemsetAsync(c->nw_gran.p, 0, ch_gran * 8 + 64, c->stream));
     char *base = (char *)c->nw_items.p;
     MCG_CHECK(hipMemsetAsync(base + ib + bb + 2 * ob, 0, 256, c->stream));
-    uint64_t at = 0;
-    int *d_err = (int *)(base + ib + bb + 2 * ob + 32);
-    for (int r = 0; r < 4; r++) {
-      const size_t n = ch_pair[r].size();
-      if (!n) continue;
-      MCG_CHECK(hipMemcpyAsync((uint32_t *)base + at, ch_pair[r].data(), n * 4, hipMemcpyHostToDevice, c->stream));
-      MCG_CHECK(hipMemcpyAsync((uint16_t *)(base + ib) + at, ch_blk[r].data(), n * 2, hipMemcpyHostToDevice, c->stream));
-      MCG_CHECK(hipMemcpyAsync((uint64_t *)(base + ib + bb) + at, ch_in[r].data(), n * 8, hipMemcpyHostToDevice, c->stream));
-      MCG_CHECK(hipMemcpyAsync((uint64_t *)(base + ib + bb + ob) + at, ch_out[r].data(), n * 8, hipMemcpyHostToDevice,
-                               c->stream));
-      NWPairs q{d_A, d_aoff, d_ai, d_B, d_boff, d_bi, (uint32_t *)base + at, (uint32_t)n, nullptr, nullptr,
-                d_ident, d_len, d_ids, d_score, d_out};
-      q.pblk = (const uint16_t *)(base + ib) + at;
-      q.ctr = (uint32_t *)(base + ib + bb + 2 * ob) + r;
-      q.cbuf = (uint64_t *)c->nw_gran.p;
-      q.cin = (const uint64_t *)(base + ib + bb) + at;
-      q.cout = (const uint64_t *)(base + ib + bb + ob) + at;
-      q.err = d_err;
-      int rc = MC_OK;
-      switch (r) {
-        case 0: rc = launch_bucket_ch<1>(c, q); break;
-        case 1: rc = launch_bucket_ch<2>(c, q); break;
-        case 2: rc = launch_bucket_ch<4>(c, q); break;
-        default: rc = launch_bucket_ch<8>(c, q); break;
-      }
-      if (rc) return rc;
-      at += n;
-    }
+    const size_t n = total_ch;
+    MCG_CHECK(hipMemcpyAsync((uint32_t *)base, ch_pair.data(), n * 4, hipMemcpyHostToDevice, c->stream));
+    MCG_CHECK(hipMemcpyAsync((uint16_t *)(base + ib), ch_blk.data(), n * 2, hipMemcpyHostToDevice, c->stream));
+    MCG_CHECK(hipMemcpyAsync((uint64_t *)(base + ib + bb), ch_in.data(), n * 8, hipMemcpyHostToDevice, c->stream));
+    MCG_CHECK(hipMemcpyAsync((uint64_t *)(base + ib + bb + ob), ch_out.data(), n * 8, hipMemcpyHostToDevice, c->stream));
+    NWPairs q{d_A, d_aoff, d_ai, d_B, d_boff, d_bi, (uint32_t *)base, (uint32_t)n, nullptr, nullptr,
+              d_ident, d_len, d_ids, d_score, d_out};
+    q.pblk = (const uint16_t *)(base + ib);
+    q.ctr = (uint32_t *)(base + ib + bb + 2 * ob);
+    q.cbuf = (uint64_t *)c->nw_gran.p;
+    q.cin = (const uint64_t *)(base + ib + bb);
+    q.cout = (const uint64_t *)(base + ib + bb + ob);
+    q.err = (int *)(base + ib + bb + 2 * ob + 32);
+    if (int rc = launch_bucket_ch(c, q, chain_r)) return rc;
   }
   uint64_t io = 0, so = 0;
   for (int k = 0; k < NB; k++) {

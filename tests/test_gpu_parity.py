@@ -7,6 +7,7 @@ bin/meshclust must reproduce the reference's --threads 1 .clstr byte for byte.
 import gzip
 import os
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -214,6 +215,43 @@ def test_nw_long_multiblock_vs_oracle(eng):
                               np.tile(b_cat, reps), np.concatenate([[0], np.cumsum(np.tile(lb, reps))]))
     for got, want in zip(big, (ident, ln, ids, sc)):
         assert np.array_equal(got, np.tile(want, reps))
+
+
+_LONG_PAIRS_SCRIPT = r"""
+import sys, numpy as np
+sys.path[:0] = [sys.argv[1], __import__("os").path.dirname(sys.argv[1])]
+import meshclust_amd as M, oracle_lib as O
+rng = np.random.default_rng(11)
+pairs = []
+for la, lb in ((1500, 1400), (2100, 2500), (4000, 3900), (513, 700), (1025, 63), (3000, 200), (9000, 8500),
+               (12000, 11000), (4100, 64), (2049, 1)):
+    a = rng.integers(0, 4, size=la).astype(np.uint8)
+    b = a[:lb].copy() if lb <= la else np.concatenate([a, rng.integers(0, 4, size=lb - la).astype(np.uint8)])
+    flip = rng.random(len(b)) < 0.08
+    b[flip] = rng.integers(0, 4, size=int(flip.sum()))
+    pairs.append((a, b))
+e = M.Engine(0)
+a_off = np.cumsum([0] + [len(a) for a, _ in pairs])
+b_off = np.cumsum([0] + [len(b) for _, b in pairs])
+got = e.nw_identity_raw(np.concatenate([a for a, _ in pairs]), a_off, np.concatenate([b for _, b in pairs]), b_off)
+for i, (a, b) in enumerate(pairs):
+    w = O.nw(a.tobytes(), b.tobytes())
+    assert tuple(x[i] for x in got) == w, (i, tuple(x[i] for x in got), w)
+print("ok", len(pairs))
+"""
+
+
+@pytest.mark.parametrize("env", [{"MC_NW_CHAIN": "0"}, {"MC_NW_CHAIN_R": "8"}, {"MC_NW_CHAIN": "2", "MC_NW_MW_MAX": "0"}],
+                         ids=["sequential", "chain_r8", "chain_throughput"])
+def test_nw_long_pairs_chain_forms_vs_oracle(built, env):
+    """Long pairs (up to 12 kb: many row blocks) in every form of the row-block hand-off: the
+    blocks of a pair in sequence inside one workgroup (MC_NW_CHAIN=0), chained single-wave
+    blocks of 8 rows per lane (the default chains 16), and the throughput form's pairs chained
+    too (MC_NW_CHAIN=2).  The settings are read once per process: a child process each."""
+    here = os.path.dirname(os.path.abspath(__file__))
+    r = subprocess.run([sys.executable, "-c", _LONG_PAIRS_SCRIPT, here], capture_output=True, text=True,
+                       timeout=300, env=dict(os.environ, **env))
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
 
 
 @pytest.fixture(scope="module")
