@@ -37,6 +37,10 @@ namespace {
 constexpr int GO = 2, GE = 1, MATCH = 1, MISMATCH = -1;
 // the same moves in T = score + i + j (see above)
 constexpr int OPEN_T = GO + GE - 1, EXT_T = 1 - GE, MATCH_T = MATCH + 2, MISMATCH_T = MISMATCH + 2;
+// M is kept as M - MOFF (T - OPEN_T): both gap recurrences then compare a stored value with a
+// stored value, and only the diagonal's comparison offsets max(X, Y) -- one VALU instruction less
+// per cell (see the cell loop)
+constexpr int MOFF = OPEN_T;
 
 template <typename P>
 struct Pack;
@@ -165,7 +169,7 @@ __global__ __launch_bounds__(64 * W) void nw_mw_kernel(NWPairs q) {
     for (int r = 0; r < R; r++) {
       const int i = itop + r;
       ac[r] = i <= la ? a[i - 1] : (uint8_t)0xFF;
-      M[r] = NINF + i;  // column 0 (GlobAlignE.cpp:140-160), T = score + i
+      M[r] = NINF + i - MOFF;  // column 0 (GlobAlignE.cpp:140-160), T = score + i
       Y[r] = NINF + i;
       X[r] = -GO - i * GE + i;
       MP[r] = XP[r] = YP[r] = 0;  // i gap moves, no diagonal
@@ -175,12 +179,12 @@ __global__ __launch_bounds__(64 * W) void nw_mw_kernel(NWPairs q) {
     {
       const int i = itop - 1;
       if (i == 0) {
-        dM = 0;
+        dM = -MOFF;
         dX = NINF;
         dY = -GO;
         dMP = dXP = dYP = 0;
       } else {
-        dM = NINF + i;
+        dM = NINF + i - MOFF;
         dX = -GO - i * GE + i;
         dY = NINF + i;
         dMP = dXP = dYP = 0;
@@ -306,7 +310,7 @@ __global__ __launch_bounds__(64 * W) void nw_mw_kernel(NWPairs q) {
           bc = (j >= 1 && j <= lb) ? b0 : 0;
           if (j >= 1 && j <= lb) {
             if (row0) {  // row 0: M = X = -inf, Y = -o - j*e, lengths j (T: + j)
-              uM = NINF + j;
+              uM = NINF + j - MOFF;
               uX = NINF + j;
               uY = -GO - j * GE + j;
               uMP = uXP = uYP = 0;
@@ -324,7 +328,7 @@ __global__ __launch_bounds__(64 * W) void nw_mw_kernel(NWPairs q) {
       } else {
         const bool l0 = lane == 0;
         bc = l0 ? b0 : bc;
-        const int hM = row0 ? NINF + j : nM, hX = row0 ? NINF + j : nX, hY = row0 ? -GO - j * GE + j : nY;
+        const int hM = row0 ? NINF + j - MOFF : nM, hX = row0 ? NINF + j : nX, hY = row0 ? -GO - j * GE + j : nY;
         const P hMP = row0 ? (P)0 : nMP, hXP = row0 ? (P)0 : nXP, hYP = row0 ? (P)0 : nYP;
         uM = l0 ? hM : uM;
         uX = l0 ? hX : uX;
@@ -367,22 +371,25 @@ __global__ __launch_bounds__(64 * W) void nw_mw_kernel(NWPairs q) {
         for (int r = 0; r < R; r++) {
           const int pM = M[r], pX = X[r], pY = Y[r];
           const P pMP = MP[r], pXP = XP[r], pYP = YP[r];
-          const int yb = pM - OPEN_T, yc = pY + EXT_T;  // upperGap (GlobAlignE.cpp:233-251)
+          // (M values are M - MOFF: pM, gM, aM below)
+          const int yb = pM, yc = pY + EXT_T;  // upperGap (GlobAlignE.cpp:233-251): M - (o+e-1) vs Y
           const bool yFromM = yb >= yc;
           Y[r] = yFromM ? yb : yc;
           YP[r] = yFromM ? pMP : pYP;
           const bool hit = ac[r] == (uint8_t)bc;  // matches (:255-299)
           const int sc = hit ? MATCH_T : MISMATCH_T;
-          // M on ties, then X, then Y: M iff gM >= max(gX, gY), else X iff gX >= gY
+          // M on ties, then X, then Y: M iff M >= max(X, Y), else X iff X >= Y -- with gM = M -
+          // MOFF: gM >= max(X, Y) - MOFF, and the new M - MOFF = max(gM, max(X, Y) - MOFF) + sc
           const bool xy = gX >= gY;
           const int mxy = xy ? gX : gY;
           const P pxy = xy ? gXP : gYP;
-          const bool fromM = gM >= mxy;
-          const int best = fromM ? gM : mxy;
+          const int m2 = mxy - MOFF;
+          const bool fromM = gM >= m2;
+          const int best = fromM ? gM : m2;
           const P bestP = fromM ? gMP : pxy;
           M[r] = best + sc;
           MP[r] = bestP + LEN1 + (hit ? (P)1 : (P)0);
-          const int xb = aM - OPEN_T, xc = aX + EXT_T;  // lowerGap (:316-330)
+          const int xb = aM, xc = aX + EXT_T;  // lowerGap (:316-330): M - (o+e-1) vs X
           const bool xFromM = xb >= xc;
           X[r] = xFromM ? xb : xc;
           XP[r] = xFromM ? aMP : aXP;
@@ -483,7 +490,7 @@ __global__ __launch_bounds__(64 * W) void nw_mw_kernel(NWPairs q) {
 #pragma unroll
       for (int rr = 0; rr < R; rr++)
         if (rr == r) {
-          mM = M[rr];
+          mM = M[rr] + MOFF;
           mX = X[rr];
           mY = Y[rr];
           pM = MP[rr];
