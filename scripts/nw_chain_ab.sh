@@ -10,12 +10,13 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_co
 rc=$?; tail -n 3 gpurun_out/${TAG}_pytest.log; [ $rc -eq 0 ] || exit $rc
 for v in ${VARIANTS:-1 r16 2 0}; do
   case $v in
+    *=*) env="${v//,/ }";;
     r16) env="MC_NW_CHAIN_R=16";;
     r8) env="MC_NW_CHAIN_R=8";;
     2r8) env="MC_NW_CHAIN=2 MC_NW_CHAIN_R=8";;
     *) env="MC_NW_CHAIN=$v";;
   esac
-  env $env timeout -k 10 300 python scripts/configs.py ${CFGS:-E9100} > gpurun_out/${TAG}_cfg_$v.log 2>&1 || exit 1
+  env $env timeout -k 10 300 python scripts/configs.py ${CFGS:-E9100} > gpurun_out/${TAG}_cfg_${v//[=,]/_}.log 2>&1 || exit 1
 done
 python - <<'PY'
 import glob, json, os
