@@ -1043,6 +1043,9 @@ int mc_accum_reserve(mc_ctx *c, uint32_t nbins) {
 
 int mc_ctx_partition(mc_ctx *c, int slot, int share) {
   if (!c || share < 1 || share > 32 || slot < 0 || slot >= share) return MC_ERR_ARG;
+  // (a run per clustering partitions again: the same slot keeps its stream -- re-creating it
+  // synchronised with the device and cost milliseconds per rehearsal step)
+  if (slot == c->part_slot && share == c->part_share) return MC_OK;
   MCG_CHECK(hipSetDevice(c->device));
   MCG_CHECK(hipStreamSynchronize(c->stream));
   int cus = 0;
