@@ -236,6 +236,26 @@ int mc_scan_part(mc_ctx *ctx, uint32_t centre_id, uint64_t S, uint64_t E, uint32
 int mc_scan_commit(mc_ctx *ctx, const uint32_t *flagged_pos, uint64_t n, mc_scan_result *res);
 
 /*
+ * Alignment mode (--align, or an identity below 0.6: Runner.cpp:231-236), a get_close step's
+ * Feature::align(*pt, *p) values (Feature.cpp:221-243; Trainer.cpp:34-114's OpenMP loop over
+ * the window) sharded over `nparts` ranks: of the alive static positions of S..E in ascending
+ * order, candidate i is aligned (GlobAlignE, the candidate as seq1, the centre as seq2) by part
+ * i % nparts.  ident[0 .. *n_part) receives this part's identities in candidate order (cap: its
+ * capacity); *pairs / *cells count the WHOLE window's alignments (the same on every part).
+ * Nothing changes on the context.
+ */
+int mc_align_part(mc_ctx *ctx, uint32_t centre_id, uint64_t S, uint64_t E, uint32_t part, uint32_t nparts,
+                  double *ident, uint64_t cap, uint64_t *n_part, uint64_t *pairs, uint64_t *cells);
+/*
+ * The rest of mc_scan's alignment-mode step with the identities given: ident[i] is
+ * Feature::align of the window's i-th alive candidate (ascending static position, as the
+ * parts of mc_align_part interleave back).  Flags, removes and re-centres exactly as mc_scan;
+ * res->nw_pairs / nw_cells are 0 (mc_align_part counted them).
+ */
+int mc_scan_ident(mc_ctx *ctx, uint32_t centre_id, uint64_t S, uint64_t E, const double *ident,
+                  uint32_t *flagged_pos, uint64_t cap, mc_scan_result *res);
+
+/*
  * The whole accumulation phase on the device: ClusterFactory::MS's loop
  * `last = points.pop(); while (last) accumulate(&last, ...)` (ClusterFactory.cpp:717-730,
  * accumulate :637-714) run by one persistent kernel, bvec included -- no host round trip per

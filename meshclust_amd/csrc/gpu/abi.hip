@@ -200,7 +200,7 @@ int mc_ctx_destroy(mc_ctx *c) {
   for (Buf *b : {&c->codes, &c->seq_off, &c->seg, &c->seg_off, &c->packed, &c->pk_off, &c->impure, &c->hist, &c->mag, &c->sumsq, &c->len, &c->order,
                  &c->alive, &c->members, &c->member_keys, &c->partials, &c->scan_dev, &c->flags_out, &c->s_a, &c->s_b,
                  &c->s_c, &c->s_d, &c->s_e, &c->s_f, &c->s_g, &c->s_h, &c->s_i, &c->s_j, &c->s_k, &c->hs, &c->mag_s, &c->sumsq_s, &c->len_s, &c->ticket,
-                 &c->msum, &c->ident_s, &c->al_a, &c->al_b, &c->al_out, &c->acc_out, &c->sp_words, &c->sp_keys,
+                 &c->msum, &c->ident_s, &c->al_a, &c->al_b, &c->al_out, &c->al_id, &c->acc_out, &c->sp_words, &c->sp_keys,
                  &c->sp_scr, &c->sp_nodes, &c->sp_nn, &c->sp_q, &c->sp_err, &c->u_off, &c->u_mem, &c->nw_items, &c->nw_gran})
     release(*b);
   if (c->h_scan) (void)hipHostFree(c->h_scan);
@@ -835,17 +835,10 @@ static int align_window(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, uint
                    nullptr, nullptr, (uint32_t *)c->al_out.p);
 }
 
-int mc_scan(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, uint32_t *flagged_pos, uint64_t cap,
-            mc_scan_result *res) {
-  if (!c || !res || !c->has_cls || c->norder == 0) return MC_ERR_STATE;
-  if (S > E || E >= c->norder || centre >= c->n) return MC_ERR_ARG;
-  c->step++;
-  uint64_t nw_pairs = 0, nw_cells = 0;
-  const double *d_ident = nullptr;
-  if (c->cls.align) {
-    TRY(align_window(c, centre, S, E, &nw_pairs, &nw_cells));
-    d_ident = (const double *)c->ident_s.p;
-  }
+// mc_scan's step after the identities (alignment mode: d_ident, per static position) are on
+// the device
+static int scan_step(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, const double *d_ident, uint64_t nw_pairs,
+                     uint64_t nw_cells, uint32_t *flagged_pos, uint64_t cap, mc_scan_result *res) {
   if (fused(c)) {
     const uint32_t seq = ++c->seq;
     TRY(launch_fused_scan(c, centre, S, E, seq, d_ident));
@@ -893,6 +886,80 @@ int mc_scan(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, uint32_t *flagge
   std::sort(flagged_pos, flagged_pos + nf);
   for (uint64_t i = 0; i < nf; i++) c->h_alive[flagged_pos[i]] = 0;
   return MC_OK;
+}
+
+int mc_scan(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, uint32_t *flagged_pos, uint64_t cap,
+            mc_scan_result *res) {
+  if (!c || !res || !c->has_cls || c->norder == 0) return MC_ERR_STATE;
+  if (S > E || E >= c->norder || centre >= c->n) return MC_ERR_ARG;
+  c->step++;
+  uint64_t nw_pairs = 0, nw_cells = 0;
+  const double *d_ident = nullptr;
+  if (c->cls.align) {
+    TRY(align_window(c, centre, S, E, &nw_pairs, &nw_cells));
+    d_ident = (const double *)c->ident_s.p;
+  }
+  return scan_step(c, centre, S, E, d_ident, nw_pairs, nw_cells, flagged_pos, cap, res);
+}
+
+int mc_align_part(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, uint32_t part, uint32_t nparts, double *ident,
+                  uint64_t cap, uint64_t *n_part, uint64_t *pairs, uint64_t *cells) {
+  if (!c || !c->has_cls || c->norder == 0 || !c->cls.align) return MC_ERR_STATE;
+  if (S > E || E >= c->norder || centre >= c->n || nparts == 0 || part >= nparts || !n_part) return MC_ERR_ARG;
+  std::vector<uint32_t> ai, bi;
+  std::vector<uint64_t> la, lb;
+  const uint64_t lc = c->h_seq_off[centre + 1] - c->h_seq_off[centre];
+  uint64_t np = 0, cl = 0, i = 0;
+  for (uint64_t pos = S; pos <= E; pos++) {
+    if (!c->h_alive[pos]) continue;
+    const uint32_t id = c->h_order[pos];
+    const uint64_t l = c->h_seq_off[id + 1] - c->h_seq_off[id];
+    np++;
+    cl += l * lc;
+    if (i++ % nparts != part) continue;
+    ai.push_back(id);
+    bi.push_back(centre);
+    la.push_back(l);
+    lb.push_back(lc);
+  }
+  if (pairs) *pairs = np;
+  if (cells) *cells = cl;
+  *n_part = ai.size();
+  if (ai.size() > cap || (!ident && !ai.empty())) {
+    set_error("mc_align_part: identity buffer too small");
+    return MC_ERR_ARG;
+  }
+  if (ai.empty()) return MC_OK;
+  // identities to a compact buffer in candidate order (no result slots: pair i -> ident[i])
+  TRY(ensure(c->ident_s, c->norder * 8 + 16));
+  TRY(ensure(c->al_id, ai.size() * 8 + 16));
+  TRY(upload(c, c->al_a, ai.data(), ai.size(), c->stream));
+  TRY(upload(c, c->al_b, bi.data(), bi.size(), c->stream));
+  TRY(launch_nw(c, (uint8_t *)c->codes.p, (uint64_t *)c->seq_off.p, (uint32_t *)c->al_a.p, (uint8_t *)c->codes.p,
+                (uint64_t *)c->seq_off.p, (uint32_t *)c->al_b.p, ai.size(), la, lb, (double *)c->al_id.p, nullptr,
+                nullptr, nullptr, nullptr));
+  MCG_CHECK(hipMemcpyAsync(ident, c->al_id.p, ai.size() * 8, hipMemcpyDeviceToHost, c->stream));
+  MCG_CHECK(hipStreamSynchronize(c->stream));
+  flush_timers(c);
+  return MC_OK;
+}
+
+int mc_scan_ident(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, const double *ident, uint32_t *flagged_pos,
+                  uint64_t cap, mc_scan_result *res) {
+  if (!c || !res || !c->has_cls || c->norder == 0 || !c->cls.align) return MC_ERR_STATE;
+  if (S > E || E >= c->norder || centre >= c->n) return MC_ERR_ARG;
+  c->step++;
+  // the window's identities at their static positions (dead positions: never read)
+  std::vector<double> win(E - S + 1, 0.0);
+  uint64_t i = 0;
+  for (uint64_t pos = S; pos <= E; pos++)
+    if (c->h_alive[pos]) win[pos - S] = ident[i++];
+  TRY(ensure(c->ident_s, c->norder * 8 + 16));
+  MCG_CHECK(hipMemcpyAsync((double *)c->ident_s.p + S, win.data(), win.size() * 8, hipMemcpyHostToDevice, c->stream));
+  // (the pageable copy is complete when the scan's result arrives: the same stream)
+  const int rc = scan_step(c, centre, S, E, (const double *)c->ident_s.p, 0, 0, flagged_pos, cap, res);
+  MCG_CHECK(hipStreamSynchronize(c->stream));
+  return rc;
 }
 
 int mc_scan_part(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, uint32_t part, uint32_t nparts,

@@ -140,7 +140,7 @@ struct mc_ctx {
   // per-static-position identity the scan kernels classify
   std::vector<uint32_t> h_order;
   std::vector<uint8_t> h_alive;
-  mcg::Buf ident_s, al_a, al_b, al_out;
+  mcg::Buf ident_s, al_a, al_b, al_out, al_id;
   mcg::Buf acc_out;  // device-resident accumulation: counters / error word
   // Trainer::split's sorted arrays (mc_split_*): words, stopper scratch, range trees, queries
   mcg::Buf sp_words, sp_keys, sp_scr, sp_nodes, sp_nn, sp_q, sp_err;

@@ -305,12 +305,45 @@ static bool attach_mailbox(const ShardComm &comm, mc_ctx *ctx, uint64_t n, uint3
   return ok;
 }
 
+// Alignment mode, one get_close step with its NW alignments split over the ranks: rank r aligns
+// every W-th alive candidate of the window (mc_align_part), the ranks all-gather the identities
+// and every rank finishes the step on the whole identity vector (mc_scan_ident) -- the same
+// flags, removals and next centre everywhere, with no other exchange.  (A window of config C
+// at 100k holds nearly every alive read: ~10^11 NW cells per step against ~0.8 MB of identities.)
+static void align_sharded_step(mc_ctx *ctx, const ShardComm &comm, uint32_t centre, uint64_t S, uint64_t E,
+                               std::vector<uint32_t> &flag_buf, mc_scan_result *res, PhaseTimer &timer,
+                               ClusterStats &stats) {
+  const uint64_t W = (uint64_t)comm.world, blk = (E - S + 1 + W - 1) / W;  // (a bound on any part's count)
+  std::vector<double> mine(blk + 1, 0.0), all((blk + 1) * W);
+  uint64_t np = 0, pairs = 0, cells = 0;
+  {
+    Scope s(timer, "accumulate.align_part");
+    check(mc_align_part(ctx, centre, S, E, (uint32_t)comm.rank, (uint32_t)W, mine.data() + 1, blk, &np, &pairs, &cells),
+          "mc_align_part");
+  }
+  memcpy(mine.data(), &np, 8);
+  if (comm.allgather(comm.user, mine.data(), mine.size() * 8, all.data()) != 0)
+    throw PeerError("identity all-gather across ranks failed");
+  std::vector<double> ident(pairs);
+  for (uint64_t r = 0; r < W; r++) {
+    uint64_t nr = 0;
+    memcpy(&nr, all.data() + r * (blk + 1), 8);
+    if (nr != (pairs + W - 1 - r) / W) throw PeerError("alignment shard: the ranks' windows differ");
+    for (uint64_t j = 0; j < nr; j++) ident[j * W + r] = all[r * (blk + 1) + 1 + j];
+  }
+  Scope sc(timer, "accumulate.mc_scan");
+  check(mc_scan_ident(ctx, centre, S, E, ident.data(), flag_buf.data(), flag_buf.size(), res), "mc_scan_ident");
+  stats.align_nw_pairs += pairs;
+  stats.align_nw_cells += cells;
+}
+
 // accumulate (ClusterFactory.cpp:637-714): grow one cluster around `last` until get_close
 // finds no similar candidate; returns the next seed through *last_ptr.  With `shard`, every
 // get_close step is split over the ranks (sharded_step).
 void accumulate(uint32_t *last_ptr, const Dataset &ds, mc_ctx *ctx, BVec &bv, std::vector<Center> &centers,
                 const ClusterConfig &cfg, ClusterStats &stats, std::vector<uint32_t> &flag_buf, PhaseTimer &timer,
-                AlignMemo *memo, const ShardComm *shard, std::vector<uint32_t> &all_flagged) {
+                AlignMemo *memo, const ShardComm *shard, std::vector<uint32_t> &all_flagged,
+                const ShardComm *ashard) {
   uint32_t last = *last_ptr;
   std::vector<uint32_t> current = {last};
   check(mc_cluster_begin(ctx, last), "mc_cluster_begin");
@@ -333,6 +366,8 @@ void accumulate(uint32_t *last_ptr, const Dataset &ds, mc_ctx *ctx, BVec &bv, st
       if (memo) memo->begin_step(last, S, E);
       if (shard) {
         sharded_step(ctx, *shard, last, S, E, flag_buf, all_flagged, &res, timer);
+      } else if (ashard) {
+        align_sharded_step(ctx, *ashard, last, S, E, flag_buf, &res, timer, stats);
       } else {
         Scope sc(timer, "accumulate.mc_scan");
         check(mc_scan(ctx, last, S, E, flag_buf.data(), flag_buf.size(), &res), "mc_scan");
@@ -424,6 +459,9 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
   // MC_SHARD_FORCE=1 (tests) takes the sharded code path with a single rank too.
   const bool multi = cfg.comm && (cfg.comm->world > 1 || getenv("MC_SHARD_FORCE"));
   const ShardComm *shard = (multi && !memo && cfg.width <= 2 && !getenv("MC_SHARD_REPLICATE")) ? cfg.comm : nullptr;
+  // Alignment mode: every step's NW alignments (the whole cost of config C) split over the ranks
+  // (align_sharded_step); MC_ALIGN_REPLICATE=1 keeps every rank aligning every window itself.
+  const ShardComm *ashard = (multi && memo && !getenv("MC_ALIGN_REPLICATE")) ? cfg.comm : nullptr;
   // The accumulation is split over the ranks only when one GPU would stream its rows from HBM
   // (more reads than the dense resident form holds in the workers' LDS: ~130k on 256 CUs).
   // Below that a get_close step is bound by its latency chain -- hand-offs, fan-in, collect --
@@ -532,7 +570,9 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
       if (cfg.verbose) fprintf(stderr, "accumulation: host-driven get_close steps: %s\n", mc_last_error());
     }
   } else {
-    stats.accum_path = memo ? "steps (alignment mode)" : "steps (MC_ACCUM_STEPS)";
+    stats.accum_path = !memo     ? std::string("steps (MC_ACCUM_STEPS)")
+                       : ashard ? "steps (alignment mode, NW sharded x" + std::to_string(ashard->world) + ")"
+                                : std::string("steps (alignment mode)");
   }
   if (!done) {
     Scope s(timer, "accumulate");
@@ -542,7 +582,7 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
       if (memo) memo->removed(last);
     }
     while (last != BVec::NONE)
-      accumulate(&last, ds, ctx, bv, part, cfg, stats, flag_buf, timer, memo.get(), shard, all_flagged);
+      accumulate(&last, ds, ctx, bv, part, cfg, stats, flag_buf, timer, memo.get(), shard, all_flagged, ashard);
   }
   comm_phase(cfg.comm, "update");
   Scope s(timer, "update+merge");

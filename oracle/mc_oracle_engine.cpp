@@ -329,19 +329,15 @@ static uint32_t mean_closest(mc_ctx *c, const std::vector<uint32_t> &mem) {
   return best;
 }
 
-int mc_scan(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, uint32_t *flagged, uint64_t cap, mc_scan_result *res) {
+// the serial get_close loop over the window (alignment mode: `ident` per position of S..E;
+// count: whether the NW pairs are counted here)
+static int scan_loop(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, const std::vector<double> &ident, bool count,
+                     uint32_t *flagged, uint64_t cap, mc_scan_result *res) {
   memset(res, 0, sizeof *res);
   double best_val = -1;
   bool has = false;
   uint64_t best_pos = 0, nf = 0;
   bool is_min = true;
-  std::vector<double> ident;
-  if (c->align) {  // Feature::align(*pt, *p) for the whole window, then the serial loop
-    ident.assign(E - S + 1, 0.0);
-#pragma omp parallel for schedule(dynamic)
-    for (uint64_t pos = S; pos <= E; pos++)
-      if (c->alive[pos]) ident[pos - S] = nw_ident(c, c->order[pos], centre);
-  }
   for (uint64_t pos = S; pos <= E; pos++) {
     if (!c->alive[pos]) continue;
     uint32_t id = c->order[pos];
@@ -350,8 +346,10 @@ int mc_scan(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, uint32_t *flagge
     if (c->align) {
       double r[MC_MAX_SINGLE] = {ident[pos - S]};
       d = mco_classify(&c->cls, r, &s, &c0);
-      res->nw_pairs++;
-      res->nw_cells += len_of(c, id) * len_of(c, centre);
+      if (count) {
+        res->nw_pairs++;
+        res->nw_cells += len_of(c, id) * len_of(c, centre);
+      }
     } else {
       d = classify(c, id, centre, &s, &c0);
     }
@@ -376,6 +374,50 @@ int mc_scan(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, uint32_t *flagge
   if (!is_min) res->new_centre = mean_closest(c, c->members);
   res->n_members = (uint32_t)c->members.size();
   return MC_OK;
+}
+
+int mc_scan(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, uint32_t *flagged, uint64_t cap, mc_scan_result *res) {
+  std::vector<double> ident;
+  if (c->align) {  // Feature::align(*pt, *p) for the whole window, then the serial loop
+    ident.assign(E - S + 1, 0.0);
+#pragma omp parallel for schedule(dynamic)
+    for (uint64_t pos = S; pos <= E; pos++)
+      if (c->alive[pos]) ident[pos - S] = nw_ident(c, c->order[pos], centre);
+  }
+  return scan_loop(c, centre, S, E, ident, true, flagged, cap, res);
+}
+
+int mc_align_part(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, uint32_t part, uint32_t nparts, double *ident,
+                  uint64_t cap, uint64_t *n_part, uint64_t *pairs, uint64_t *cells) {
+  if (!c->align) return fail(MC_ERR_STATE, "mc_align_part: alignment mode only");
+  if (S > E || E >= c->order.size() || nparts == 0 || part >= nparts || !n_part) return fail(MC_ERR_ARG, "bad window");
+  std::vector<uint32_t> mine;
+  uint64_t np = 0, cl = 0, i = 0;
+  for (uint64_t pos = S; pos <= E; pos++) {
+    if (!c->alive[pos]) continue;
+    const uint32_t id = c->order[pos];
+    np++;
+    cl += len_of(c, id) * len_of(c, centre);
+    if (i++ % nparts == part) mine.push_back(id);
+  }
+  if (pairs) *pairs = np;
+  if (cells) *cells = cl;
+  *n_part = mine.size();
+  if (mine.size() > cap || (!ident && !mine.empty())) return fail(MC_ERR_ARG, "mc_align_part: identity buffer too small");
+#pragma omp parallel for schedule(dynamic)
+  for (int64_t j = 0; j < (int64_t)mine.size(); j++) ident[j] = nw_ident(c, mine[j], centre);
+  return MC_OK;
+}
+
+int mc_scan_ident(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, const double *ident, uint32_t *flagged,
+                  uint64_t cap, mc_scan_result *res) {
+  if (!c->align) return fail(MC_ERR_STATE, "mc_scan_ident: alignment mode only");
+  if (S > E || E >= c->order.size()) return fail(MC_ERR_ARG, "bad window");
+  std::vector<double> win(E - S + 1, 0.0);
+  uint64_t i = 0;
+  for (uint64_t pos = S; pos <= E; pos++)
+    if (c->alive[pos]) win[pos - S] = ident[i++];
+  return scan_loop(c, centre, S, E, win, false, flagged, cap, res);
 }
 
 int mc_scan_part(mc_ctx *c, uint32_t centre, uint64_t S, uint64_t E, uint32_t part, uint32_t nparts, uint32_t *flagged,

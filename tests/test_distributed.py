@@ -76,6 +76,33 @@ def test_sharded_gloo_cpu_byte_identical(cpu_lib, name, world, tmp_path):
     _run_world(name, tmp_path, gpu=False, world=world)
 
 
+def _run_align_world(name, tmp_path, gpu, world):
+    """Alignment mode shares the NW alignments of every get_close window over the ranks
+    (cluster.cpp align_sharded_step: mc_align_part + identity all-gather + mc_scan_ident):
+    rank 0's .clstr equals the reference golden and every rank reports the sharded path."""
+    fa, flags = fixtures.e2e_input(name, tmp_path)
+    out = str(tmp_path / (name + ".clstr"))
+    ranks = _launch(fa, flags, out, gpu, world)
+    with gzip.open(fixtures.golden("e2e_%s.clstr.gz" % name), "rb") as f:
+        assert open(out, "rb").read() == f.read()
+    for rk in ranks:
+        assert rk["accum_path"] == "steps (alignment mode, NW sharded x%d)" % world, rk["accum_path"]
+        assert rk["calls"] >= rk["scan_steps"] > 0  # one identity exchange per step
+    return ranks
+
+
+@pytest.mark.parametrize("name,world", [("al300", 2), ("al_mix300", 3)])
+def test_align_sharded_gloo_cpu_byte_identical(cpu_lib, name, world, tmp_path):
+    _run_align_world(name, tmp_path, gpu=False, world=world)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["al300", "al_mix300", "c2k_m15_al55"])
+def test_align_sharded_gpu_byte_identical(name, tmp_path):
+    """Two ranks on the GPU (each on half of the CUs) share every alignment window's NW."""
+    _run_align_world(name, tmp_path, gpu=True, world=2)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["a1k", "fam2k", "m2k_id80", "big2_3k", "s1k_k5"])
 def test_world2_gpu_byte_identical(name, tmp_path):
