@@ -328,14 +328,41 @@ __device__ __forceinline__ void count_words(const Pre &w, int64_t p0, int cnt, i
   }
 }
 
+// The same with k a compile-time constant K (k = 4, 5, 6: configs B, D, E): the 16 k-mers
+// unrolled, each one a bitfield of the window with its 2-bit groups reversed once (base j of
+// the window at bits [62 - 2j, 63 - 2j]: the k-mer of start j, first base most significant as
+// KmerHashTable's hash, is bits [64 - 2(j + K), 64 - 2j)) instead of a rolling hash with a
+// variable 64-bit shift, and the starts past `cnt` (a sequence's last group) counted into a
+// trash word instead of a divergent loop: 2-4 VALU instructions per k-mer instead of 7 (the
+// kernel is VALU-issue bound: 0.83 of the issue rate at D1M, LDS 0.41 busy)
+template <int K>
+__device__ __forceinline__ void count_words_k(const Pre &w, int64_t p0, int cnt, uint32_t *tab, uint32_t *trash) {
+  const uint64_t lo = ((uint64_t)w.w1 << 32) | w.w0, hi = w.w2;
+  const int sh = (int)(p0 & 15) * 2;
+  const uint64_t win = sh ? (lo >> sh) | (hi << (64 - sh)) : lo;  // base j at bits 2j (low), 2j + 1
+  // bit reversal puts base j at bits 31 - 2j / 30 - 2j with its two bits swapped: swap them back
+  uint32_t a = __builtin_bitreverse32((uint32_t)win), b = __builtin_bitreverse32((uint32_t)(win >> 32));
+  a = ((a >> 1) & 0x55555555u) | ((a & 0x55555555u) << 1);
+  b = ((b >> 1) & 0x55555555u) | ((b & 0x55555555u) << 1);
+  const uint64_t r = ((uint64_t)a << 32) | b;
+  constexpr uint32_t mask = (1u << (2 * K)) - 1u;
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    const uint32_t h = (uint32_t)(r >> (64 - 2 * (j + K))) & mask;
+    atomicAdd(j < cnt ? tab + h : trash, 1u);
+  }
+}
+
 // S sub-tables per wave (lanes l*64/S .. (l+1)*64/S - 1 count into sub-table l): a k-mer
 // increment is an LDS atomic, and lanes of one instruction that hit the same bin serialise;
 // S tables take those collisions apart (k = 4: S = 4, 4 KiB per wave).  The row sums them.
-template <int S>
-__device__ __forceinline__ void kmer_stream8(const KArgs &A, uint32_t *tab0, int B, bool write, uint64_t *wmax_out) {
+template <int S, int K = 0>
+__device__ __forceinline__ void kmer_stream8(const KArgs &A, uint32_t *tab0, int B_, bool write, uint64_t *wmax_out,
+                                             uint32_t *trash) {
   const int wv = wave_id(), lane = threadIdx.x & 63;
+  const int B = K ? 1 << (2 * K) : B_;
   uint32_t *tab = tab0 + (size_t)(lane / (64 / S)) * B;
-  const int k = A.k;
+  const int k = K ? K : A.k;
   const uint32_t mask = (1u << (2 * k)) - 1u;
   const uint64_t stride = (uint64_t)gridDim.x * KW;
   uint32_t lmax = 0;  // this lane's largest bin (+ pseudocount) over every row it wrote
@@ -383,7 +410,8 @@ __device__ __forceinline__ void kmer_stream8(const KArgs &A, uint32_t *tab0, int
             atomicOr(A.err, 1);
             continue;
           }
-          count_words(g == lane ? cur : pre_load(A, q0, q1, p0, true), p0, cnt, k, mask, tab);
+          if constexpr (K > 0) count_words_k<K>(g == lane ? cur : pre_load(A, q0, q1, p0, true), p0, cnt, tab, trash);
+          else count_words(g == lane ? cur : pre_load(A, q0, q1, p0, true), p0, cnt, k, mask, tab);
         }
       } else {
         count_sequence(A, s, tab, 0, 1);
@@ -421,7 +449,16 @@ __device__ __forceinline__ void kmer_stream8(const KArgs &A, uint32_t *tab0, int
       }
       if (write)  // the row's padding up to the pitch
         for (uint64_t b = (uint64_t)B + lane; b < A.pitch; b += 64) row[b] = 0;
-      if (small) {
+      // (a pure one-segment sequence counted every start of [p_lo, p_hi] once: its magnitude is
+      // that count + B pseudocounts, no reduction)
+      const bool one_jj = K > 0 && __builtin_amdgcn_readlane((int)one, jj) != 0;
+      if (one_jj && small) {
+        const int64_t first = __builtin_amdgcn_readlane(sf, jj);
+        const int64_t last0 = (int64_t)__builtin_amdgcn_readlane(sl, jj) - k + 1;
+        m64 = (uint64_t)((last0 < first ? first : last0) - first + 1) + (uint64_t)B;
+        sq = wave_sum32_all(sq);
+        sq64 = sq;
+      } else if (small) {
         m = wave_sum32_all(m);
         sq = wave_sum32_all(sq);
         m64 = m;
@@ -454,7 +491,7 @@ __device__ __forceinline__ void kmer_stream8(const KArgs &A, uint32_t *tab0, int
 // at run time between LDS and global memory makes every table access a FLAT instruction.
 // STREAM: kmer_stream8 alone (a kernel of its own: its register allocation, not the general
 // form's, sets the occupancy).
-template <typename T, bool GLOB, bool STREAM = false, int S = 1>
+template <typename T, bool GLOB, bool STREAM = false, int S = 1, int K = 0>
 __global__ __launch_bounds__(KT) void kmer_kernel(KArgs A, bool write) {
   extern __shared__ __attribute__((aligned(16))) uint32_t ltab[];
   __shared__ uint64_t s_max[KW];
@@ -470,7 +507,8 @@ __global__ __launch_bounds__(KT) void kmer_kernel(KArgs A, bool write) {
     for (int b = lane; b < S * B; b += 64) tab_zero(mytab + b, glob);
   tab_drain(glob);
   if constexpr (STREAM) {
-    kmer_stream8<S>(A, mytab, B, write, &wmax);
+    // (trash: one word per wave past the tables, for the starts a last group does not have)
+    kmer_stream8<S, K>(A, mytab, B, write, &wmax, ltab + (size_t)KW * S * B + wv);
   } else if (!A.coop) {
     // one wave per sequence: the wave's own table, no workgroup barrier.  The metadata of the
     // wave's next 64 sequences (offsets, purity, segment bounds) are loaded lane by lane in two
@@ -602,9 +640,12 @@ int launch_kmer(mc_ctx *c, int k, int width, bool write, uint64_t *d_max, int *d
         // (S > 1 measured slower: 76 vs 68 us at config B, 531 vs 507 us at D1M -- the table
         // atomics are not what bounds the kernel; MC_KMER_SUB=1 keeps the sub-tables for tests)
         const int S = getenv("MC_KMER_SUB") ? (k == 4 ? 4 : k == 5 ? 2 : 1) : 1;
-        const size_t sl = (size_t)KW * S * B * 4;
+        const size_t sl = (size_t)KW * S * B * 4 + KW * 4;
         if (S == 4) kmer_kernel<uint8_t, false, true, 4><<<grid, KT, sl, c->stream>>>(A, write);
         else if (S == 2) kmer_kernel<uint8_t, false, true, 2><<<grid, KT, sl, c->stream>>>(A, write);
+        else if (k == 4 && !getenv("MC_KMER_RUNTIME_K")) kmer_kernel<uint8_t, false, true, 1, 4><<<grid, KT, sl, c->stream>>>(A, write);
+        else if (k == 5 && !getenv("MC_KMER_RUNTIME_K")) kmer_kernel<uint8_t, false, true, 1, 5><<<grid, KT, sl, c->stream>>>(A, write);
+        else if (k == 6 && !getenv("MC_KMER_RUNTIME_K")) kmer_kernel<uint8_t, false, true, 1, 6><<<grid, KT, sl, c->stream>>>(A, write);
         else kmer_kernel<uint8_t, false, true, 1><<<grid, KT, sl, c->stream>>>(A, write);
       }
       else

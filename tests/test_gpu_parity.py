@@ -99,7 +99,8 @@ def test_kmer_all_k_and_table_modes_vs_oracle(eng, mean_len):
 @pytest.mark.parametrize("k", [4, 5, 6])
 def test_kmer_stream_equals_general(eng, k, monkeypatch):
     """K1's streaming form (8-bit rows, k = 4..6: the next sequence's words in flight while the
-    current one is counted, statistics stored per 64 sequences) against the general form
+    current one is counted, statistics stored per 64 sequences; k compiled in, and k at run time)
+    against the general form
     (MC_KMER_NO_STREAM) and the oracle: several 64-sequence batches per wave, sequences longer
     than 64 16-start groups, several segments, 'N' bytes (impure), segments shorter than k.
     The PEARSON feature checks the sums of squares, the histograms and magnitudes the rest."""
@@ -121,7 +122,9 @@ def test_kmer_stream_equals_general(eng, k, monkeypatch):
     ij = np.array([(i, (i * 7 + 3) % len(recs)) for i in range(len(recs))], np.uint32)
     flags = [(1 << 5), (1 << 4), (1 << 2)]  # PEARSON, INTERSECTION, MANHATTAN
     out = {}
-    for mode in ("stream", "general"):
+    for mode in ("stream", "runtime_k", "general"):
+        if mode == "runtime_k":  # the streaming form with k a run-time value (not K = 4 / 5 / 6)
+            monkeypatch.setenv("MC_KMER_RUNTIME_K", "1")
         if mode == "general":
             monkeypatch.setenv("MC_KMER_NO_STREAM", "1")
         assert eng.kmer_max(k) == int(want.max())
@@ -131,6 +134,7 @@ def test_kmer_stream_equals_general(eng, k, monkeypatch):
         assert np.array_equal(mags, want.sum(axis=1)), mode
         out[mode] = eng.pair_features(ij[:, 0], ij[:, 1], flags)
     assert np.array_equal(out["stream"], out["general"])
+    assert np.array_equal(out["runtime_k"], out["general"])
 
 
 def test_load_packed_equals_bytes(eng):
