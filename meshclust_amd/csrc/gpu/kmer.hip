@@ -344,11 +344,17 @@ __device__ __forceinline__ void count_words_k(const Pre &w, int64_t p0, int cnt,
   uint32_t a = __builtin_bitreverse32((uint32_t)win), b = __builtin_bitreverse32((uint32_t)(win >> 32));
   a = ((a >> 1) & 0x55555555u) | ((a & 0x55555555u) << 1);
   b = ((b >> 1) & 0x55555555u) | ((b & 0x55555555u) << 1);
-  const uint64_t r = ((uint64_t)a << 32) | b;
-  constexpr uint32_t mask = (1u << (2 * K)) - 1u;
+  // k-mer j is bits [lo, lo + 2K) of a:b, lo = 64 - 2(j + K): one bitfield extract from the word
+  // that holds it (a compile-time choice), then the table address (one shift-add)
 #pragma unroll
   for (int j = 0; j < 16; j++) {
-    const uint32_t h = (uint32_t)(r >> (64 - 2 * (j + K))) & mask;
+    const int lo = 64 - 2 * (j + K);
+    // (the extract as asm: left to itself the compiler folds the table's x4 into a shift and a
+    // mask and adds the base -- three instructions where bfe + lshl_add are two)
+    uint32_t h;
+    if (lo >= 32) asm("v_bfe_u32 %0, %1, %2, %3" : "=v"(h) : "v"(a), "i"(lo - 32), "i"(2 * K));
+    else if (lo + 2 * K <= 32) asm("v_bfe_u32 %0, %1, %2, %3" : "=v"(h) : "v"(b), "i"(lo), "i"(2 * K));
+    else asm("v_bfe_u32 %0, %1, 0, %2" : "=v"(h) : "v"(__builtin_amdgcn_alignbit(a, b, (uint32_t)lo)), "i"(2 * K));
     atomicAdd(j < cnt ? tab + h : trash, 1u);
   }
 }
