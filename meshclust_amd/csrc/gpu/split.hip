@@ -117,18 +117,24 @@ struct SelArgs {
   int nowave;                // MC_SPLIT_NO_WAVE: every LDS partition by the whole workgroup
 };
 
+// inclusive scan over the wave by DPP (rows of 16 by row_shr 1 / 2 / 4 / 8, then the rows'
+// totals by row_bcast 15 / 31): six VALU adds, no LDS round trip (a __shfl_up scan is six
+// dependent ds_bpermute round trips)
+__device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+  return x;
+}
+
 // Workgroup-wide exclusive scan of two counters (every thread gets its offsets and the totals).
 __device__ __forceinline__ void block_scan2(uint32_t a, uint32_t b, uint32_t *ea, uint32_t *eb, uint32_t *ta,
                                             uint32_t *tb, uint32_t *s) {
   const int lane = threadIdx.x & 63, wv = wave_id();
-  uint32_t ia = a, ib = b;  // inclusive scans within the wave
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t ua = (uint32_t)__shfl_up((int)ia, o, 64), ub = (uint32_t)__shfl_up((int)ib, o, 64);
-    if (lane >= o) {
-      ia += ua;
-      ib += ub;
-    }
-  }
+  const uint32_t ia = wave_scan_incl(a), ib = wave_scan_incl(b);  // inclusive scans within the wave
   if (lane == 63) {
     s[wv] = ia;
     s[SW + wv] = ib;
@@ -188,13 +194,21 @@ __device__ int64_t partition_wg(FP f, int64_t n, PT *L, PT *R, uint32_t *s32, ui
   } else {
     // global range: chunks of CPT words per thread, every load of a chunk in flight at once,
     // stopper positions written chunk after chunk (so in order)
+    // (the next chunk's words are loaded before this chunk's scan: the scan's barriers wait for
+    // LDS only, so the loads stay in flight across it)
     constexpr int CPT = 8;
     uint32_t bg = 0, bl = 0;  // stoppers before this chunk
+    uint32_t kn[CPT];
+#pragma unroll
+    for (int e = 0; e < CPT; e++) kn[e] = (int64_t)t * CPT + e < n ? (uint32_t)(f[(int64_t)t * CPT + e] >> 32) : 0u;
     for (int64_t c0 = 0; c0 < n; c0 += (int64_t)ST * CPT) {
       const int64_t i0 = c0 + (int64_t)t * CPT;
       uint32_t kk[CPT];
 #pragma unroll
-      for (int e = 0; e < CPT; e++) kk[e] = i0 + e < n ? (uint32_t)(f[i0 + e] >> 32) : 0u;
+      for (int e = 0; e < CPT; e++) kk[e] = kn[e];
+      const int64_t i1 = i0 + (int64_t)ST * CPT;
+#pragma unroll
+      for (int e = 0; e < CPT; e++) kn[e] = i1 + e < n ? (uint32_t)(f[i1 + e] >> 32) : 0u;
       uint32_t mg = 0, ml = 0;
 #pragma unroll
       for (int e = 0; e < CPT; e++)
