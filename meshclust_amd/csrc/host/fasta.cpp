@@ -327,6 +327,163 @@ void parse_chunk(const char *buf, size_t a, size_t z, bool first, bool eof, cons
   close();
 }
 
+// The same for a chunk with no '\r' (lines end at '\n' alone), without copying a plain record's
+// lines into one buffer first: each record's sequence bytes are classified 32 at a time (the
+// '\n' bytes dropped, every other byte A/C/G/T in either case) and their 2-bit codes gathered
+// straight into the record's packed words (pext over each 8-byte group, the newline bytes left
+// out of its mask).  A record with any other byte, or shorter than 20 bases, is handed to
+// parse_chunk's path (its lines gathered, process_record).  Records, headers, lengths, segments
+// and packed words are exactly parse_chunk's.
+void parse_chunk_lf(const char *buf, size_t a, size_t z, bool first, bool eof, const std::string &path, Chunk &ck) {
+  // ck.pk's words [0, np) are this chunk's so far; the vector is kept at least as long (and is
+  // cut to np at the end), so the packed words of a plain record are stored without a bounds
+  // check per word
+  size_t np = ck.pk.size();
+  ck.pk.resize(np + (z - a) / 16 + 64);
+  std::vector<uint8_t> tmp;
+  std::vector<uint32_t> fb;
+  std::vector<int32_t> segs;
+  const __m256i lower = _mm256_set1_epi8(0x20), three = _mm256_set1_epi8(3), nlv = _mm256_set1_epi8('\n'),
+                gtv = _mm256_set1_epi8('>');
+  const __m256i tbl = _mm256_setr_epi8('a', 'c', 'g', 't', 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,  //
+                                       'a', 'c', 'g', 't', 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0);
+  const uint64_t M8 = 0x0303030303030303ull;
+  size_t pos = a;
+  // lines before the first header: blank ones are skipped, anything else is an error
+  while (pos < z && buf[pos] != '>') {
+    const char *nl = (const char *)memchr(buf + pos, '\n', z - pos);
+    const size_t e = nl ? (size_t)(nl - buf) : z;
+    if (e > pos) {
+      if (first) throw Error("sequence data before the first '>' header in " + path, 1);
+      throw Error("internal: chunk does not start at a record", 1);
+    }
+    pos = e + 1;
+  }
+  while (pos < z) {
+    // the header line [pos, he)
+    const char *hn = (const char *)memchr(buf + pos, '\n', z - pos);
+    const size_t he = hn ? (size_t)(hn - buf) : z;
+    Chunk::Rec r{pos, he - pos, 0, 0, (uint64_t)np, false};
+    // the record's lines are [s, t), t = the next '>' at the start of a line (or the chunk's
+    // end); t is found in the same pass that classifies and packs the bytes
+    const size_t s = he < z ? he + 1 : z;
+    size_t t = z, i = s, o = np;
+    bool plain = true, found = false;
+    uint64_t acc = 0, nb = 0;
+    uint32_t fill = 0, carry = 1;  // carry: the byte before block i is '\n' (buf[he] at first)
+    for (; i < z; i += 32) {
+      const __m256i v = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(buf + i));  // (64 bytes of slack)
+      const __m256i c = _mm256_and_si256(_mm256_xor_si256(_mm256_srli_epi16(v, 1), _mm256_srli_epi16(v, 2)), three);
+      const uint32_t ok = (uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(_mm256_shuffle_epi8(tbl, c), _mm256_or_si256(v, lower)));
+      const uint32_t nl = (uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(v, nlv));
+      const uint32_t gt = (uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(v, gtv));
+      uint32_t live = z - i >= 32 ? 0xffffffffu : (1u << (z - i)) - 1u;
+      const uint32_t st = gt & ((nl << 1) | carry) & live;
+      if (st) {
+        const uint32_t e = (uint32_t)__builtin_ctz(st);
+        live = (1u << e) - 1u;
+        t = i + e;
+        found = true;
+      }
+      carry = nl >> 31;
+      if (((ok | nl) & live) != live) {
+        plain = false;
+        break;
+      }
+      if (o + 4 > ck.pk.size()) ck.pk.resize(2 * ck.pk.size() + 64);
+      uint32_t *out = ck.pk.data();
+      const uint32_t keep = ok & ~nl & live;
+      alignas(32) uint64_t q[4];
+      _mm256_store_si256(reinterpret_cast<__m256i *>(q), c);
+      // two 16-byte halves: their 2-bit codes (pext of each byte's two low bits), then the
+      // kept bytes' codes (pext with the keep mask spread to 2-bit fields) appended to acc
+#pragma GCC unroll 2
+      for (int h = 0; h < 2; h++) {
+        const uint64_t codes = _pext_u64(q[2 * h], M8) | (_pext_u64(q[2 * h + 1], M8) << 16);
+        const uint32_t k16 = (keep >> (16 * h)) & 0xffffu;
+        const uint64_t bits = _pext_u64(codes, _pdep_u64(k16, 0x55555555ull) * 3u);
+        const uint32_t n = (uint32_t)__builtin_popcount(k16);
+        acc |= bits << fill;
+        fill += 2 * n;
+        nb += n;
+        out[o] = (uint32_t)acc;
+        const uint32_t adv = fill >> 5;
+        o += adv;
+        acc >>= 32 * adv;
+        fill &= 31;
+      }
+      if (found) break;
+    }
+    if (!found && i < z && !plain) {
+      // a non-plain byte before the record's end was known: find the end as parse_chunk would
+      for (t = i;;) {
+        const char *g = t < z ? (const char *)memchr(buf + t, '>', z - t) : nullptr;
+        if (!g) {
+          t = z;
+          break;
+        }
+        t = (size_t)(g - buf);
+        if (buf[t - 1] == '\n') break;
+        t++;
+      }
+    }
+    r.ready = s < t || (t == z && eof);  // some line followed the header (or the file ended)
+    if (plain && nb >= 20) {
+      if (fill) ck.pk[o++] = (uint32_t)acc;
+      np = o;
+      r.off = ck.bytes;
+      r.len = nb;
+      ck.bytes += nb;
+      const size_t s0 = ck.seg.size();
+      plain_segments((int64_t)nb, ck.seg);
+      ck.nseg.push_back((ck.seg.size() - s0) / 2);
+      ck.recs.push_back(r);
+    } else {
+      // parse_chunk's path for this record: its lines gathered, then encode_plain or
+      // process_record, packing into fb; fb is then copied to words [np, ...)
+      tmp.clear();
+      fb.clear();
+      for (size_t u = s; u < t;) {
+        const char *nl = (const char *)memchr(buf + u, '\n', t - u);
+        const size_t e = nl ? (size_t)(nl - buf) : t;
+        tmp.insert(tmp.end(), buf + u, buf + e);
+        u = e + 1;
+      }
+      r.off = ck.bytes;
+      r.len = tmp.size();
+      ck.bytes += r.len;
+      if (r.len >= 20 && encode_plain(tmp.data(), tmp.size(), fb)) {
+        const size_t s0 = ck.seg.size();
+        plain_segments((int64_t)r.len, ck.seg);
+        ck.nseg.push_back((ck.seg.size() - s0) / 2);
+      } else {
+        if (!r.ready) throw Error("The header and the sequence must be set before calling finalize", 1);
+        process_record(tmp.data(), tmp.size(), segs);
+        ck.seg.insert(ck.seg.end(), segs.begin(), segs.end());
+        ck.nseg.push_back(segs.size() / 2);
+        for (size_t j = 0; j < tmp.size(); j += 16) {
+          uint32_t x = 0;
+          for (size_t u = 0; u < 16 && j + u < tmp.size(); u++) {
+            const uint8_t cc = tmp[j + u];
+            x |= (uint32_t)(cc & 3) << (2 * u);
+            if (cc > 3) {
+              ck.exc_pos.push_back(r.off + j + u);
+              ck.exc_val.push_back(cc);
+            }
+          }
+          fb.push_back(x);
+        }
+      }
+      ck.recs.push_back(r);
+      if (np + fb.size() + 4 > ck.pk.size()) ck.pk.resize(std::max(2 * ck.pk.size(), np + fb.size() + 64));
+      if (!fb.empty()) memcpy(ck.pk.data() + np, fb.data(), fb.size() * sizeof(uint32_t));
+      np += fb.size();
+    }
+    pos = t;
+  }
+  ck.pk.resize(np);
+}
+
 }  // namespace
 
 void parse_fasta_files(const std::vector<std::string> &files, Dataset &ds, int threads) {
@@ -398,10 +555,16 @@ void parse_fasta_files(const std::vector<std::string> &files, Dataset &ds, int t
     }
     lap("read+cut");
     std::vector<Chunk> ck(T);
+    static const bool fast_lf = !getenv("MC_PARSE_LINES");  // (MC_PARSE_LINES=1: parse_chunk only)
 #pragma omp parallel for schedule(dynamic, 1) num_threads(threads)
     for (int t = 0; t < T; t++) {
       try {
-        if (cut[t] < cut[t + 1]) parse_chunk(buf, cut[t], cut[t + 1], t == 0, cut[t + 1] == n, path, ck[t]);
+        if (cut[t] < cut[t + 1]) {
+          if (fast_lf && !memchr(buf + cut[t], '\r', cut[t + 1] - cut[t]))
+            parse_chunk_lf(buf, cut[t], cut[t + 1], t == 0, cut[t + 1] == n, path, ck[t]);
+          else
+            parse_chunk(buf, cut[t], cut[t + 1], t == 0, cut[t + 1] == n, path, ck[t]);
+        }
       } catch (const std::exception &e) {
         ck[t].err = e.what();
       }

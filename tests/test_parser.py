@@ -75,3 +75,55 @@ def test_parse_errors_match_reference(host_built, tmp_path, case):
     with pytest.raises(M.MCError) as ei:
         M.Dataset([str(p)], threads=1)
     assert spec["message"] in str(ei.value)
+
+
+_DIFF_SCRIPT = r"""
+import hashlib, sys
+import meshclust_amd as M
+h = hashlib.sha256()
+for hdr, codes, segs in M.Dataset([sys.argv[1]], threads=int(sys.argv[2])).records():
+    h.update(repr((hdr, segs)).encode()); h.update(codes.tobytes())
+print(h.hexdigest())
+"""
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_lf_fast_path_matches_line_path(host_built, tmp_path, seed):
+    """parse_chunk_lf (records of a '\\r'-free chunk packed straight from the file bytes) gives
+    the records of parse_chunk (lines gathered first; pinned by the goldens above, and forced by
+    MC_PARSE_LINES=1): random multi-line records of mixed case, N runs, IUPAC codes, blank lines,
+    records under 20 bases and line widths that straddle the 32-byte blocks, parsed in many
+    chunks."""
+    import os
+    import subprocess
+    import sys
+    rng = np.random.default_rng(seed)
+    out = []
+    for r in range(3000):
+        L = int(rng.choice([20, 21, 31, 32, 33, 64, 95, 150, 700, 2000]) + rng.integers(0, 3))
+        s = rng.choice(list(b"ACGTacgt"), L).astype(np.uint8)
+        kind = rng.integers(0, 8)
+        if kind == 0:
+            i = int(rng.integers(0, L - 5)); s[i:i + 5] = ord("N")
+        elif kind == 1:
+            s[int(rng.integers(0, L))] = ord(rng.choice(list("RYKMSWn")))
+        seq = s.tobytes()
+        w = int(rng.choice([10, 31, 32, 33, 60, 80, 1000]))
+        lines = [seq[i:i + w] for i in range(0, len(seq), w)]
+        if rng.integers(0, 10) == 0:
+            lines.insert(int(rng.integers(0, len(lines) + 1)), b"")
+        out.append(b">r%d some text\n" % r + b"\n".join(lines) + (b"\n" if rng.integers(0, 20) else b"\n\n"))
+    if seed == 2:
+        out[-1] = out[-1].rstrip(b"\n")
+    p = tmp_path / "mix.fa"
+    p.write_bytes(b"\n" + b"".join(out))
+    digest = {}
+    for mode in ("fast", "lines"):
+        env = dict(os.environ)
+        env.pop("MC_PARSE_LINES", None)
+        if mode == "lines":
+            env["MC_PARSE_LINES"] = "1"
+        res = subprocess.run([sys.executable, "-c", _DIFF_SCRIPT, str(p), "8"], env=env, capture_output=True,
+                             text=True, check=True, cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        digest[mode] = res.stdout.strip()
+    assert digest["fast"] == digest["lines"]
