@@ -158,10 +158,23 @@ __device__ __forceinline__ void block_scan2(uint32_t a, uint32_t b, uint32_t *ea
 
 // One workgroup partitions f[0, n) (n > 16) exactly as std::__unguarded_partition_pivot;
 // returns the cut.  L / R: scratch for n positions each (global u32, or LDS u16 when f is the
-// LDS copy of a range of at most LMAX words).
+// LDS copy of a range of at most LMAX words).  Global ranges: `stg` (LDS, 2 ST * 8 words) stages
+// the stopper positions, `scnt` (LDS, 256 words) holds the pass's counts.
 template <typename PT, typename FP>
-__device__ int64_t partition_wg(FP f, int64_t n, PT *L, PT *R, uint32_t *s32, uint64_t *s64) {
+__device__ int64_t partition_wg(FP f, int64_t n, PT *L, PT *R, uint32_t *s32, uint64_t *s64,
+                                unsigned long long *prof = nullptr, SP_LDS uint32_t *stg = nullptr,
+                                SP_LDS uint32_t *scnt = nullptr) {
   const int t = threadIdx.x;
+  // (MC_SPLIT_PROFILE, global ranges: thread 0's realtime ticks in the median, the stopper pass,
+  // the bisection and the swaps, prof[8..11])
+  uint64_t tp = prof && t == 0 ? __builtin_amdgcn_s_memrealtime() : 0;
+  auto pmark = [&](int i) {
+    if (prof && t == 0) {
+      const uint64_t u = __builtin_amdgcn_s_memrealtime();
+      atomicAdd(&prof[8 + i], (unsigned long long)(u - tp));
+      tp = u;
+    }
+  };
   if (t == 0) {  // std::__move_median_to_first(first, first + 1, mid, last - 1)
     const uint64_t a = f[1], b = f[n / 2], c = f[n - 1];
     int64_t m;
@@ -172,6 +185,7 @@ __device__ int64_t partition_wg(FP f, int64_t n, PT *L, PT *R, uint32_t *s32, ui
     f[m] = x;
   }
   __syncthreads();
+  pmark(0);
   const uint64_t pk = f[0] >> 32;
   uint32_t CL, TL;
   if constexpr (sizeof(PT) == 2) {
@@ -192,39 +206,63 @@ __device__ int64_t partition_wg(FP f, int64_t n, PT *L, PT *R, uint32_t *s32, ui
       if (k <= pk) R[ol++] = (PT)i;
     }
   } else {
-    // global range: chunks of CPT words per thread, every load of a chunk in flight at once,
-    // stopper positions written chunk after chunk (so in order)
-    // (the next chunk's words are loaded before this chunk's scan: the scan's barriers wait for
-    // LDS only, so the loads stay in flight across it)
+    // global range: chunks of ST * CPT words, word e * ST + t of a chunk to thread t (every load
+    // of a chunk in flight at once, each load instruction 512 contiguous bytes per wave).  The
+    // stoppers are ranked in position order by ballots and a scan over the (e, wave) counts, staged
+    // in LDS (`stg`) and written out contiguously -- one coalesced store per 64 positions instead
+    // of a scattered 4-byte store per stopper.
+    // (the next chunk's words are loaded before this chunk's ranking: the barriers wait for LDS
+    // only, so the loads stay in flight across them)
     constexpr int CPT = 8;
+    constexpr uint32_t CH = (uint32_t)ST * CPT;
+    static_assert(CPT * SW == 128, "the (e, wave) counts are two per lane of one wave");
+    const int wv = __builtin_amdgcn_readfirstlane(wave_id()), lane = t & 63;
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;  // lanes below this one
     uint32_t bg = 0, bl = 0;  // stoppers before this chunk
     uint32_t kn[CPT];
 #pragma unroll
-    for (int e = 0; e < CPT; e++) kn[e] = (int64_t)t * CPT + e < n ? (uint32_t)(f[(int64_t)t * CPT + e] >> 32) : 0u;
-    for (int64_t c0 = 0; c0 < n; c0 += (int64_t)ST * CPT) {
-      const int64_t i0 = c0 + (int64_t)t * CPT;
+    for (int e = 0; e < CPT; e++) {
+      const int64_t i = (int64_t)e * ST + t;
+      kn[e] = i < n ? (uint32_t)(f[i] >> 32) : 0u;
+    }
+    for (int64_t c0 = 0; c0 < n; c0 += (int64_t)CH) {
       uint32_t kk[CPT];
 #pragma unroll
       for (int e = 0; e < CPT; e++) kk[e] = kn[e];
-      const int64_t i1 = i0 + (int64_t)ST * CPT;
-#pragma unroll
-      for (int e = 0; e < CPT; e++) kn[e] = i1 + e < n ? (uint32_t)(f[i1 + e] >> 32) : 0u;
-      uint32_t mg = 0, ml = 0;
-#pragma unroll
-      for (int e = 0; e < CPT; e++)
-        if (i0 + e < n) {
-          mg |= (i0 + e >= 1 && kk[e] >= pk) ? 1u << e : 0u;
-          ml |= kk[e] <= pk ? 1u << e : 0u;
-        }
-      uint32_t og, ol, tg, tl;
-      block_scan2((uint32_t)__popc(mg), (uint32_t)__popc(ml), &og, &ol, &tg, &tl, s32);
-      og += bg;
-      ol += bl;
 #pragma unroll
       for (int e = 0; e < CPT; e++) {
-        if (mg >> e & 1) L[og++] = (PT)(i0 + e);
-        if (ml >> e & 1) R[ol++] = (PT)(i0 + e);
+        const int64_t i = c0 + CH + (int64_t)e * ST + t;
+        kn[e] = i < n ? (uint32_t)(f[i] >> 32) : 0u;
       }
+      uint64_t bL[CPT], bR[CPT];
+#pragma unroll
+      for (int e = 0; e < CPT; e++) {
+        const int64_t i = c0 + (int64_t)e * ST + t;
+        bL[e] = __ballot(i < n && i >= 1 && kk[e] >= pk);
+        bR[e] = __ballot(i < n && kk[e] <= pk);
+        if (lane == 0) {
+          scnt[e * SW + wv] = (uint32_t)__popcll(bL[e]);
+          scnt[CPT * SW + e * SW + wv] = (uint32_t)__popcll(bR[e]);
+        }
+      }
+      __syncthreads();
+      // exclusive offsets of the (e, wave) groups in position order, by every wave
+      const uint32_t a0 = scnt[2 * lane], a1 = scnt[2 * lane + 1];
+      const uint32_t b0 = scnt[CPT * SW + 2 * lane], b1 = scnt[CPT * SW + 2 * lane + 1];
+      const uint32_t ia = wave_scan_incl(a0 + a1), ib = wave_scan_incl(b0 + b1);
+      const uint32_t tg = (uint32_t)__builtin_amdgcn_readlane((int)ia, 63), tl = (uint32_t)__builtin_amdgcn_readlane((int)ib, 63);
+      const uint32_t ma = (wv & 1) ? ia - a1 : ia - a0 - a1, mb = (wv & 1) ? ib - b1 : ib - b0 - b1;
+#pragma unroll
+      for (int e = 0; e < CPT; e++) {
+        const int src = (e * SW + wv) >> 1;
+        const uint32_t oa = (uint32_t)__builtin_amdgcn_readlane((int)ma, src), ob = (uint32_t)__builtin_amdgcn_readlane((int)mb, src);
+        const uint32_t i = (uint32_t)(c0 + (int64_t)e * ST + t);
+        if ((bL[e] >> lane) & 1) stg[oa + (uint32_t)__popcll(bL[e] & lt)] = i;
+        if ((bR[e] >> lane) & 1) stg[CH + ob + (uint32_t)__popcll(bR[e] & lt)] = i;
+      }
+      __syncthreads();
+      for (uint32_t j = t; j < tg; j += ST) L[bg + j] = (PT)stg[j];
+      for (uint32_t j = t; j < tl; j += ST) R[bl + j] = (PT)stg[CH + j];
       bg += tg;
       bl += tl;
     }
@@ -232,6 +270,7 @@ __device__ int64_t partition_wg(FP f, int64_t n, PT *L, PT *R, uint32_t *s32, ui
     TL = bl;
   }
   __syncthreads();
+  pmark(1);
   // K = the last k with l_k < r_k (l_k = L[k - 1], r_k = R[TL - k]); monotone in k: bisection
   // over (lo, hi) with P(lo) true, P(hi) false, ST probes per round
   const int64_t m = CL < TL ? CL : TL;
@@ -256,6 +295,7 @@ __device__ int64_t partition_wg(FP f, int64_t n, PT *L, PT *R, uint32_t *s32, ui
     hi = nhi;
   }
   const int64_t K = lo;
+  pmark(2);
   // the K independent swaps, four per thread in flight
   for (int64_t k0 = 1 + t; k0 <= K; k0 += 4 * ST) {
     uint32_t a[4], b[4];
@@ -281,6 +321,11 @@ __device__ int64_t partition_wg(FP f, int64_t n, PT *L, PT *R, uint32_t *s32, ui
   }
   const int64_t lk1 = K < (int64_t)CL ? (int64_t)L[K] : n, rK = K >= 1 ? (int64_t)R[TL - K] : n;
   __syncthreads();
+  pmark(3);
+  if (prof && t == 0) {
+    atomicAdd(&prof[12], (unsigned long long)n);
+    atomicAdd(&prof[13], (unsigned long long)K);
+  }
   return lk1 < rK ? lk1 : rK;
 }
 
@@ -296,8 +341,17 @@ constexpr int NCACHE = 512;
 // cut in every lane.  (The same stoppers, K, swaps and cut as partition_wg: the swaps are
 // disjoint, so their order does not matter.)
 constexpr int64_t WMAX = 2048;
-__device__ int64_t partition_wave(SP_LDS uint64_t *f, int64_t n, SP_LDS uint16_t *L, SP_LDS uint16_t *R) {
+__device__ int64_t partition_wave(SP_LDS uint64_t *f, int64_t n, SP_LDS uint16_t *L, SP_LDS uint16_t *R,
+                                  unsigned long long *prof = nullptr) {
   const int lane = threadIdx.x & 63;
+  uint64_t tp = prof && lane == 0 ? __builtin_amdgcn_s_memrealtime() : 0;
+  auto pmark = [&](int i) {  // (MC_SPLIT_PROFILE: prof[17..19] stoppers, bisection, swaps; [20] swaps)
+    if (prof && lane == 0) {
+      const uint64_t u = __builtin_amdgcn_s_memrealtime();
+      atomicAdd(&prof[17 + i], (unsigned long long)(u - tp));
+      tp = u;
+    }
+  };
   if (lane == 0) {  // std::__move_median_to_first(first, first + 1, mid, last - 1)
     const uint64_t a = f[1], b = f[n / 2], c = f[n - 1];
     int64_t m;
@@ -330,6 +384,7 @@ __device__ int64_t partition_wave(SP_LDS uint64_t *f, int64_t n, SP_LDS uint16_t
       TL += (uint32_t)__popcll(br);
     }
   }
+  pmark(0);
   // K = the last k with L[k - 1] < R[TL - k]: bracket (lo, hi), 64 probes per round
   const int64_t m = CL < TL ? CL : TL;
   int64_t lo = 0, hi = m + 1;
@@ -344,6 +399,7 @@ __device__ int64_t partition_wave(SP_LDS uint64_t *f, int64_t n, SP_LDS uint16_t
     hi = nhi;
   }
   const int64_t K = lo;
+  pmark(1);
   for (int64_t k = 1 + lane; k <= K; k += 64) {
     const uint32_t pa = L[k - 1], pb = R[TL - k];
     const uint64_t x = f[pa], y = f[pb];
@@ -351,6 +407,8 @@ __device__ int64_t partition_wave(SP_LDS uint64_t *f, int64_t n, SP_LDS uint16_t
     f[pb] = x;
   }
   const int64_t lk1 = K < (int64_t)CL ? (int64_t)L[K] : n, rK = K >= 1 ? (int64_t)R[TL - K] : n;
+  pmark(2);
+  if (prof && lane == 0) atomicAdd(&prof[20], (unsigned long long)K);
   return lk1 < rK ? lk1 : rK;
 }
 
@@ -361,6 +419,7 @@ __global__ __launch_bounds__(ST) void select_kernel(SelArgs a) {
   __shared__ SplitNode s_nd;
   __shared__ int32_t s_nn, s_idx;
   __shared__ SplitNode s_cache[NCACHE];
+  __shared__ uint32_t s_cnt[256];
   uint64_t *LW = s_dyn;                                       // LMAX words
   uint16_t *LL = reinterpret_cast<uint16_t *>(s_dyn + LMAX);  // LMAX + LMAX stopper positions
   uint16_t *LR = LL + LMAX;
@@ -455,17 +514,24 @@ __global__ __launch_bounds__(ST) void select_kernel(SelArgs a) {
         continue;
       }
       int64_t cut;
+      const uint64_t tp0 = a.prof && t == 0 ? __builtin_amdgcn_s_memrealtime() : 0;
       if (in_lds && n <= WMAX && !a.nowave) {
         if (t < 64) {
-          const int64_t c = partition_wave(fl, n, (SP_LDS uint16_t *)LL, (SP_LDS uint16_t *)LR);
+          const int64_t c = partition_wave(fl, n, (SP_LDS uint16_t *)LL, (SP_LDS uint16_t *)LR, a.prof);
           if (t == 0) s64[0] = (uint64_t)c;
         }
         __syncthreads();
         cut = x.lo + (int64_t)s64[0];
         __syncthreads();  // (s64 is partition_wg's scratch too)
+        if (a.prof && t == 0) {
+          atomicAdd(&a.prof[14], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - tp0));
+          atomicAdd(&a.prof[15], 1ull);
+          atomicAdd(&a.prof[16], (unsigned long long)n);
+        }
       } else {
         cut = x.lo + (in_lds ? partition_wg<uint16_t>(fl, n, LL, LR, s32, s64)
-                             : partition_wg<uint32_t>(fg, n, L + x.lo, R + x.lo, s32, s64));
+                             : partition_wg<uint32_t>(fg, n, L + x.lo, R + x.lo, s32, s64, a.prof,
+                                                    (SP_LDS uint32_t *)LW, (SP_LDS uint32_t *)s_cnt));
       }
       if (t == 0) {
         if (s_nn + 2 > a.maxnode) {
@@ -533,8 +599,8 @@ int launch_select(mc_ctx *c, uint64_t *d_words, uint64_t n, uint32_t *d_scr, Spl
   static const bool prof = getenv("MC_SPLIT_PROFILE") != nullptr;
   static unsigned long long *d_prof = nullptr;
   if (prof && !d_prof) {
-    MCG_CHECK(hipMalloc(&d_prof, 64));
-    MCG_CHECK(hipMemset(d_prof, 0, 64));
+    MCG_CHECK(hipMalloc(&d_prof, 256));
+    MCG_CHECK(hipMemset(d_prof, 0, 256));
   }
   SelArgs a;
   a.words = d_words;
@@ -556,13 +622,19 @@ int launch_select(mc_ctx *c, uint64_t *d_words, uint64_t n, uint32_t *d_scr, Spl
   select_kernel<<<ngroups, ST, SEL_LDS, c->stream>>>(a);
   MCG_CHECK(hipGetLastError());
   if (prof) {  // this call, in us summed over workgroups
-    unsigned long long h[8];
-    MCG_CHECK(hipMemcpyAsync(h, d_prof, 64, hipMemcpyDeviceToHost, c->stream));
-    MCG_CHECK(hipMemsetAsync(d_prof, 0, 64, c->stream));
+    unsigned long long h[32];
+    MCG_CHECK(hipMemcpyAsync(h, d_prof, 256, hipMemcpyDeviceToHost, c->stream));
+    MCG_CHECK(hipMemsetAsync(d_prof, 0, 256, c->stream));
     MCG_CHECK(hipStreamSynchronize(c->stream));
     fprintf(stderr, "[split] ngroups %u  sum over WGs (us): nodes %.0f lds-load %.0f leaf %.0f part-global %.0f (%llu) "
             "part-lds %.0f (%llu) writeback %.0f\n", ngroups, h[0] / 100.0, h[1] / 100.0, h[2] / 100.0, h[3] / 100.0,
             h[6], h[4] / 100.0, h[7], h[5] / 100.0);
+    if (h[6])
+      fprintf(stderr, "[split]   global partitions (us): median %.0f pass %.0f bisect %.0f swaps %.0f; words %llu swaps %llu\n",
+              h[8] / 100.0, h[9] / 100.0, h[10] / 100.0, h[11] / 100.0, h[12], h[13]);
+    if (h[15])
+      fprintf(stderr, "[split]   one-wave partitions (us): %.0f (%llu, words %llu): stoppers %.0f bisect %.0f swaps %.0f (%llu)\n",
+              h[14] / 100.0, h[15], h[16], h[17] / 100.0, h[18] / 100.0, h[19] / 100.0, h[20]);
   }
   return MC_OK;
 }
