@@ -146,6 +146,28 @@ static int download(T *h, const void *d, size_t count, hipStream_t s) {
   return MC_OK;
 }
 
+// One device region of a call's results copied to the context's pinned landing buffer (a plain
+// DMA; a pageable destination is staged by the runtime, one staged copy per download) and the
+// stream synchronized: the caller then copies the parts out of the returned host pointer.
+// nullptr after an allocation failure: the caller downloads the parts directly instead.
+static uint8_t *download_pinned(mc_ctx *c, const void *d, size_t bytes, hipStream_t s) {
+  if (bytes > c->h_dstage_cap) {
+    if (c->h_dstage) (void)hipHostFree(c->h_dstage);
+    c->h_dstage = nullptr;
+    c->h_dstage_cap = 0;
+    const size_t cap = std::max<size_t>(bytes, 1u << 20);
+    if (hipHostMalloc((void **)&c->h_dstage, cap, hipHostMallocDefault) != hipSuccess) {
+      (void)hipGetLastError();
+      c->h_dstage = nullptr;
+      return nullptr;
+    }
+    c->h_dstage_cap = cap;
+  }
+  if (hipMemcpyAsync(c->h_dstage, d, bytes, hipMemcpyDeviceToHost, s) != hipSuccess) return nullptr;
+  if (hipStreamSynchronize(s) != hipSuccess) return nullptr;
+  return c->h_dstage;
+}
+
 }  // namespace mcg
 
 using namespace mcg;
@@ -205,6 +227,7 @@ int mc_ctx_destroy(mc_ctx *c) {
     release(*b);
   if (c->h_scan) (void)hipHostFree(c->h_scan);
   if (c->h_stage) (void)hipHostFree(c->h_stage);
+  if (c->h_dstage) (void)hipHostFree(c->h_dstage);
   if (c->h_res) (void)hipHostFree(c->h_res);
   for (auto e : c->ev_pool) (void)hipEventDestroy(e);
   (void)hipEventDestroy(c->ev0);
@@ -1429,10 +1452,11 @@ int mc_update_iteration(mc_ctx *c, const uint32_t *centre_ids, uint32_t C, const
     c->h_umem.assign(members, members + nm);
   }
   TRY(upload(c, c->s_h, poff.data(), C + 1, c->stream));
-  TRY(ensure(c->flags_out, (size_t)C * 4 + 16));
+  // results in one region of s_j: combo0 (m doubles) | similar (m bytes) | new centres (C words)
+  const size_t o_new = (m * 9 + 15) / 16 * 16, res_bytes = o_new + (size_t)C * 4;
   TRY(ensure(c->s_i, m * 8 + 16));
-  TRY(ensure(c->s_j, m * 9 + 64));
-  uint32_t *d_new = (uint32_t *)c->flags_out.p;
+  TRY(ensure(c->s_j, res_bytes + 64));
+  uint32_t *d_new = (uint32_t *)((uint8_t *)c->s_j.p + o_new);
   uint32_t *d_pa = (uint32_t *)c->s_i.p, *d_pb = d_pa + m;
   double *d_c0 = (double *)c->s_j.p;
   uint8_t *d_sim = (uint8_t *)(d_c0 + m);
@@ -1441,11 +1465,19 @@ int mc_update_iteration(mc_ctx *c, const uint32_t *centre_ids, uint32_t C, const
   if (m) {
     TRY(launch_merge_pairs(c, d_new, C, (const uint64_t *)c->s_h.p, d_pa, d_pb));
     TRY(launch_pairs(c, d_pa, d_pb, m, nullptr, 0, nullptr, d_sim, d_c0, nullptr, true));
-    if (similar) TRY(download(similar, d_sim, m, c->stream));
-    if (combo0) TRY(download(combo0, d_c0, m, c->stream));
   }
-  TRY(download(new_centre, d_new, C, c->stream));
-  MCG_CHECK(hipStreamSynchronize(c->stream));
+  // the whole result region in one copy to pinned memory (three pageable downloads were three
+  // staged copies per iteration)
+  if (const uint8_t *h = download_pinned(c, c->s_j.p, res_bytes, c->stream)) {
+    if (m && combo0) memcpy(combo0, h, m * 8);
+    if (m && similar) memcpy(similar, h + m * 8, m);
+    memcpy(new_centre, h + o_new, (size_t)C * 4);
+  } else {
+    if (m && similar) TRY(download(similar, d_sim, m, c->stream));
+    if (m && combo0) TRY(download(combo0, d_c0, m, c->stream));
+    TRY(download(new_centre, d_new, C, c->stream));
+    MCG_CHECK(hipStreamSynchronize(c->stream));
+  }
   flush_timers(c);
   *npairs = m;
   return MC_OK;

@@ -105,6 +105,8 @@ struct mc_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   uint8_t *h_stage = nullptr;  // pinned staging ring for small uploads (abi.hip upload)
+  uint8_t *h_dstage = nullptr;  // pinned landing buffer for a call's results (abi.hip download_pinned)
+  size_t h_dstage_cap = 0;
   size_t stage_off = 0;
   // sequences
   uint64_t n = 0;
