@@ -10,6 +10,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <initializer_list>
 #include <map>
 #include <mutex>
 #include <string>
@@ -146,6 +147,43 @@ static int download(T *h, const void *d, size_t count, hipStream_t s) {
   return MC_OK;
 }
 
+struct DPart {  // one result of a call: `bytes` from device `d` to host `h` (h null: not wanted)
+  void *h;
+  const void *d;
+  size_t bytes;
+};
+static uint8_t *download_pinned(mc_ctx *c, const void *d, size_t bytes, hipStream_t s);
+// A call's results through the pinned landing buffer: one DMA per part into it, one stream
+// synchronize, then the host copies (every part a pageable download was a runtime-staged copy).
+// Ends with the stream synchronized, as the direct downloads it replaces did.
+static int download_parts(mc_ctx *c, std::initializer_list<DPart> parts, hipStream_t s) {
+  size_t total = 0;
+  for (const DPart &p : parts)
+    if (p.h && p.bytes) total += (p.bytes + 255) / 256 * 256;
+  bool pinned = total > 0 && (c->h_dstage_cap >= total || download_pinned(c, nullptr, total, s) != nullptr);
+  if (pinned) {
+    size_t off = 0;
+    for (const DPart &p : parts)
+      if (p.h && p.bytes) {
+        MCG_CHECK(hipMemcpyAsync(c->h_dstage + off, p.d, p.bytes, hipMemcpyDeviceToHost, s));
+        off += (p.bytes + 255) / 256 * 256;
+      }
+  } else {
+    for (const DPart &p : parts)
+      if (p.h && p.bytes) MCG_CHECK(hipMemcpyAsync(p.h, p.d, p.bytes, hipMemcpyDeviceToHost, s));
+  }
+  MCG_CHECK(hipStreamSynchronize(s));
+  if (pinned) {
+    size_t off = 0;
+    for (const DPart &p : parts)
+      if (p.h && p.bytes) {
+        memcpy(p.h, c->h_dstage + off, p.bytes);
+        off += (p.bytes + 255) / 256 * 256;
+      }
+  }
+  return MC_OK;
+}
+
 // One device region of a call's results copied to the context's pinned landing buffer (a plain
 // DMA; a pageable destination is staged by the runtime, one staged copy per download) and the
 // stream synchronized: the caller then copies the parts out of the returned host pointer.
@@ -163,6 +201,7 @@ static uint8_t *download_pinned(mc_ctx *c, const void *d, size_t bytes, hipStrea
     }
     c->h_dstage_cap = cap;
   }
+  if (!d) return c->h_dstage;  // (download_parts: the buffer only)
   if (hipMemcpyAsync(c->h_dstage, d, bytes, hipMemcpyDeviceToHost, s) != hipSuccess) return nullptr;
   if (hipStreamSynchronize(s) != hipSuccess) return nullptr;
   return c->h_dstage;
@@ -509,9 +548,7 @@ int mc_split_select_words(mc_ctx *c, uint64_t nq, const uint32_t *arr, const uin
   timed_end(c, F_KEYS);
   std::vector<uint64_t> qout(nq);
   int err = 0;
-  MCG_CHECK(hipMemcpyAsync(qout.data(), dq + o_out, nq * 8, hipMemcpyDeviceToHost, c->stream));
-  MCG_CHECK(hipMemcpyAsync(&err, c->sp_err.p, 4, hipMemcpyDeviceToHost, c->stream));
-  MCG_CHECK(hipStreamSynchronize(c->stream));
+  TRY(download_parts(c, {{qout.data(), dq + o_out, nq * 8}, {&err, c->sp_err.p, 4}}, c->stream));
   flush_timers(c);
   if (err) {
     set_error("mc_split_select: more partitioned ranges than the device tree holds");
@@ -637,10 +674,7 @@ int mc_classify_pairs(mc_ctx *c, const uint32_t *a, const uint32_t *b, uint64_t 
   double *d_c0 = (double *)((char *)c->s_c.p + (m + 15) / 16 * 16);
   double *d_sum = d_c0 + m;
   TRY(launch_pairs(c, (uint32_t *)c->s_a.p, (uint32_t *)c->s_b.p, m, nullptr, 0, nullptr, d_sim, d_c0, d_sum, true));
-  if (similar) TRY(download(similar, d_sim, m, c->stream));
-  if (combo0) TRY(download(combo0, d_c0, m, c->stream));
-  if (sum) TRY(download(sum, d_sum, m, c->stream));
-  MCG_CHECK(hipStreamSynchronize(c->stream));
+  TRY(download_parts(c, {{similar, d_sim, m}, {combo0, d_c0, m * 8}, {sum, d_sum, m * 8}}, c->stream));
   flush_timers(c);
   return MC_OK;
 }
@@ -664,10 +698,7 @@ int mc_nw_identity(mc_ctx *c, const uint32_t *a, const uint32_t *b, uint64_t m, 
   int32_t *d_len = (int32_t *)(d_id + m), *d_ids = d_len + m;
   TRY(launch_nw(c, (uint8_t *)c->codes.p, (uint64_t *)c->seq_off.p, (uint32_t *)c->s_d.p, (uint8_t *)c->codes.p,
                 (uint64_t *)c->seq_off.p, (uint32_t *)c->s_e.p, m, la, lb, d_id, d_len, d_ids, nullptr));
-  TRY(download(ident, d_id, m, c->stream));
-  if (len) TRY(download(len, d_len, m, c->stream));
-  if (ids) TRY(download(ids, d_ids, m, c->stream));
-  MCG_CHECK(hipStreamSynchronize(c->stream));
+  TRY(download_parts(c, {{ident, d_id, m * 8}, {len, d_len, m * 4}, {ids, d_ids, m * 4}}, c->stream));
   flush_timers(c);
   return MC_OK;
 }
@@ -707,11 +738,7 @@ int mc_nw_identity_raw(mc_ctx *c, const uint8_t *a, const uint64_t *a_off, const
   MCG_CHECK(hipMemcpyAsync(dBo, bo.data(), (m + 1) * 8, hipMemcpyHostToDevice, c->stream));
   MCG_CHECK(hipMemcpyAsync(dI, idx.data(), m * 4, hipMemcpyHostToDevice, c->stream));
   TRY(launch_nw(c, dA, dAo, dI, dB, dBo, dI, m, la, lb, dId, dL, dIds, dSc));
-  TRY(download(ident, dId, m, c->stream));
-  if (len) TRY(download(len, dL, m, c->stream));
-  if (ids) TRY(download(ids, dIds, m, c->stream));
-  if (score) TRY(download(score, dSc, m, c->stream));
-  MCG_CHECK(hipStreamSynchronize(c->stream));
+  TRY(download_parts(c, {{ident, dId, m * 8}, {len, dL, m * 4}, {ids, dIds, m * 4}, {score, dSc, m * 4}}, c->stream));
   flush_timers(c);
   return MC_OK;
 }
@@ -1376,10 +1403,7 @@ int mc_classify_values(mc_ctx *c, const double *raw, uint64_t m, uint8_t *simila
   double *d_c0 = (double *)((char *)c->s_c.p + (m + 15) / 16 * 16);
   double *d_sum = d_c0 + m;
   TRY(launch_values(c, (const double *)c->s_a.p, m, d_sim, d_c0, d_sum));
-  if (similar) TRY(download(similar, d_sim, m, c->stream));
-  if (combo0) TRY(download(combo0, d_c0, m, c->stream));
-  if (sum) TRY(download(sum, d_sum, m, c->stream));
-  MCG_CHECK(hipStreamSynchronize(c->stream));
+  TRY(download_parts(c, {{similar, d_sim, m}, {combo0, d_c0, m * 8}, {sum, d_sum, m * 8}}, c->stream));
   flush_timers(c);
   return MC_OK;
 }
