@@ -1224,8 +1224,7 @@ int mc_accumulate(mc_ctx *c, const uint32_t *bin_lo, const uint64_t *bounds, uin
                    (uint64_t *)c->member_keys.p, (uint32_t *)c->s_f.p, (uint64_t *)c->s_g.p,
                    (uint64_t *)c->acc_out.p));
   uint64_t out[32];
-  MCG_CHECK(hipMemcpyAsync(out, c->acc_out.p, 256, hipMemcpyDeviceToHost, c->stream));
-  MCG_CHECK(hipStreamSynchronize(c->stream));
+  TRY(download_parts(c, {{out, c->acc_out.p, 256}}, c->stream));
   flush_timers(c);
   if (out[3]) {
     set_error(out[3] == 99 ? "device accumulation: hand-off timed out"
@@ -1238,13 +1237,30 @@ int mc_accumulate(mc_ctx *c, const uint32_t *bin_lo, const uint64_t *bounds, uin
     set_error("device accumulation produced an inconsistent partition");
     return MC_ERR_HIP;
   }
-  std::vector<uint32_t> pos(n);
-  std::vector<uint64_t> keys(n);
-  MCG_CHECK(hipMemcpyAsync(centre_ids, c->s_f.p, ncl * 4, hipMemcpyDeviceToHost, c->stream));
-  MCG_CHECK(hipMemcpyAsync(member_off, c->s_g.p, (ncl + 1) * 8, hipMemcpyDeviceToHost, c->stream));
-  MCG_CHECK(hipMemcpyAsync(pos.data(), c->members.p, n * 4, hipMemcpyDeviceToHost, c->stream));
-  MCG_CHECK(hipMemcpyAsync(keys.data(), c->member_keys.p, n * 8, hipMemcpyDeviceToHost, c->stream));
-  MCG_CHECK(hipStreamSynchronize(c->stream));
+  // the partition through the pinned landing buffer (keys and positions are read in place)
+  std::vector<uint32_t> pos_v;
+  std::vector<uint64_t> keys_v;
+  const uint32_t *pos = nullptr;
+  const uint64_t *keys = nullptr;
+  {
+    const size_t bk = (n * 8 + 255) / 256 * 256, bp = (n * 4 + 255) / 256 * 256;
+    if (uint8_t *L = download_pinned(c, nullptr, bk + bp, c->stream)) {
+      MCG_CHECK(hipMemcpyAsync(L, c->member_keys.p, n * 8, hipMemcpyDeviceToHost, c->stream));
+      MCG_CHECK(hipMemcpyAsync(L + bk, c->members.p, n * 4, hipMemcpyDeviceToHost, c->stream));
+      keys = reinterpret_cast<const uint64_t *>(L);
+      pos = reinterpret_cast<const uint32_t *>(L + bk);
+    } else {
+      pos_v.resize(n);
+      keys_v.resize(n);
+      MCG_CHECK(hipMemcpyAsync(pos_v.data(), c->members.p, n * 4, hipMemcpyDeviceToHost, c->stream));
+      MCG_CHECK(hipMemcpyAsync(keys_v.data(), c->member_keys.p, n * 8, hipMemcpyDeviceToHost, c->stream));
+      pos = pos_v.data();
+      keys = keys_v.data();
+    }
+    MCG_CHECK(hipMemcpyAsync(centre_ids, c->s_f.p, ncl * 4, hipMemcpyDeviceToHost, c->stream));
+    MCG_CHECK(hipMemcpyAsync(member_off, c->s_g.p, (ncl + 1) * 8, hipMemcpyDeviceToHost, c->stream));
+    MCG_CHECK(hipStreamSynchronize(c->stream));
+  }
   // `current` order: the seed, then each step's flagged candidates in bvec order -- each
   // cluster's members sorted by key, clusters split over a few host threads by member count
   auto order_clusters = [&](uint64_t k0, uint64_t k1) {
