@@ -637,11 +637,13 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
       }
     }
     for (uint32_t j = 0; j < C; j++) cids[j] = part[j].centre;
+    uint64_t it_update_evals = 0;
     for (uint32_t j = 0; j < C; j++) {
       uint32_t b = j >= (uint32_t)cfg.delta ? j - cfg.delta : 0;
       uint32_t e = std::min<uint32_t>(j + cfg.delta, C - 1);
-      stats.update_evals += off[e + 1] - off[b];
+      it_update_evals += off[e + 1] - off[b];
     }
+    stats.update_evals += it_update_evals;
     if (C && !memo && multi && split_update == 1) {
       // this rank's share of the centres, then the centre-reassignment all-gather
       const uint32_t W = (uint32_t)cfg.comm->world, per = (C + W - 1) / W;
@@ -712,7 +714,11 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
       check(mc_mean_shift_select(ctx, cids.data(), C, off.data(), members.data(), cfg.delta, keep.data(), newc.data()),
             "mc_mean_shift_select");
     }
-    for (uint32_t j = 0; j < C; j++) part[j].centre = newc[j];
+    bool moved = false;  // some centre changed in this iteration's mean shift
+    for (uint32_t j = 0; j < C; j++) {
+      moved |= newc[j] != part[j].centre;
+      part[j].centre = newc[j];
+    }
     std::vector<uint32_t> pa, pb;
     std::vector<uint64_t> poff(C + 1, 0);
     for (uint32_t i = 0; i < C; i++) {
@@ -753,10 +759,24 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
         c0[idx[r]] = c2[r];
       }
     }
-    Scope sc(timer, "update.cascade");
-    merge_cascade(part, poff, sim, c0);
+    {
+      Scope sc(timer, "update.cascade");
+      merge_cascade(part, poff, sim, c0);
+    }
     rebuild = part.size() != C;
     if (it == 0) t_first = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_it0).count();
+    // A fixed point: no centre moved and nothing merged (a merge always deletes a cluster), so
+    // the state -- every cluster's centre and members -- is what this iteration started from, and
+    // each remaining iteration (a deterministic function of that state: the same mean shifts,
+    // the same merge pairs, no merge) would leave it unchanged again.  Their evaluations are
+    // counted as if run.  (Alignment mode keeps running them: its memo lookups count hits.)
+    if (!memo && !moved && !rebuild && !getenv("MC_UPDATE_ALL_ITERATIONS")) {
+      const uint64_t rest = (uint64_t)(cfg.iterations - 1 - it);
+      stats.update_evals += rest * it_update_evals;
+      stats.merge_evals += rest * (uint64_t)pa.size();
+      stats.update_iters_fixed = rest;
+      break;
+    }
   }
   if (multi && !memo)
     stats.update_path = split_update == 1 ? "split x" + std::to_string(cfg.comm->world) : "replicated";

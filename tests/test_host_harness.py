@@ -49,3 +49,29 @@ def test_e2e_nw_lookahead_depth(harness, name, look, tmp_path):
     assert r.returncode == 0, r.stderr[-2000:]
     with gzip.open(fixtures.golden("e2e_%s.clstr.gz" % name), "rb") as f:
         assert out.read_bytes() == f.read()
+
+
+@pytest.mark.parametrize("name", ["fam2k", "noisy2k", "m2k_id80", "b3k300"])
+def test_update_stops_at_fixed_point(harness, name, tmp_path):
+    """The update loop (ClusterFactory.cpp:737-752) ends at a fixed point -- no centre moved and
+    nothing merged, so every remaining iteration would find the same state -- and counts the
+    iterations it leaves out: the .clstr (pinned to the reference above) and the evaluation
+    counts equal a run of every iteration (MC_UPDATE_ALL_ITERATIONS=1)."""
+    import json
+    fa, flags = fixtures.e2e_input(name, tmp_path)
+    got = {}
+    for mode in ("fixed", "all"):
+        env = dict(os.environ)
+        env.pop("MC_UPDATE_ALL_ITERATIONS", None)
+        if mode == "all":
+            env["MC_UPDATE_ALL_ITERATIONS"] = "1"
+        out, js = tmp_path / (mode + ".clstr"), tmp_path / (mode + ".json")
+        r = subprocess.run([harness, fa] + flags + ["--output", str(out), "--stats-json", str(js), "--quiet"],
+                           capture_output=True, text=True, timeout=900, env=env)
+        assert r.returncode == 0, r.stderr[-2000:]
+        got[mode] = (out.read_bytes(), json.load(open(js)))
+    assert got["fixed"][0] == got["all"][0]
+    for k in ("update_evals", "merge_evals", "clusters"):
+        assert got["fixed"][1][k] == got["all"][1][k], k
+    assert got["all"][1]["update_iters_fixed"] == 0
+    assert got["fixed"][1]["update_iters_fixed"] > 0
