@@ -372,7 +372,9 @@ def main():
                                  "frac": round(kb / ks / 1e9 / HBM_PEAK_GBS, 4),
                                  "traffic": kernel_pmc("kmer_kernel<unsigned char") if width == 1 and a.workload == "B" else None}
     if fam_n["mean_shift"]:
-        mb = sum(s["update_evals"] for s in stats) * (B * width + 16) / fam_n["mean_shift"] / (world if shard else 1)
+        # (the evaluations of the update iterations actually run: a fixed point ends the loop early)
+        mb = sum(s.get("update_evals_run", s["update_evals"]) for s in stats) * (B * width + 16) / fam_n["mean_shift"] \
+            / (world if shard else 1)
         ms = fam_ms["mean_shift"] / fam_n["mean_shift"] / 1e3
         others["mean_shift_kernel"] = {"bound": "hbm", "bytes_per_member": B * width + 16,
                                        "algorithmic_bytes_per_launch": round(mb), "avg_launch_us": round(ms * 1e6, 2),
@@ -448,6 +450,9 @@ def main():
                   "host_phases_ms": s0["phases_ms"], "accum_path": s0.get("accum_path"),
                   "comm_ms_per_step": comm_summary(stats),
                   "warmup_s": round(first_s, 3), "scan_steps": s0["scan_steps"],
+                  # (the reference's default --iterations 15; bench passes none)
+                  "update_iterations": {"run": 15 - s0.get("update_iters_fixed", 0),
+                                        "fixed_point_left_out": s0.get("update_iters_fixed", 0)},
                   "rehearsal_one_gpu": one_gpu},
     }
     if cpu is None and world == 1 and a.workload != "B":

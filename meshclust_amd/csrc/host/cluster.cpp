@@ -644,6 +644,7 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
       it_update_evals += off[e + 1] - off[b];
     }
     stats.update_evals += it_update_evals;
+    stats.update_evals_run += it_update_evals;
     if (C && !memo && multi && split_update == 1) {
       // this rank's share of the centres, then the centre-reassignment all-gather
       const uint32_t W = (uint32_t)cfg.comm->world, per = (C + W - 1) / W;

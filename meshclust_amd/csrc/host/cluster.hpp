@@ -45,6 +45,7 @@ struct ClusterStats {
   uint64_t update_evals = 0;     // filter evaluations in the mean-shift updates
   uint64_t merge_evals = 0;
   uint64_t update_iters_fixed = 0;  // update iterations left out at a fixed point (counted, not run)
+  uint64_t update_evals_run = 0;    // update_evals of the iterations actually run
   uint64_t nw_pairs = 0, nw_cells = 0;  // training alignments
   uint64_t align_nw_pairs = 0, align_nw_cells = 0;  // alignment mode: classifier alignments
   // which accumulation loop ran: "device" (mc_accumulate, one persistent kernel) or "steps"

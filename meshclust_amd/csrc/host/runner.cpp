@@ -328,6 +328,7 @@ std::string stats_json(const RunResult &rr, double parse_ms, double write_ms) {
   o += ", \"accum_path\": \"" + rr.stats.accum_path + "\"";
   if (!rr.stats.update_path.empty()) o += ", \"update_path\": \"" + rr.stats.update_path + "\"";
   o += ", \"update_iters_fixed\": " + std::to_string(rr.stats.update_iters_fixed);
+  o += ", \"update_evals_run\": " + std::to_string(rr.stats.update_evals_run);
   o += ", \"phases_ms\": {";
   for (size_t i = 0; i < rr.timer.order.size(); i++) {
     snprintf(b, sizeof b, "%s\"%s\": %.3f", i ? ", " : "", rr.timer.order[i].c_str(), rr.timer.ms.at(rr.timer.order[i]));
