@@ -14,6 +14,7 @@
 #include <condition_variable>
 #include <exception>
 #include <mutex>
+#include <memory>
 #include <thread>
 #include <cstdio>
 #include <cstdlib>
@@ -263,17 +264,19 @@ RunResult run_pipeline(const Dataset &ds, mc_ctx *ctx, Options opt, bool upload,
   tc.verbose = verbose;
   tc.comm = comm;
   Trainer tr(ds, ctx, tc, rr.timer);
-  // The bvec (Runner.cpp:345-350: insert every point, insert_finalize) depends only on the
-  // lengths, so a host thread builds it while the trainer runs, with a quarter of the
-  // cores (the trainer's teams keep the rest); its time overlaps "train".
-  BVec bv(ds.lengths, 1000);
+  // The bvec (Runner.cpp:345-350: construct, insert every point, insert_finalize) depends only
+  // on the lengths, so a host thread builds it while the trainer runs, with a quarter of the
+  // cores (the trainer's teams keep the rest); its time -- the constructor's length sort
+  // included -- overlaps "train".
+  std::unique_ptr<BVec> bvp;
   double bvec_ms = 0;
   std::exception_ptr bvec_err;
   std::thread bvec_thread([&]() {
     try {
       const auto b0 = std::chrono::steady_clock::now();
-      for (uint32_t id = 0; id < ds.size(); id++) bv.insert(id);
-      bv.insert_finalize(std::max(1, threads / 4));
+      bvp.reset(new BVec(ds.lengths, 1000));
+      for (uint32_t id = 0; id < ds.size(); id++) bvp->insert(id);
+      bvp->insert_finalize(std::max(1, threads / 4));
       bvec_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - b0).count();
     } catch (...) {
       bvec_err = std::current_exception();
@@ -303,7 +306,7 @@ RunResult run_pipeline(const Dataset &ds, mc_ctx *ctx, Options opt, bool upload,
   cc.align = opt.align;
   cc.width = rr.width;
   cc.comm = comm;
-  rr.part = mean_shift_cluster(ds, ctx, bv, cc, rr.timer, rr.stats);
+  rr.part = mean_shift_cluster(ds, ctx, *bvp, cc, rr.timer, rr.stats);
   rr.stats.nw_pairs = tr.nw_pairs;
   rr.stats.nw_cells = tr.nw_cells;
   rr.timer.add("total_pipeline",
