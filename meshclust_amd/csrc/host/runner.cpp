@@ -236,6 +236,18 @@ RunResult run_pipeline(const Dataset &ds, mc_ctx *ctx, Options opt, bool upload,
   if (opt.k < 1 || opt.k > 12) throw Error("k must be in 1..12 on this engine (4^k-bin dense histograms)", 1);
   rr.k = opt.k;
   auto t0 = std::chrono::steady_clock::now();
+  // split's first sort (ids by length) depends on the lengths alone: a host thread computes it
+  // while the upload and K1 run (k-mer mode; joined before the trainer starts)
+  std::vector<uint32_t> len_order;
+  std::thread len_thread;
+  if (!opt.align && opt.similarity >= 0.6)
+    len_thread = std::thread([&]() { len_order = Trainer::length_order(ds, threads); });
+  struct JoinLen {
+    std::thread &t;
+    ~JoinLen() {
+      if (t.joinable()) t.join();
+    }
+  } join_len{len_thread};
   fault_point(comm, "upload");
   if (upload) {
     Scope s(rr.timer, "upload");
@@ -263,6 +275,8 @@ RunResult run_pipeline(const Dataset &ds, mc_ctx *ctx, Options opt, bool upload,
   tc.threads = threads;
   tc.verbose = verbose;
   tc.comm = comm;
+  if (len_thread.joinable()) len_thread.join();
+  tc.length_order = std::move(len_order);
   Trainer tr(ds, ctx, tc, rr.timer);
   // The bvec (Runner.cpp:345-350: construct, insert every point, insert_finalize) depends only
   // on the lengths, so a host thread builds it while the trainer runs, with a quarter of the

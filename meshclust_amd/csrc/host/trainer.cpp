@@ -93,6 +93,28 @@ void Trainer::nw_batch(const std::vector<PairId> &pairs, std::vector<double> &id
   check(mc_nw_identity(ctx_, a.data(), b.data(), pairs.size(), ident.data(), nullptr, nullptr), "mc_nw_identity");
 }
 
+std::vector<uint32_t> Trainer::length_order(const Dataset &ds, int threads) {
+  const size_t N = ds.size();
+  std::vector<uint32_t> points(N);
+  for (size_t i = 0; i < N; i++) points[i] = (uint32_t)i;
+  bool wide = false;
+  for (size_t t = 0; t < N; t++) wide |= ds.lengths[t] >> 32 != 0;
+  if (wide) {
+    std::sort(points.begin(), points.end(),
+              [&](uint32_t a, uint32_t b) { return ds.lengths[a] < ds.lengths[b]; });  // Trainer.cpp:672-675
+  } else {
+    // std::sort with a key-only comparator on (key << 32 | id) words: LazyIntroSort::sort_words
+    // performs the same partitions and leaves (so the same permutation, ties included)
+    std::vector<uint64_t> w(N);
+    for (size_t t = 0; t < N; t++) w[t] = ((uint64_t)ds.lengths[t] << 32) | t;
+#pragma omp parallel num_threads(threads)
+#pragma omp single
+    LazyIntroSort::sort_words(w.data(), (int64_t)w.size());
+    for (size_t t = 0; t < N; t++) points[t] = (uint32_t)w[t];
+  }
+  return points;
+}
+
 // Trainer::split (Trainer.cpp:653-783)
 std::vector<PairId> Trainer::split() {
   const size_t N = ds_.size();
@@ -116,16 +138,8 @@ std::vector<PairId> Trainer::split() {
       LazyIntroSort::sort_words(w.data(), (int64_t)w.size());
     };
     std::vector<uint64_t> w(N);
-    bool wide = false;
-    for (size_t t = 0; t < N; t++) wide |= ds_.lengths[t] >> 32 != 0;
-    if (wide) {
-      std::sort(points.begin(), points.end(),
-                [&](uint32_t a, uint32_t b) { return ds_.lengths[a] < ds_.lengths[b]; });  // Trainer.cpp:672-675
-    } else {
-      for (size_t t = 0; t < N; t++) w[t] = ((uint64_t)ds_.lengths[t] << 32) | t;
-      exact_sort(w);
-      for (size_t t = 0; t < N; t++) points[t] = (uint32_t)w[t];
-    }
+    if (cfg_.length_order.size() == N) points = cfg_.length_order;
+    else points = length_order(ds_, cfg_.threads);
     uint32_t begin_pt = points[N / 2];
     std::vector<uint16_t> key0(N);
     check(mc_distance_keys(ctx_, &begin_pt, 1, all_ids.data(), N, key0.data()), "mc_distance_keys");

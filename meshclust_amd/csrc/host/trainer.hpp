@@ -28,6 +28,10 @@ struct TrainerConfig {
   // several ranks: each runs the sampler's binary searches of its block of pivots and its
   // share of the label alignments; the results are all-gathered (null / world 1: one rank)
   const ShardComm *comm = nullptr;
+  // the ids ordered by length as split's first std::sort leaves them (Trainer.cpp:672-675),
+  // computed ahead by the caller (Trainer::length_order, overlapping the upload and K1); empty:
+  // split computes it
+  std::vector<uint32_t> length_order;
 };
 
 class Trainer {
@@ -35,6 +39,8 @@ class Trainer {
   Trainer(const Dataset &ds, mc_ctx *ctx, const TrainerConfig &cfg, PhaseTimer &timer)
       : ds_(ds), ctx_(ctx), cfg_(cfg), timer_(timer) {}
   void train(double acc_cutoff = 97.5);
+  // split's first sort: the ids by length, exactly as std::sort leaves them
+  static std::vector<uint32_t> length_order(const Dataset &ds, int threads);
   mc_classifier classifier() const { return feat.to_classifier(weights); }
 
   FeatureSet feat;
