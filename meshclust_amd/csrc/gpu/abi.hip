@@ -1262,19 +1262,22 @@ int mc_accumulate(mc_ctx *c, const uint32_t *bin_lo, const uint64_t *bounds, uin
     MCG_CHECK(hipStreamSynchronize(c->stream));
   }
   // `current` order: the seed, then each step's flagged candidates in bvec order -- each
-  // cluster's members sorted by key, clusters split over a few host threads by member count
+  // cluster's members sorted by key, clusters split over a few host threads by member count.
+  // A key is step << 32 | position with step >= 1, or 0 for the cluster's seed: with the seed's
+  // key replaced by its position (< 2^32, so still first) one u64 sort orders a cluster and its
+  // low half is the position.
   auto order_clusters = [&](uint64_t k0, uint64_t k1) {
-    std::vector<std::pair<uint64_t, uint32_t>> tmp;
+    std::vector<uint64_t> tmp;
     for (uint64_t k = k0; k < k1; k++) {
       const uint64_t a = member_off[k], b = member_off[k + 1];
-      tmp.clear();
-      for (uint64_t i = a; i < b; i++) tmp.emplace_back(keys[i], pos[i]);
+      tmp.resize(b - a);
+      for (uint64_t i = a; i < b; i++) tmp[i - a] = keys[i] ? keys[i] : (uint64_t)pos[i];
       std::sort(tmp.begin(), tmp.end());
-      for (uint64_t i = a; i < b; i++) member_ids[i] = c->h_order[tmp[i - a].second];
+      for (uint64_t i = a; i < b; i++) member_ids[i] = c->h_order[(uint32_t)tmp[i - a]];
     }
   };
   {
-    const unsigned T = n >= 65536 ? std::min(8u, std::max(1u, std::thread::hardware_concurrency())) : 1u;
+    const unsigned T = n >= 65536 ? std::min(16u, std::max(1u, std::thread::hardware_concurrency())) : 1u;
     std::vector<uint64_t> cut(T + 1, ncl);
     cut[0] = 0;
     for (unsigned t = 1; t < T; t++) {  // first cluster whose members start at or after t/T of n

@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstring>
 #include <exception>
+#include <memory>
 #include <set>
 #include <thread>
 
@@ -93,6 +94,61 @@ void Trainer::nw_batch(const std::vector<PairId> &pairs, std::vector<double> &id
   check(mc_nw_identity(ctx_, a.data(), b.data(), pairs.size(), ident.data(), nullptr, nullptr), "mc_nw_identity");
 }
 
+// Header order of pair ids (the reference's std::set<pair<Point*, Point*>> comparators order
+// by Point::get_header, Trainer.cpp:653-667 / 264-269): each id's first 16 header bytes as two
+// big-endian words, so most comparisons are integer ones; equal prefixes of headers longer than
+// 16 bytes fall back to the full compare.  (string_view::compare is a memcmp: unsigned bytes,
+// a prefix first -- which the zero-padded words and then the lengths reproduce.)
+namespace {
+struct HdrKey {
+  uint64_t k0, k1;
+  uint32_t len, id;
+};
+HdrKey hdr_key(const Dataset &ds, uint32_t id) {
+  const std::string_view h = ds.headers[id];
+  unsigned char b[16] = {0};
+  memcpy(b, h.data(), h.size() < 16 ? h.size() : 16);
+  uint64_t w0 = 0, w1 = 0;
+  for (int i = 0; i < 8; i++) {
+    w0 = (w0 << 8) | b[i];
+    w1 = (w1 << 8) | b[8 + i];
+  }
+  return HdrKey{w0, w1, (uint32_t)std::min<size_t>(h.size(), 0xffffffffu), id};
+}
+int hdr_cmp(const Dataset &ds, const HdrKey &x, const HdrKey &y) {
+  if (x.k0 != y.k0) return x.k0 < y.k0 ? -1 : 1;
+  if (x.k1 != y.k1) return x.k1 < y.k1 ? -1 : 1;
+  if (x.len <= 16 && y.len <= 16) return x.len < y.len ? -1 : x.len > y.len ? 1 : 0;
+  const int c = ds.headers[x.id].compare(ds.headers[y.id]);
+  return c < 0 ? -1 : c > 0 ? 1 : 0;
+}
+// std::set<pair, header order>'s contents and order from inserting v[0], v[1], ... (what
+// insert keeps: the first of each run of equivalent elements): the indices of v in that order.
+// Each element carries its two ids' keys, so the sort reads no header for most comparisons.
+template <typename GetPair>
+std::vector<uint32_t> header_set_order(const Dataset &ds, size_t n, GetPair pair_of) {
+  struct E {
+    HdrKey a, b;
+    uint32_t idx;
+  };
+  std::vector<E> e(n);
+  for (size_t i = 0; i < n; i++) {
+    const PairId p = pair_of(i);
+    e[i] = E{hdr_key(ds, p.first), hdr_key(ds, p.second), (uint32_t)i};
+  }
+  auto cmp = [&](const E &x, const E &y) {
+    const int c = hdr_cmp(ds, x.a, y.a);
+    return c != 0 ? c : hdr_cmp(ds, x.b, y.b);
+  };
+  std::stable_sort(e.begin(), e.end(), [&](const E &x, const E &y) { return cmp(x, y) < 0; });
+  std::vector<uint32_t> out;
+  out.reserve(n);
+  for (size_t i = 0; i < n; i++)
+    if (i == 0 || cmp(e[i - 1], e[i]) != 0) out.push_back(e[i].idx);
+  return out;
+}
+}  // namespace
+
 std::vector<uint32_t> Trainer::length_order(const Dataset &ds, int threads) {
   const size_t N = ds.size();
   std::vector<uint32_t> points(N);
@@ -118,11 +174,7 @@ std::vector<uint32_t> Trainer::length_order(const Dataset &ds, int threads) {
 // Trainer::split (Trainer.cpp:653-783)
 std::vector<PairId> Trainer::split() {
   const size_t N = ds_.size();
-  auto hcmp = [&](const PairId &a, const PairId &b) {
-    int c = ds_.headers[a.first].compare(ds_.headers[b.first]);
-    return c < 0 || (c == 0 && ds_.headers[a.second].compare(ds_.headers[b.second]) < 0);
-  };
-  std::set<PairId, decltype(hcmp)> pairs(hcmp);
+  std::vector<PairId> pairs;  // the reference's header-ordered std::set (set_order below)
   std::vector<uint32_t> points(N);
   for (size_t i = 0; i < N; i++) points[i] = (uint32_t)i;
   std::vector<uint32_t> all_ids = points;  // distance keys are requested in id order
@@ -341,25 +393,28 @@ std::vector<PairId> Trainer::split() {
       }
     }
   }
+  Scope sp(timer_, "train.sample.pair_set");
   for (size_t i = 0; i < P; i++) {  // the warning flag keeps the serial loop's last writer
     double before_inc = (double)pivot[i] / to_add_each;
     double after_inc = ((double)(N - pivot[i])) / to_add_each;
     if (before_inc < 1) aerr = 1;
     else if (after_inc < 1) aerr = -1;
-    pairs.insert(bufs[i].begin(), bufs[i].end());
+    pairs.insert(pairs.end(), bufs[i].begin(), bufs[i].end());
+  }
+  {
+    const std::vector<uint32_t> ord = header_set_order(ds_, pairs.size(), [&](size_t i) { return pairs[i]; });
+    std::vector<PairId> set(ord.size());
+    for (size_t i = 0; i < ord.size(); i++) set[i] = pairs[ord[i]];
+    pairs.swap(set);
   }
   if (aerr < 0) fprintf(stderr, "Warning: Alignment may be too small for sampling\n");
   else if (aerr > 0) fprintf(stderr, "Warning: Alignment may be too large for sampling\n");
-  return std::vector<PairId>(pairs.begin(), pairs.end());
+  return pairs;
 }
 
 // Trainer::get_labels (Trainer.cpp:253-333).  random_shuffle only permutes the alignment
 // order; results land in header-ordered sets, so it has no effect and is skipped.
 void Trainer::get_labels(const std::vector<PairId> &vec, std::vector<Labeled> &bp, std::vector<Labeled> &bn) {
-  auto hcmp = [&](const Labeled &a, const Labeled &b) {
-    int c = ds_.headers[a.first.first].compare(ds_.headers[b.first.first]);
-    return c < 0 || (c == 0 && ds_.headers[a.first.second].compare(ds_.headers[b.first.second]) < 0);
-  };
   std::vector<double> al;
   {
     Scope s(timer_, "train.nw_labels");
@@ -390,10 +445,18 @@ void Trainer::get_labels(const std::vector<PairId> &vec, std::vector<Labeled> &b
       }
     }
   }
-  std::set<Labeled, decltype(hcmp)> buf_pos(hcmp), buf_neg(hcmp);
+  Scope sl(timer_, "train.label_sets");
+  // the reference's header-ordered std::set<pair<pair<Point*, Point*>, double>> per side
+  std::vector<Labeled> buf_pos, buf_neg;
   for (size_t i = 0; i < vec.size(); i++) {
-    if (al[i] >= cfg_.cutoff) buf_pos.insert({vec[i], al[i]});
-    else buf_neg.insert({vec[i], al[i]});
+    if (al[i] >= cfg_.cutoff) buf_pos.push_back({vec[i], al[i]});
+    else buf_neg.push_back({vec[i], al[i]});
+  }
+  for (std::vector<Labeled> *v : {&buf_pos, &buf_neg}) {
+    const std::vector<uint32_t> ord = header_set_order(ds_, v->size(), [&](size_t i) { return (*v)[i].first; });
+    std::vector<Labeled> set(ord.size());
+    for (size_t i = 0; i < ord.size(); i++) set[i] = (*v)[ord[i]];
+    v->swap(set);
   }
   if (cfg_.verbose) printf("positive=%zu negative=%zu\n", buf_pos.size(), buf_neg.size());
   if (buf_pos.empty() || buf_neg.empty()) {
@@ -403,7 +466,7 @@ void Trainer::get_labels(const std::vector<PairId> &vec, std::vector<Labeled> &b
     throw ExitZero(m);
   }
   size_t m_size = std::min(buf_pos.size(), buf_neg.size());
-  std::vector<Labeled> vpos(buf_pos.begin(), buf_pos.end()), vneg(buf_neg.begin(), buf_neg.end());
+  std::vector<Labeled> &vpos = buf_pos, &vneg = buf_neg;
   bp = resize_vec(vpos, m_size, cfg_.cutoff, 1, 5);
   bn = resize_vec(vneg, m_size, 0.4, cfg_.cutoff, 5);
   if (cfg_.verbose) printf("positive=%zu negative=%zu\n", bp.size(), bn.size());
