@@ -141,6 +141,32 @@ static int upload(mc_ctx *c, Buf &b, const T *h, size_t count, hipStream_t s) {
   return MC_OK;
 }
 
+// launch helpers' small host arrays (nw.hip's bucket lists) through the same pinned ring
+int stage_h2d(mc_ctx *c, void *dst, const void *src, size_t bytes) {
+  if (!bytes) return MC_OK;
+  constexpr size_t STAGE = 8u << 20, SMALL = 1u << 20;
+  if (bytes <= SMALL && !getenv("MC_PAGEABLE_UPLOADS")) {
+    if (!c->h_stage && hipHostMalloc((void **)&c->h_stage, STAGE, hipHostMallocDefault) != hipSuccess) {
+      (void)hipGetLastError();
+      c->h_stage = nullptr;
+    }
+    if (c->h_stage) {
+      size_t off = (c->stage_off + 255) & ~(size_t)255;
+      if (off + bytes > STAGE) {
+        MCG_CHECK(hipStreamSynchronize(c->stream));
+        off = 0;
+      }
+      memcpy(c->h_stage + off, src, bytes);
+      MCG_CHECK(hipMemcpyAsync(dst, c->h_stage + off, bytes, hipMemcpyHostToDevice, c->stream));
+      c->stage_off = off + bytes;
+      return MC_OK;
+    }
+  }
+  MCG_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
+  MCG_CHECK(hipStreamSynchronize(c->stream));  // (a pageable source may go out of scope)
+  return MC_OK;
+}
+
 template <typename T>
 static int download(T *h, const void *d, size_t count, hipStream_t s) {
   if (count) MCG_CHECK(hipMemcpyAsync(h, d, count * sizeof(T), hipMemcpyDeviceToHost, s));

@@ -196,6 +196,8 @@ int launch_distance_keys(mc_ctx *c, const uint32_t *d_piv, uint32_t npiv, const 
 constexpr int32_t SPLIT_MAXNODE = 32768;
 int split_build_words(mc_ctx *c, const uint32_t *d_order, uint64_t n, uint32_t npiv, const uint16_t *d_keys,
                       uint64_t *d_words);
+// a small host array to device memory through the context's pinned staging ring (abi.hip)
+int stage_h2d(mc_ctx *c, void *dst, const void *src, size_t bytes);
 int launch_select(mc_ctx *c, uint64_t *d_words, uint64_t n, uint32_t *d_scr, SplitNode *d_nodes, int32_t *d_nnodes,
                   int32_t maxnode, int32_t depth0, uint32_t ngroups, const uint32_t *d_qarr, const uint64_t *d_qoff,
                   const uint64_t *d_qpos, uint64_t *d_qout, int *d_err);

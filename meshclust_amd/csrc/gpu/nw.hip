@@ -669,10 +669,10 @@ int launch_nw(mc_ctx *c, const uint8_t *d_A, const uint64_t *d_aoff, const uint3
     char *base = (char *)c->nw_items.p;
     MCG_CHECK(hipMemsetAsync(base + ib + bb + 2 * ob, 0, 256, c->stream));
     const size_t n = total_ch;
-    MCG_CHECK(hipMemcpyAsync((uint32_t *)base, ch_pair.data(), n * 4, hipMemcpyHostToDevice, c->stream));
-    MCG_CHECK(hipMemcpyAsync((uint16_t *)(base + ib), ch_blk.data(), n * 2, hipMemcpyHostToDevice, c->stream));
-    MCG_CHECK(hipMemcpyAsync((uint64_t *)(base + ib + bb), ch_in.data(), n * 8, hipMemcpyHostToDevice, c->stream));
-    MCG_CHECK(hipMemcpyAsync((uint64_t *)(base + ib + bb + ob), ch_out.data(), n * 8, hipMemcpyHostToDevice, c->stream));
+    if (int rc = stage_h2d(c, base, ch_pair.data(), n * 4)) return rc;
+    if (int rc = stage_h2d(c, base + ib, ch_blk.data(), n * 2)) return rc;
+    if (int rc = stage_h2d(c, base + ib + bb, ch_in.data(), n * 8)) return rc;
+    if (int rc = stage_h2d(c, base + ib + bb + ob, ch_out.data(), n * 8)) return rc;
     NWPairs q{d_A, d_aoff, d_ai, d_B, d_boff, d_bi, (uint32_t *)base, (uint32_t)n, nullptr, nullptr,
               d_ident, d_len, d_ids, d_score, d_out};
     q.pblk = (const uint16_t *)(base + ib);
@@ -687,10 +687,8 @@ int launch_nw(mc_ctx *c, const uint8_t *d_A, const uint64_t *d_aoff, const uint3
   for (int k = 0; k < NB; k++) {
     if (bucket[k].empty()) continue;
     for (auto &v : boff[k]) v += so;
-    MCG_CHECK(hipMemcpyAsync((uint32_t *)c->s_a.p + io, bucket[k].data(), bucket[k].size() * 4, hipMemcpyHostToDevice,
-                             c->stream));
-    MCG_CHECK(hipMemcpyAsync((uint64_t *)c->s_b.p + io, boff[k].data(), boff[k].size() * 8, hipMemcpyHostToDevice,
-                             c->stream));
+    if (int rc = stage_h2d(c, (uint32_t *)c->s_a.p + io, bucket[k].data(), bucket[k].size() * 4)) return rc;
+    if (int rc = stage_h2d(c, (uint64_t *)c->s_b.p + io, boff[k].data(), boff[k].size() * 8)) return rc;
     NWPairs q{d_A, d_aoff, d_ai, d_B, d_boff, d_bi, (uint32_t *)c->s_a.p + io, (uint32_t)bucket[k].size(),
               (int *)c->s_c.p, (uint64_t *)c->s_b.p + io, d_ident, d_len, d_ids, d_score, d_out};
     int rc = MC_OK;
@@ -718,10 +716,10 @@ int launch_nw(mc_ctx *c, const uint8_t *d_A, const uint64_t *d_aoff, const uint3
     io += bucket[k].size();
     so += scratch[k];
   }
-  // keep the host vectors alive until the async copies have run
+  // (the host arrays went through the pinned ring: nothing here waits for the copies)
   timed_end(c, F_NW);
-  MCG_CHECK(hipStreamSynchronize(c->stream));
   if (total_ch) {
+    MCG_CHECK(hipStreamSynchronize(c->stream));
     const size_t ib = (total_ch * 4 + 255) / 256 * 256, bb = (total_ch * 2 + 255) / 256 * 256,
                  ob = (total_ch * 8 + 255) / 256 * 256;
     int herr = 0;
