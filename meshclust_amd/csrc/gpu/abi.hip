@@ -287,7 +287,7 @@ int mc_ctx_destroy(mc_ctx *c) {
   for (Buf *b : {&c->codes, &c->seq_off, &c->seg, &c->seg_off, &c->packed, &c->pk_off, &c->impure, &c->hist, &c->mag, &c->sumsq, &c->len, &c->order,
                  &c->alive, &c->members, &c->member_keys, &c->partials, &c->scan_dev, &c->flags_out, &c->s_a, &c->s_b,
                  &c->s_c, &c->s_d, &c->s_e, &c->s_f, &c->s_g, &c->s_h, &c->s_i, &c->s_j, &c->s_k, &c->hs, &c->mag_s, &c->sumsq_s, &c->len_s, &c->ticket,
-                 &c->msum, &c->ident_s, &c->al_a, &c->al_b, &c->al_out, &c->al_id, &c->acc_out, &c->sp_words, &c->sp_keys,
+                 &c->msum, &c->ident_s, &c->al_a, &c->al_b, &c->al_out, &c->al_id, &c->ord_ids, &c->acc_out, &c->sp_words, &c->sp_keys,
                  &c->sp_scr, &c->sp_nodes, &c->sp_nn, &c->sp_q, &c->sp_err, &c->u_off, &c->u_mem, &c->nw_items, &c->nw_gran})
     release(*b);
   if (c->h_scan) (void)hipHostFree(c->h_scan);
@@ -1263,59 +1263,28 @@ int mc_accumulate(mc_ctx *c, const uint32_t *bin_lo, const uint64_t *bounds, uin
     set_error("device accumulation produced an inconsistent partition");
     return MC_ERR_HIP;
   }
-  // the partition through the pinned landing buffer (keys and positions are read in place)
-  std::vector<uint32_t> pos_v;
-  std::vector<uint64_t> keys_v;
-  const uint32_t *pos = nullptr;
-  const uint64_t *keys = nullptr;
-  {
-    const size_t bk = (n * 8 + 255) / 256 * 256, bp = (n * 4 + 255) / 256 * 256;
-    if (uint8_t *L = download_pinned(c, nullptr, bk + bp, c->stream)) {
-      MCG_CHECK(hipMemcpyAsync(L, c->member_keys.p, n * 8, hipMemcpyDeviceToHost, c->stream));
-      MCG_CHECK(hipMemcpyAsync(L + bk, c->members.p, n * 4, hipMemcpyDeviceToHost, c->stream));
-      keys = reinterpret_cast<const uint64_t *>(L);
-      pos = reinterpret_cast<const uint32_t *>(L + bk);
-    } else {
-      pos_v.resize(n);
-      keys_v.resize(n);
-      MCG_CHECK(hipMemcpyAsync(pos_v.data(), c->members.p, n * 4, hipMemcpyDeviceToHost, c->stream));
-      MCG_CHECK(hipMemcpyAsync(keys_v.data(), c->member_keys.p, n * 8, hipMemcpyDeviceToHost, c->stream));
-      pos = pos_v.data();
-      keys = keys_v.data();
-    }
-    MCG_CHECK(hipMemcpyAsync(centre_ids, c->s_f.p, ncl * 4, hipMemcpyDeviceToHost, c->stream));
-    MCG_CHECK(hipMemcpyAsync(member_off, c->s_g.p, (ncl + 1) * 8, hipMemcpyDeviceToHost, c->stream));
-    MCG_CHECK(hipStreamSynchronize(c->stream));
-  }
-  // `current` order: the seed, then each step's flagged candidates in bvec order -- each
-  // cluster's members sorted by key, clusters split over a few host threads by member count.
-  // A key is step << 32 | position with step >= 1, or 0 for the cluster's seed: with the seed's
-  // key replaced by its position (< 2^32, so still first) one u64 sort orders a cluster and its
-  // low half is the position.
-  auto order_clusters = [&](uint64_t k0, uint64_t k1) {
-    std::vector<uint64_t> tmp;
-    for (uint64_t k = k0; k < k1; k++) {
-      const uint64_t a = member_off[k], b = member_off[k + 1];
-      tmp.resize(b - a);
-      for (uint64_t i = a; i < b; i++) tmp[i - a] = keys[i] ? keys[i] : (uint64_t)pos[i];
-      std::sort(tmp.begin(), tmp.end());
-      for (uint64_t i = a; i < b; i++) member_ids[i] = c->h_order[(uint32_t)tmp[i - a]];
-    }
-  };
-  {
-    const unsigned T = n >= 65536 ? std::min(16u, std::max(1u, std::thread::hardware_concurrency())) : 1u;
-    std::vector<uint64_t> cut(T + 1, ncl);
-    cut[0] = 0;
-    for (unsigned t = 1; t < T; t++) {  // first cluster whose members start at or after t/T of n
-      const uint64_t want = n * t / T;
-      cut[t] = (uint64_t)(std::lower_bound(member_off, member_off + ncl + 1, want) - member_off);
-      if (cut[t] > ncl) cut[t] = ncl;
-      if (cut[t] < cut[t - 1]) cut[t] = cut[t - 1];
-    }
-    std::vector<std::thread> th;
-    for (unsigned t = 1; t < T; t++) th.emplace_back(order_clusters, cut[t], cut[t + 1]);
-    order_clusters(cut[0], cut[1]);
-    for (auto &x : th) x.join();
+  // the partition: each cluster's members sorted on the device (order_members_kernel), then the
+  // ids, centres and offsets copied out through the pinned landing buffer; a cluster too large
+  // for the kernel is sorted here
+  TRY(ensure(c->ord_ids, n * 4 + 16));
+  TRY(launch_order_members(c, (const uint64_t *)c->member_keys.p, (const uint32_t *)c->members.p,
+                           (const uint64_t *)c->s_g.p, ncl, (uint32_t *)c->ord_ids.p));
+  TRY(download_parts(c, {{member_ids, c->ord_ids.p, n * 4}, {centre_ids, c->s_f.p, ncl * 4},
+                         {member_off, c->s_g.p, (ncl + 1) * 8}}, c->stream));
+  const uint64_t om = order_members_max();
+  for (uint64_t k = 0; k < ncl; k++) {
+    const uint64_t a = member_off[k], b = member_off[k + 1];
+    if (b - a <= om) continue;
+    // `current` order: a key is step << 32 | position with step >= 1, or 0 for the seed -- with
+    // the seed's key replaced by its position (< 2^32, so still first) one u64 sort orders it
+    std::vector<uint64_t> kk(b - a);
+    std::vector<uint32_t> pp(b - a);
+    TRY(download_parts(c, {{kk.data(), (const uint64_t *)c->member_keys.p + a, (b - a) * 8},
+                           {pp.data(), (const uint32_t *)c->members.p + a, (b - a) * 4}}, c->stream));
+    for (uint64_t i = 0; i < b - a; i++)
+      if (kk[i] == 0) kk[i] = pp[i];
+    std::sort(kk.begin(), kk.end());
+    for (uint64_t i = a; i < b; i++) member_ids[i] = c->h_order[(uint32_t)kk[i - a]];
   }
   for (uint64_t k = 0; k < ncl; k++) centre_ids[k] = c->h_order[centre_ids[k]];  // static positions -> ids
   *nclusters = ncl;

@@ -142,7 +142,7 @@ struct mc_ctx {
   // per-static-position identity the scan kernels classify
   std::vector<uint32_t> h_order;
   std::vector<uint8_t> h_alive;
-  mcg::Buf ident_s, al_a, al_b, al_out, al_id;
+  mcg::Buf ident_s, al_a, al_b, al_out, al_id, ord_ids;
   mcg::Buf acc_out;  // device-resident accumulation: counters / error word
   // Trainer::split's sorted arrays (mc_split_*): words, stopper scratch, range trees, queries
   mcg::Buf sp_words, sp_keys, sp_scr, sp_nodes, sp_nn, sp_q, sp_err;
@@ -196,6 +196,11 @@ int launch_distance_keys(mc_ctx *c, const uint32_t *d_piv, uint32_t npiv, const 
 constexpr int32_t SPLIT_MAXNODE = 32768;
 int split_build_words(mc_ctx *c, const uint32_t *d_order, uint64_t n, uint32_t npiv, const uint16_t *d_keys,
                       uint64_t *d_words);
+// each accumulation cluster's members sorted by key and mapped to ids (k2.hip); clusters of
+// more than order_members_max() members are left untouched
+int launch_order_members(mc_ctx *c, const uint64_t *d_keys, const uint32_t *d_pos, const uint64_t *d_cl_off, uint64_t ncl,
+                         uint32_t *d_ids);
+uint64_t order_members_max();
 // a small host array to device memory through the context's pinned staging ring (abi.hip)
 int stage_h2d(mc_ctx *c, void *dst, const void *src, size_t bytes);
 int launch_select(mc_ctx *c, uint64_t *d_words, uint64_t n, uint32_t *d_scr, SplitNode *d_nodes, int32_t *d_nnodes,

@@ -396,6 +396,10 @@ def test_devices_cli_gpu_default_env_replicated(name, tmp_path):
     stats = json.load(open(st))
     assert stats["accum_path"] == "device (replicated x2)", stats["accum_path"]
     assert stats["phases_ms"].get("gpu_share") == 2.0
-    assert stats["phases_ms"]["comm.update.calls"] >= 1
+    assert stats["phases_ms"]["comm.train.calls"] >= 1
+    # (the update exchanges from its second iteration on; a loop that reached its fixed point in
+    # the first, cluster.cpp, exchanged nothing there)
+    if 15 - stats["update_iters_fixed"] > 1:
+        assert stats["phases_ms"]["comm.update.calls"] >= 1
     with gzip.open(fixtures.golden("e2e_%s.clstr.gz" % name), "rb") as f:
         assert open(out, "rb").read() == f.read()
