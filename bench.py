@@ -189,8 +189,8 @@ def kernel_pmc(kname):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="B",
                     help="B: 100k x 1 kb (BASELINE configs[1]); D: 1M x 1 kb (configs[3])")
     ap.add_argument("--mode", choices=["auto", "shard", "replicas"], default="auto",
