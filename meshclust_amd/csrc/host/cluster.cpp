@@ -770,8 +770,10 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
     // the state -- every cluster's centre and members -- is what this iteration started from, and
     // each remaining iteration (a deterministic function of that state: the same mean shifts,
     // the same merge pairs, no merge) would leave it unchanged again.  Their evaluations are
-    // counted as if run.  (Alignment mode keeps running them: its memo lookups count hits.)
-    if (!memo && !moved && !rebuild && !getenv("MC_UPDATE_ALL_ITERATIONS")) {
+    // counted as if run.  (Alignment mode: the remaining iterations would look up the same pairs
+    // in the memo, every one of them aligned by now -- memo_lookup aligns only pairs it has not
+    // seen, and nothing else changes the memo during the updates -- so they would add nothing.)
+    if (!moved && !rebuild && !getenv("MC_UPDATE_ALL_ITERATIONS")) {
       const uint64_t rest = (uint64_t)(cfg.iterations - 1 - it);
       stats.update_evals += rest * it_update_evals;
       stats.merge_evals += rest * (uint64_t)pa.size();

@@ -51,7 +51,7 @@ def test_e2e_nw_lookahead_depth(harness, name, look, tmp_path):
         assert out.read_bytes() == f.read()
 
 
-@pytest.mark.parametrize("name", ["fam2k", "noisy2k", "m2k_id80", "b3k300"])
+@pytest.mark.parametrize("name", ["fam2k", "noisy2k", "m2k_id80", "b3k300", "al300", "c2k_al55"])
 def test_update_stops_at_fixed_point(harness, name, tmp_path):
     """The update loop (ClusterFactory.cpp:737-752) ends at a fixed point -- no centre moved and
     nothing merged, so every remaining iteration would find the same state -- and counts the
@@ -71,7 +71,8 @@ def test_update_stops_at_fixed_point(harness, name, tmp_path):
         assert r.returncode == 0, r.stderr[-2000:]
         got[mode] = (out.read_bytes(), json.load(open(js)))
     assert got["fixed"][0] == got["all"][0]
-    for k in ("update_evals", "merge_evals", "clusters"):
+    for k in ("update_evals", "merge_evals", "clusters", "align_nw_pairs", "align_nw_cells"):
         assert got["fixed"][1][k] == got["all"][1][k], k
     assert got["all"][1]["update_iters_fixed"] == 0
-    assert got["fixed"][1]["update_iters_fixed"] > 0
+    if not name.startswith(("al", "c2k")):  # (these k-mer inputs settle early; al300 never does)
+        assert got["fixed"][1]["update_iters_fixed"] > 0
