@@ -542,7 +542,12 @@ void parse_fasta_files(const std::vector<std::string> &files, Dataset &ds, int t
     }
     const char *buf = mem.get();
     // chunk starts: the first record start at or after t * n / T
-    const int T = (int)std::max<size_t>(1, std::min<size_t>((size_t)threads * 4, n / (1 << 16) + 1));
+    static const int per_thread = [] {  // MC_PARSE_CHUNKS_PER_THREAD (default 4)
+      const char *e = getenv("MC_PARSE_CHUNKS_PER_THREAD");
+      const int v = e ? atoi(e) : 4;
+      return v < 1 ? 1 : v > 64 ? 64 : v;
+    }();
+    const int T = (int)std::max<size_t>(1, std::min<size_t>((size_t)threads * per_thread, n / (1 << 16) + 1));
     std::vector<size_t> cut(T + 1, n);
     cut[0] = 0;
     for (int t = 1; t < T; t++) {
