@@ -79,11 +79,12 @@ def host_threads():
     return max(1, min(n, int(env))) if env and env.isdigit() else n
 
 
-def cpu_baseline(fasta, args, n_reads, threads, repeats, limit_s=600):
+def cpu_baseline(fasta, args, n_reads, threads, repeats, limit_s=600, binary="meshclust", march="x86-64-v4"):
     """The reference itself (oracle/_ref/meshclust, compiled from /root/reference by
-    oracle/Makefile) on the same FASTA on this host's cores, end to end (process start to
-    .clstr written), median of `repeats` runs."""
-    ref = os.path.join(ROOT, "oracle", "_ref", "meshclust")
+    oracle/Makefile with the reference's own flags, -march=native pinned to x86-64-v4: AVX-512)
+    on the same FASTA on this host's cores, end to end (process start to .clstr written),
+    median of `repeats` runs."""
+    ref = os.path.join(ROOT, "oracle", "_ref", binary)
     if not os.path.exists(ref):
         return None
     walls = []
@@ -103,8 +104,10 @@ def cpu_baseline(fasta, args, n_reads, threads, repeats, limit_s=600):
     dt = walls[len(walls) // 2]
     return {"value": round(n_reads / dt, 1), "unit": "sequences/s", "cores": threads, "kind": "reference",
             "sample": "the full workload (%d reads, the same FASTA), reference meshclust %s --threads %d, "
-                      "wall %s s (median of %d), parse to .clstr written"
-                      % (n_reads, " ".join(args), threads, "/".join("%.2f" % w for w in walls), len(walls)),
+                      "wall %s s (median of %d), parse to .clstr written; built -O3 -march=%s -fopenmp "
+                      "(src/cluster/Makefile's flags, -march=native pinned)"
+                      % (n_reads, " ".join(args), threads, "/".join("%.2f" % w for w in walls), len(walls), march),
+            "march": march,
             "cpu_model": cpu_model(), "host_cpus": os.cpu_count(), "threads": threads}
 
 
@@ -205,6 +208,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--stats-out", default=None)
     ap.add_argument("--keep-clstr", default=None, help="rank 0 keeps the last timed step's .clstr here")
+    ap.add_argument("--config-d-steps", type=int, default=2,
+                    help="with the config-B line: also time config D (1M reads, BASELINE configs[3], the workload "
+                         "that shards) at the same N, reported in extra.config_d (0: skip)")
+    ap.add_argument("--no-config-d", action="store_true", help="same as --config-d-steps 0")
     a = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and a.gpus > 1:
@@ -255,7 +262,7 @@ def main():
     nstep = [0]
     last_clstr = [None]
 
-    def one_step():
+    def one_step(fa):
         """parse -> upload -> GPU pipeline -> .clstr written (the BASELINE metric's work).
         Every run writes a new output file, as a clustering run does (rewriting one path would
         time the kernel freeing the previous run's page-cache pages on O_TRUNC: 2.5 ms for
@@ -264,7 +271,7 @@ def main():
         clstr = os.path.join(out_dir, "bench_rank%d_%d.clstr" % (rank, nstep[0]))
         last_clstr[0] = clstr
         t = time.perf_counter()
-        ds = M.Dataset([fasta], threads=threads)
+        ds = M.Dataset([fa], threads=threads)
         t1 = time.perf_counter()
         st = ds.run(eng, args, upload=True, clstr=clstr, comm=comm)
         t2 = time.perf_counter()
@@ -274,38 +281,57 @@ def main():
         st["free_s"] = time.perf_counter() - t2
         return st
 
-    # warm-up: end-to-end steps, then resident-data runs (sequences already in HBM)
-    t0 = time.perf_counter()
-    for _ in range(max(1, a.warmup)):
-        one_step()
-    first_s = time.perf_counter() - t0
-    ds_res = M.Dataset([fasta], threads=threads)
-    ds_res.run(eng, args, upload=True, comm=comm)
-    res_t = []
-    for _ in range(2):
-        t = time.perf_counter()
-        ds_res.run(eng, args, upload=False, comm=comm)
-        res_t.append(time.perf_counter() - t)
-    del ds_res
-    eng.timers(reset=True)
+    def timed(fa, steps, warmup, resident_runs):
+        """`warmup` untimed end-to-end steps (and `resident_runs` runs on sequences already in
+        HBM), then exactly `steps` timed steps bracketed by a barrier + device sync on both sides;
+        the elapsed time is the maximum over the ranks."""
+        t0 = time.perf_counter()
+        for _ in range(max(1, warmup)):
+            one_step(fa)
+        first = time.perf_counter() - t0
+        res = []
+        if resident_runs:
+            ds_res = M.Dataset([fa], threads=threads)
+            ds_res.run(eng, args, upload=True, comm=comm)
+            for _ in range(resident_runs):
+                t = time.perf_counter()
+                ds_res.run(eng, args, upload=False, comm=comm)
+                res.append(time.perf_counter() - t)
+            del ds_res
+        eng.timers(reset=True)
+        if dist:
+            dist.barrier()
+        sync()
+        t0 = time.perf_counter()
+        st = [one_step(fa) for _ in range(steps)]
+        sync()
+        if dist:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        tm = eng.timers()
+        if dist:
+            import torch as _t
+            t = _t.tensor([el], dtype=_t.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el, st, tm, first, res
 
-    if dist:
-        dist.barrier()
-    sync()
-    t0 = time.perf_counter()
-    stats = []
-    for _ in range(a.steps):
-        stats.append(one_step())
-    sync()
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    tim = eng.timers()
-    if dist:
-        import torch as _t
-        t = _t.tensor([elapsed], dtype=_t.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed, stats, tim, first_s, res_t = timed(fasta, a.steps, a.warmup, 2)
+    keep_src = last_clstr[0]
+
+    # config D at the same N (the workload that shards by record: BASELINE configs[3]), so the
+    # driver's 1 -> 8 GPU runs carry a config-D curve beside the config-B headline
+    d_run = None
+    d_steps = 0 if a.no_config_d or a.workload != "B" or replicas else a.config_d_steps
+    if d_steps > 0:
+        dn, dt_, ds_ = WORKLOADS["D"]
+        if rank == 0:
+            ensure_fasta(dn, a.len, dt_, a.mut, ds_)
+        if dist:
+            dist.barrier()
+        d_fa = ensure_fasta(dn, a.len, dt_, a.mut, ds_)
+        d_el, d_stats, d_tim, d_first, _ = timed(d_fa, d_steps, 1, 0)
+        d_run = (dn, dt_, ds_, d_el, d_stats, d_tim, d_first)
 
     if rank != 0:
         if comm is not None:
@@ -324,41 +350,51 @@ def main():
     fam_n = {f: v[1] for f, v in tim.items()}
     B = 4 ** s0["k"]
     width = s0["width"]
-    eval_bytes = B * width + 17  # row + length + magnitude + flag per candidate
-    scan_evals = sum(s["scan_candidates"] for s in stats)
     dominant = max(fam_ms, key=lambda f: fam_ms[f])
-    roof = None
-    acc_split = shard and str(s0.get("accum_path", "")).startswith("device x")  # (vs replicated)
-    if fam_n["scan"]:
+
+    def scan_roofline(stats, tim, steps, workload):
+        """accum_kernel's roofline: evaluations x (B*w + 17) algorithmic bytes per launch over
+        the launch's duration by HIP events on the library's stream."""
+        fms = {f: v[0] for f, v in tim.items()}
+        fn = {f: v[1] for f, v in tim.items()}
+        st0 = stats[-1]
+        eval_bytes = 4 ** st0["k"] * st0["width"] + 17  # row + length + magnitude + flag per candidate
+        scan_evals = sum(s["scan_candidates"] for s in stats)
+        acc_split = shard and str(st0.get("accum_path", "")).startswith("device x")  # (vs replicated)
+        if not fn["scan"]:
+            return None, acc_split
         # (accumulation split over the ranks: each rank's kernel scans its 1/world of every window)
-        per_launch_bytes = scan_evals * eval_bytes / fam_n["scan"] / (world if acc_split else 1)
-        avg_s = fam_ms["scan"] / fam_n["scan"] / 1e3
+        per_launch_bytes = scan_evals * eval_bytes / fn["scan"] / (world if acc_split else 1)
+        avg_s = fms["scan"] / fn["scan"] / 1e3
         ach = per_launch_bytes / avg_s / 1e9
         # one launch per clustering = the device-resident accumulation (accum.hip); otherwise
         # one fused scan launch per get_close step (scan.hip)
-        device_loop = fam_n["scan"] <= a.steps
+        device_loop = fn["scan"] <= steps
         kname = "accum_kernel<unsigned char" if device_loop else "fused_scan_kernel<unsigned char"
-        roof = {"kernel": ("accum_kernel (whole accumulation phase, %d dependent get_close steps per launch)"
-                           % s0["scan_steps"]) if device_loop else "fused_scan_kernel (Trainer::get_close step)",
-                "bound": "hbm", "achieved": round(ach, 1),
-                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
-                "bytes_per_eval": eval_bytes, "evals_per_launch": round(scan_evals / fam_n["scan"], 1),
-                "avg_launch_us": round(avg_s * 1e6, 2),
-                "us_per_step": round(fam_ms["scan"] * 1e3 / sum(s["scan_steps"] for s in stats), 2),
-                "note": ("priced against HBM by algorithmic bytes (SURVEY.md §8(d)); the rows stay in LDS, "
-                         "so the kernel is bound by its dependent step chain, not by HBM (DESIGN.md §3.1)")
-                        if a.workload == "B" else
-                        ("priced against HBM by algorithmic bytes (SURVEY.md §8(d)); on one to four GPUs "
-                         "the workers stream every window's rows from HBM (dense streaming form, DESIGN.md "
-                         "§3.1c); at eight each rank's share of the rows is LDS-resident (§6)")}
-        if device_loop and a.workload == "B":
-            roof["latency_floor"] = latency_floor(roof["us_per_step"], stats)
-        if a.workload == "B" and not shard and world == 1:  # (the counters are of the config-B launch)
+        r = {"kernel": ("accum_kernel (whole accumulation phase, %d dependent get_close steps per launch)"
+                        % st0["scan_steps"]) if device_loop else "fused_scan_kernel (Trainer::get_close step)",
+             "bound": "hbm", "achieved": round(ach, 1),
+             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+             "bytes_per_eval": eval_bytes, "evals_per_launch": round(scan_evals / fn["scan"], 1),
+             "avg_launch_us": round(avg_s * 1e6, 2),
+             "us_per_step": round(fms["scan"] * 1e3 / sum(s["scan_steps"] for s in stats), 2),
+             "note": ("priced against HBM by algorithmic bytes (SURVEY.md §8(d)); the rows stay in LDS, "
+                      "so the kernel is bound by its dependent step chain, not by HBM (DESIGN.md §3.1)")
+                     if workload == "B" else
+                     ("priced against HBM by algorithmic bytes (SURVEY.md §8(d)); on one to four GPUs "
+                      "the workers stream every window's rows from HBM (dense streaming form, DESIGN.md "
+                      "§3.1c); at eight each rank's share of the rows is LDS-resident (§6)")}
+        if device_loop and workload == "B":
+            r["latency_floor"] = latency_floor(r["us_per_step"], stats)
+        if workload == "B" and not shard and world == 1:  # (the counters are of the config-B launch)
             tr = kernel_pmc(kname)
             if tr is not None:
-                roof["traffic"] = tr
-                roof["traffic_unit"] = "bytes/launch (FETCH_SIZE x2 + WRITE_SIZE, profiles/pmc_latest.json)"
-                roof["algorithmic_bytes_per_launch"] = round(per_launch_bytes)
+                r["traffic"] = tr
+                r["traffic_unit"] = "bytes/launch (FETCH_SIZE x2 + WRITE_SIZE, profiles/pmc_latest.json)"
+                r["algorithmic_bytes_per_launch"] = round(per_launch_bytes)
+        return r, acc_split
+
+    roof, acc_split = scan_roofline(stats, tim, a.steps, a.workload)
     # K1 and the mean-shift update, the other two HBM-class kernels north_star names
     # (K1: ceil(L/4) packed bytes in + B*w row + 8 magnitude out per read; mean shift: one read
     # of each neighbourhood member's row and magnitudes per centre, update_evals of them)
@@ -401,10 +437,12 @@ def main():
                "cells_per_step": nw_cells / a.steps, "ms_per_step": round(fam_ms["nw"] / a.steps, 3)}
     if nwc:
         nw_roof["counters"] = nwc
-    cpu = None
+    cpu = cpu_v3 = None
     if not a.no_cpu_baseline and world == 1 and mode == "single" and a.workload == "B":
         # the reference: rank 0 at N = 1 only, on the full config-B FASTA (~27 s a run)
         cpu = cpu_baseline(fasta, ["--id", a.id], a.n, host_threads(), a.cpu_repeats)
+        # (rounds 1-5 timed an x86-64-v3 build: one run of it, for continuity)
+        cpu_v3 = cpu_baseline(fasta, ["--id", a.id], a.n, host_threads(), 1, binary="meshclust_v3", march="x86-64-v3")
     wl = "config %s: %dk synthetic 1kb reads (%d templates), --id %s k-mer mean-shift" % (
         a.workload, a.n // 1000, a.templates, a.id)
     line = {
@@ -455,15 +493,40 @@ def main():
                                         "fixed_point_left_out": s0.get("update_iters_fixed", 0)},
                   "rehearsal_one_gpu": one_gpu},
     }
+    if cpu_v3 is not None:
+        line["extra"]["cpu_baseline_x86_64_v3"] = cpu_v3
     if cpu is None and world == 1 and a.workload != "B":
         line["extra"]["cpu_baseline_note"] = "the reference is timed on config B only (config D takes it hours)"
+    if a.workload == "B" and world > 1 and not replicas:
+        line["config"]["config_b_at_n_gt_1"] = (
+            "config B's accumulation is replicated by design (its 100k rows fit one GPU's LDS, so a per-step "
+            "exchange would only lengthen the dependent chain: DESIGN.md §6); the training and the mean shift "
+            "split by rank.  extra.config_d is the workload that shards by record")
+    if d_run is not None:
+        dn, dt_, ds_, d_el, d_stats, d_tim, d_first = d_run
+        d0 = d_stats[-1]
+        d_roof, d_split = scan_roofline(d_stats, d_tim, len(d_stats), "D")
+        nd = len(d_stats)
+        line["extra"]["config_d"] = {
+            "workload": "config D: %dk synthetic 1kb reads (%d templates, seed %d), --id %s k-mer mean-shift, one "
+                        "clustering%s" % (dn // 1000, dt_, ds_, a.id,
+                                          " sharded by record over %d GPU(s)" % world if shard else " on one GPU"),
+            "value": round(dn * nd / d_el, 1), "unit": "sequences/s", "n_gpus": world, "steps": nd, "warmup": 1,
+            "ms_per_step": round(d_el / nd * 1e3, 2), "scaling": "strong", "roofline": d_roof,
+            "accum_path": d0.get("accum_path"), "accum_sharded_by_record": d_split, "clusters": d0["clusters"],
+            "scan_steps": d0["scan_steps"],
+            "step_split_ms": {"parse": round(1e3 * sum(s["parse_s"] for s in d_stats) / nd, 2),
+                              "upload_to_partition": round(sum(s["phases_ms"]["total_pipeline"] for s in d_stats) / nd, 2),
+                              "write_clstr": round(sum(s["write_ms"] for s in d_stats) / nd, 2)},
+            "device_ms_per_step": {f: round(v[0] / nd, 3) for f, v in d_tim.items()},
+            "comm_ms_per_step": comm_summary(d_stats), "warmup_s": round(d_first, 3)}
     print(json.dumps(line), flush=True)
     if a.stats_out:
         with open(a.stats_out, "w") as f:
             json.dump({"line": line, "stats": stats, "timers": tim}, f, indent=1)
-    if a.keep_clstr and last_clstr[0]:
+    if a.keep_clstr and keep_src:
         import shutil
-        shutil.copyfile(last_clstr[0], a.keep_clstr)
+        shutil.copyfile(keep_src, a.keep_clstr)
     if comm is not None:
         comm.close()
     eng.close()

@@ -178,7 +178,7 @@ struct DPart {  // one result of a call: `bytes` from device `d` to host `h` (h 
   const void *d;
   size_t bytes;
 };
-static uint8_t *download_pinned(mc_ctx *c, const void *d, size_t bytes, hipStream_t s);
+static int download_pinned(mc_ctx *c, const void *d, size_t bytes, hipStream_t s, uint8_t **h);
 // A call's results through the pinned landing buffer: one DMA per part into it, one stream
 // synchronize, then the host copies (every part a pageable download was a runtime-staged copy).
 // Ends with the stream synchronized, as the direct downloads it replaces did.
@@ -186,7 +186,9 @@ static int download_parts(mc_ctx *c, std::initializer_list<DPart> parts, hipStre
   size_t total = 0;
   for (const DPart &p : parts)
     if (p.h && p.bytes) total += (p.bytes + 255) / 256 * 256;
-  bool pinned = total > 0 && (c->h_dstage_cap >= total || download_pinned(c, nullptr, total, s) != nullptr);
+  uint8_t *stage = nullptr;  // (the buffer only: no copy, so no failure but the allocation's)
+  if (total > 0 && c->h_dstage_cap < total) (void)download_pinned(c, nullptr, total, s, &stage);
+  const bool pinned = total > 0 && c->h_dstage_cap >= total;
   if (pinned) {
     size_t off = 0;
     for (const DPart &p : parts)
@@ -212,9 +214,11 @@ static int download_parts(mc_ctx *c, std::initializer_list<DPart> parts, hipStre
 
 // One device region of a call's results copied to the context's pinned landing buffer (a plain
 // DMA; a pageable destination is staged by the runtime, one staged copy per download) and the
-// stream synchronized: the caller then copies the parts out of the returned host pointer.
-// nullptr after an allocation failure: the caller downloads the parts directly instead.
-static uint8_t *download_pinned(mc_ctx *c, const void *d, size_t bytes, hipStream_t s) {
+// stream synchronized: the caller then copies the parts out of *h.  *h is null only when the
+// landing buffer cannot be allocated (the caller then downloads the parts directly); a failing
+// copy or synchronize is reported as the error it is, with its call site.
+static int download_pinned(mc_ctx *c, const void *d, size_t bytes, hipStream_t s, uint8_t **h) {
+  *h = nullptr;
   if (bytes > c->h_dstage_cap) {
     if (c->h_dstage) (void)hipHostFree(c->h_dstage);
     c->h_dstage = nullptr;
@@ -223,14 +227,16 @@ static uint8_t *download_pinned(mc_ctx *c, const void *d, size_t bytes, hipStrea
     if (hipHostMalloc((void **)&c->h_dstage, cap, hipHostMallocDefault) != hipSuccess) {
       (void)hipGetLastError();
       c->h_dstage = nullptr;
-      return nullptr;
+      return MC_OK;
     }
     c->h_dstage_cap = cap;
   }
-  if (!d) return c->h_dstage;  // (download_parts: the buffer only)
-  if (hipMemcpyAsync(c->h_dstage, d, bytes, hipMemcpyDeviceToHost, s) != hipSuccess) return nullptr;
-  if (hipStreamSynchronize(s) != hipSuccess) return nullptr;
-  return c->h_dstage;
+  if (d) {  // (download_parts passes none: the buffer only)
+    MCG_CHECK(hipMemcpyAsync(c->h_dstage, d, bytes, hipMemcpyDeviceToHost, s));
+    MCG_CHECK(hipStreamSynchronize(s));
+  }
+  *h = c->h_dstage;
+  return MC_OK;
 }
 
 }  // namespace mcg
@@ -1506,7 +1512,9 @@ int mc_update_iteration(mc_ctx *c, const uint32_t *centre_ids, uint32_t C, const
   }
   // the whole result region in one copy to pinned memory (three pageable downloads were three
   // staged copies per iteration)
-  if (const uint8_t *h = download_pinned(c, c->s_j.p, res_bytes, c->stream)) {
+  uint8_t *h = nullptr;
+  TRY(download_pinned(c, c->s_j.p, res_bytes, c->stream, &h));
+  if (h) {
     if (m && combo0) memcpy(combo0, h, m * 8);
     if (m && similar) memcpy(similar, h + m * 8, m);
     memcpy(new_centre, h + o_new, (size_t)C * 4);

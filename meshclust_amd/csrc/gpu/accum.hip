@@ -217,7 +217,8 @@ int accum_alloc(mc_ctx *c, const AccPlan &pl, uint32_t nb, AccBytes *ab) {
                                        : 0;
   if (cc_bytes && ensure(c->s_k, cc_bytes)) return MC_ERR_OOM;
   if (ensure(c->s_d, ((size_t)nb + 1) * 4 + 16) || ensure(c->s_e, (size_t)nb * 8 + 16) ||
-      ensure(c->s_f, c->norder * 4 + 16) || ensure(c->s_g, (c->norder + 1) * 8 + 16) || ensure(c->acc_out, 256))
+      ensure(c->s_f, c->norder * 4 + 16) || ensure(c->s_g, (c->norder + 1) * 8 + 16) || ensure(c->acc_out, 256) ||
+      ensure(c->ord_ids, c->norder * 4 + 16))  // (mc_accumulate's ordered member ids)
     return MC_ERR_OOM;
   return MC_OK;
 }

@@ -1991,30 +1991,38 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
   };
   // (Every word of a lane is read before its first store: on gfx9 stores count in vmcnt, so a
   // load issued after a store waits for that store to complete -- a write-through round trip.)
-  auto publish = [&](uint64_t S, uint64_t E, bool have) {
-    uint64_t *r = A.ring + (uint64_t)(step % RING) * A.rec_g;
-    constexpr int PW = 4;  // words per lane read before the lane's stores
+  // rec_read / rec_store: the record's words j0 .. j0 + 64 * PW - 1 (PW per lane, held in
+  // registers between the reads and the stores); publish: every word
+  constexpr int PW = 4;
+  auto rec_read = [&](int j0, uint64_t S, uint64_t E, bool have, uint32_t (&d)[PW]) {
     const bool fastw = !WIDE && last != NONE && last_q < A.mrow;  // (uniform)
-    for (int j0 = 0; j0 < rec_words; j0 += 64 * PW) {
-      uint32_t d[PW];
-      if (fastw) {
-#pragma unroll
-        for (int u = 0; u < PW; u++) {
-          const int j = j0 + u * 64 + lane;
-          d[u] = j < rec_words ? rec_word_cached(j, have, S, E) : 0u;
-        }
-      } else {
-#pragma unroll
-        for (int u = 0; u < PW; u++) {
-          const int j = j0 + u * 64 + lane;
-          d[u] = j < rec_words ? rec_word(j, have, S, E) : 0u;
-        }
-      }
+    if (fastw) {
 #pragma unroll
       for (int u = 0; u < PW; u++) {
         const int j = j0 + u * 64 + lane;
-        if (j < rec_words) st64(r + j, gran(step, d[u]));
+        d[u] = j < rec_words ? rec_word_cached(j, have, S, E) : 0u;
       }
+    } else {
+#pragma unroll
+      for (int u = 0; u < PW; u++) {
+        const int j = j0 + u * 64 + lane;
+        d[u] = j < rec_words ? rec_word(j, have, S, E) : 0u;
+      }
+    }
+  };
+  auto rec_store = [&](int j0, const uint32_t (&d)[PW]) {
+    uint64_t *r = A.ring + (uint64_t)(step % RING) * A.rec_g;
+#pragma unroll
+    for (int u = 0; u < PW; u++) {
+      const int j = j0 + u * 64 + lane;
+      if (j < rec_words) st64(r + j, gran(step, d[u]));
+    }
+  };
+  auto publish = [&](uint64_t S, uint64_t E, bool have) {
+    for (int j0 = 0; j0 < rec_words; j0 += 64 * PW) {
+      uint32_t d[PW];
+      rec_read(j0, S, E, have, d);
+      rec_store(j0, d);
     }
     if (lane == 0) st32(A.go, step);
   };
@@ -2129,7 +2137,21 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
         step++;
         uint64_t tp0 = 0;
         if (prof_on && threadIdx.x == 0) tp0 = now();
-        if (wv == 0) publish(fast_after ? lo[wt.fb] : 0, fast_after ? lo[wt.bb + 1] - 1 : A.N - 1, true);
+        // The record's words are read from LDS before the other waves start the last step's
+        // bvec kills: those are LDS atomics on shared Fenwick nodes, and the record's reads
+        // queued behind them held every member step's record back by ≈2 µs.
+        const uint64_t S0 = fast_after ? lo[wt.fb] : 0, E0 = fast_after ? lo[wt.bb + 1] - 1 : A.N - 1;
+        if (rec_words <= 64 * PW) {  // (uniform: every record of a dense or narrow-row launch)
+          uint32_t d[PW];
+          if (wv == 0) rec_read(0, S0, E0, true, d);
+          if (npend) __syncthreads();
+          if (wv == 0) {
+            rec_store(0, d);
+            if (lane == 0) st32(A.go, step);
+          }
+        } else if (wv == 0) {
+          publish(S0, E0, true);
+        }
         if (prof_on && threadIdx.x == 0) {
           const uint64_t t = now();
           t_pub[0] += tp0 - t_mark;  // the record's span (edge bins' counts)
@@ -2141,7 +2163,9 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
       if (prof_on && threadIdx.x == 0) tk0 = now();
       if (npend) {  // the last step's bvec kills, after the record is out
         if (!(A.dbg & 1)) {
-          for (uint32_t i = threadIdx.x; i < npend; i += NT) bv.kill_in(s_plist[i], s_pbin[i]);
+          // (waves 1.. only: wave 0 is issuing the record's stores)
+          if (threadIdx.x >= 64)
+            for (uint32_t i = threadIdx.x - 64; i < npend; i += NT - 64) bv.kill_in(s_plist[i], s_pbin[i]);
         } else
         for (uint32_t i0 = 0; i0 < npend; i0 += NT) {
           const uint32_t i = i0 + threadIdx.x;

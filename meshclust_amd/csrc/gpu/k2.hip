@@ -528,40 +528,50 @@ __global__ __launch_bounds__(NT) void mean_shift_kernel(HistView H, DevClassifie
 // Each cluster's members in `current` order (the seed, then each step's flagged candidates in
 // bvec order): one workgroup per cluster sorts its u64 keys -- step << 32 | static position,
 // or the seed's 0 replaced by its position -- by a bitonic network in LDS and writes the ids
-// (static order -> id).  Clusters of more than OM_MAX members are left to the host.
+// (static order -> id).  Clusters of more than OM_MAX members are left to the host.  The grid is
+// capped (OM_GRID) and strides over the clusters: a mostly-singleton input can have more clusters
+// than a launch may hold workgroups.
 constexpr int OM_MAX = 4096, OM_T = 256;
+constexpr uint64_t OM_GRID = 65536;
 __global__ __launch_bounds__(OM_T) void order_members_kernel(const uint64_t *__restrict__ keys,
                                                              const uint32_t *__restrict__ pos,
                                                              const uint64_t *__restrict__ cl_off,
                                                              const uint32_t *__restrict__ order,
-                                                             uint32_t *__restrict__ ids) {
+                                                             uint32_t *__restrict__ ids, uint64_t ncl) {
   __shared__ uint64_t k[OM_MAX];
-  const uint64_t a = cl_off[blockIdx.x], b = cl_off[blockIdx.x + 1];
-  const uint32_t m = (uint32_t)(b - a);
-  if (m > (uint32_t)OM_MAX) return;  // (uniform)
-  uint32_t P = 1;
-  while (P < m) P <<= 1;
-  for (uint32_t i = threadIdx.x; i < P; i += OM_T) {
-    const uint64_t x = i < m ? keys[a + i] : ~0ull;
-    k[i] = i < m && x == 0 ? (uint64_t)pos[a + i] : x;
-  }
-  __syncthreads();
-  for (uint32_t len = 2; len <= P; len <<= 1)
-    for (uint32_t j = len >> 1; j > 0; j >>= 1) {
-      for (uint32_t i = threadIdx.x; i < P; i += OM_T) {
-        const uint32_t l = i ^ j;
-        if (l > i) {
-          const uint64_t x = k[i], y = k[l];
-          const bool up = (i & len) == 0;
-          if (up ? x > y : x < y) {
-            k[i] = y;
-            k[l] = x;
+  for (uint64_t cl = blockIdx.x; cl < ncl; cl += gridDim.x) {
+    const uint64_t a = cl_off[cl], b = cl_off[cl + 1];
+    const uint32_t m = (uint32_t)(b - a);
+    if (b - a > (uint64_t)OM_MAX) continue;  // (uniform)
+    if (m == 1) {  // (a singleton: nothing to order)
+      if (threadIdx.x == 0) ids[a] = order[pos[a]];
+      continue;
+    }
+    uint32_t P = 1;
+    while (P < m) P <<= 1;
+    __syncthreads();  // (the previous cluster's reads of k are done)
+    for (uint32_t i = threadIdx.x; i < P; i += OM_T) {
+      const uint64_t x = i < m ? keys[a + i] : ~0ull;
+      k[i] = i < m && x == 0 ? (uint64_t)pos[a + i] : x;
+    }
+    __syncthreads();
+    for (uint32_t len = 2; len <= P; len <<= 1)
+      for (uint32_t j = len >> 1; j > 0; j >>= 1) {
+        for (uint32_t i = threadIdx.x; i < P; i += OM_T) {
+          const uint32_t l = i ^ j;
+          if (l > i) {
+            const uint64_t x = k[i], y = k[l];
+            const bool up = (i & len) == 0;
+            if (up ? x > y : x < y) {
+              k[i] = y;
+              k[l] = x;
+            }
           }
         }
+        __syncthreads();
       }
-      __syncthreads();
-    }
-  for (uint32_t i = threadIdx.x; i < m; i += OM_T) ids[a + i] = order[(uint32_t)k[i]];
+    for (uint32_t i = threadIdx.x; i < m; i += OM_T) ids[a + i] = order[(uint32_t)k[i]];
+  }
 }
 
 int grid_for(uint64_t work, int per_block, int cap) {
@@ -584,7 +594,9 @@ int grid_for(uint64_t work, int per_block, int cap) {
 int launch_order_members(mc_ctx *c, const uint64_t *d_keys, const uint32_t *d_pos, const uint64_t *d_cl_off, uint64_t ncl,
                          uint32_t *d_ids) {
   if (!ncl) return MC_OK;
-  order_members_kernel<<<(unsigned)ncl, OM_T, 0, c->stream>>>(d_keys, d_pos, d_cl_off, (const uint32_t *)c->order.p, d_ids);
+  const unsigned grid = (unsigned)(ncl < OM_GRID ? ncl : OM_GRID);
+  order_members_kernel<<<grid, OM_T, 0, c->stream>>>(d_keys, d_pos, d_cl_off, (const uint32_t *)c->order.p, d_ids,
+                                                     ncl);
   MCG_CHECK(hipGetLastError());
   return MC_OK;
 }

@@ -316,14 +316,36 @@ static void align_sharded_step(mc_ctx *ctx, const ShardComm &comm, uint32_t cent
   const uint64_t W = (uint64_t)comm.world, blk = (E - S + 1 + W - 1) / W;  // (a bound on any part's count)
   std::vector<double> mine(blk + 1, 0.0), all((blk + 1) * W);
   uint64_t np = 0, pairs = 0, cells = 0;
+  // A rank whose NW part fails (an MC_ERR_TIMEOUT of the chained blocks, an allocation, a HIP
+  // error) still joins the all-gather with its count word set to kFailed, so every rank stops
+  // after the same exchange (as sharded_step) instead of its peers waiting in it.
+  constexpr uint64_t kFailed = ~0ull;
+  std::string part_err;
   {
     Scope s(timer, "accumulate.align_part");
-    check(mc_align_part(ctx, centre, S, E, (uint32_t)comm.rank, (uint32_t)W, mine.data() + 1, blk, &np, &pairs, &cells),
-          "mc_align_part");
+    try {
+      fault_point(&comm, "align_part");
+      check(mc_align_part(ctx, centre, S, E, (uint32_t)comm.rank, (uint32_t)W, mine.data() + 1, blk, &np, &pairs,
+                          &cells),
+            "mc_align_part");
+    } catch (const std::exception &e) {
+      part_err = e.what();
+      np = kFailed;
+    }
   }
   memcpy(mine.data(), &np, 8);
-  if (comm.allgather(comm.user, mine.data(), mine.size() * 8, all.data()) != 0)
+  if (comm.allgather(comm.user, mine.data(), mine.size() * 8, all.data()) != 0) {
+    if (!part_err.empty()) throw Error(part_err, 1);
     throw PeerError("identity all-gather across ranks failed");
+  }
+  for (uint64_t r = 0; r < W; r++) {
+    uint64_t nr = 0;
+    memcpy(&nr, all.data() + r * (blk + 1), 8);
+    if (nr == kFailed) {
+      if (part_err.empty()) throw PeerError("alignment part failed on rank " + std::to_string(r));
+      throw Error(part_err, 1);
+    }
+  }
   std::vector<double> ident(pairs);
   for (uint64_t r = 0; r < W; r++) {
     uint64_t nr = 0;
@@ -602,6 +624,16 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
   int split_update = (multi && !memo) ? -1 : 0;
   if (split_update < 0 && getenv("MC_SHARD_FORCE")) split_update = 1;
   if (split_update < 0 && getenv("MC_SHARD_UPDATE")) split_update = atoi(getenv("MC_SHARD_UPDATE")) ? 1 : 0;
+  bool all_iterations = getenv("MC_UPDATE_ALL_ITERATIONS") != nullptr;
+  if (multi) {
+    // the loop's branches that lead to an exchange (the fixed-point exit, the split decision)
+    // must be the same on every rank: every rank takes rank 0's environment choices
+    int32_t mine[2] = {split_update, all_iterations ? 1 : 0}, all[2 * 64];
+    if (cfg.comm->world > 64 || cfg.comm->allgather(cfg.comm->user, mine, 8, all) != 0)
+      throw PeerError("all-gather across ranks failed");
+    split_update = all[0];
+    all_iterations = all[1] != 0;
+  }
   double t_first = 0;
   for (int it = 0; it < cfg.iterations; it++) {
     bool fused = false;
@@ -773,7 +805,7 @@ std::vector<Center> mean_shift_cluster(const Dataset &ds, mc_ctx *ctx, BVec &bv,
     // counted as if run.  (Alignment mode: the remaining iterations would look up the same pairs
     // in the memo, every one of them aligned by now -- memo_lookup aligns only pairs it has not
     // seen, and nothing else changes the memo during the updates -- so they would add nothing.)
-    if (!moved && !rebuild && !getenv("MC_UPDATE_ALL_ITERATIONS")) {
+    if (!moved && !rebuild && !all_iterations) {
       const uint64_t rest = (uint64_t)(cfg.iterations - 1 - it);
       stats.update_evals += rest * it_update_evals;
       stats.merge_evals += rest * (uint64_t)pa.size();

@@ -239,9 +239,16 @@ RunResult run_pipeline(const Dataset &ds, mc_ctx *ctx, Options opt, bool upload,
   // split's first sort (ids by length) depends on the lengths alone: a host thread computes it
   // while the upload and K1 run (k-mer mode; joined before the trainer starts)
   std::vector<uint32_t> len_order;
+  std::exception_ptr len_err;  // (rethrown after the join: an exception must not end the thread)
   std::thread len_thread;
   if (!opt.align && opt.similarity >= 0.6)
-    len_thread = std::thread([&]() { len_order = Trainer::length_order(ds, threads); });
+    len_thread = std::thread([&]() {
+      try {
+        len_order = Trainer::length_order(ds, threads);
+      } catch (...) {
+        len_err = std::current_exception();
+      }
+    });
   struct JoinLen {
     std::thread &t;
     ~JoinLen() {
@@ -276,6 +283,7 @@ RunResult run_pipeline(const Dataset &ds, mc_ctx *ctx, Options opt, bool upload,
   tc.verbose = verbose;
   tc.comm = comm;
   if (len_thread.joinable()) len_thread.join();
+  if (len_err) std::rethrow_exception(len_err);
   tc.length_order = std::move(len_order);
   Trainer tr(ds, ctx, tc, rr.timer);
   // The bvec (Runner.cpp:345-350: construct, insert every point, insert_finalize) depends only

@@ -4,6 +4,7 @@
 #include "lazysort.hpp"  // (the two full sorts; the per-pivot sorts are on the device)
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <cmath>
 #include <cstdio>
@@ -212,31 +213,66 @@ std::vector<PairId> Trainer::split() {
   // on the device (mc_split_*, split.hip): the (key << 32 | id) arrays stay in HBM and only
   // the positions the binary search and the sampler read are resolved, with std::sort's exact
   // tie order.
-  // Two levels per round measured fastest at config B (9 rounds of 450 pairs in the latency
-  // form instead of 16 of 150); MC_NW_LOOKAHEAD = 1..4.
+  // Rounds after the first align the next `look` levels of every chain's decision tree (2^look - 1
+  // pairs per chain); two levels per round measured fastest at config B without the spine round
+  // (9 rounds of 450 pairs in the latency form instead of 16 of 150); MC_NW_LOOKAHEAD = 1..4.
   const int look = [] {
     const char *e = getenv("MC_NW_LOOKAHEAD");
     const int v = e ? atoi(e) : 2;
     return v < 1 ? 1 : v > 4 ? 4 : v;
   }();
-  // the decision tree of chain state (p, o) to depth d, breadth first: node n's children are
-  // 2n+1 (identity below the cutoff: p - o) and 2n+2 (above: p + o), each with offset o / 2;
-  // a node whose offset is 0 is not aligned (the chain stops there, as `gather` drops it)
-  auto tree = [&](size_t p, size_t o, int d, std::vector<size_t> &pos, std::vector<char> &live) {
-    const size_t nn = ((size_t)1 << d) - 1;
-    pos.assign(nn, 0);
-    live.assign(nn, 0);
-    std::vector<size_t> off(nn, 0);
-    pos[0] = p;
-    off[0] = o;
-    live[0] = o > 0;
-    for (size_t n = 0; 2 * n + 2 < nn; n++) {
-      if (!live[n]) continue;
-      const size_t oc = off[n] / 2;
-      pos[2 * n + 1] = pos[n] - off[n];
-      pos[2 * n + 2] = pos[n] + off[n];
-      off[2 * n + 1] = off[2 * n + 2] = oc;
-      live[2 * n + 1] = live[2 * n + 2] = oc > 0;
+  // The first round aligns each chain's whole "left spine" -- the pivots the search visits while
+  // every identity stays below the cutoff (N/2, N/4, N/8, ...) -- in one batch (MC_NW_SPINE=0: off).
+  // The array is sorted by k-mer distance to the pivot, so the search walks left until it nears
+  // the few points within the cutoff of the pivot (its own cluster): at config B the first ~9 of
+  // ~15 levels, in one round of ~2,400 pairs (the throughput form) instead of ~5 dependent rounds.
+  // A chain whose identities turn above the cutoff earlier just leaves the rest of its spine
+  // unused; every decision is still taken from its own alignment, so the pivots are the same.
+  const bool spine = [] {
+    const char *e = getenv("MC_NW_SPINE");
+    return !e || atoi(e) != 0;
+  }();
+  // one round's nodes of chain state (p, o): node n aligns position pos[n]; its children (identity
+  // below the cutoff: p - o; above: p + o, both with offset o / 2) are kid[n][0] / kid[n][1], -1
+  // when not aligned this round (the walk stops there and the next round starts from it); a node
+  // whose offset is 0 is not aligned (the chain stops there, as `gather` drops it)
+  struct Plan {
+    std::vector<size_t> pos;
+    std::vector<std::array<int, 2>> kid;
+  };
+  auto tree = [&](size_t p, size_t o, int d, Plan &pl) {  // the complete tree of depth d
+    pl.pos.clear();
+    pl.kid.clear();
+    if (o == 0) return;
+    std::vector<size_t> off;
+    pl.pos.push_back(p);
+    pl.kid.push_back({-1, -1});
+    off.push_back(o);
+    std::vector<int> level = {0};
+    for (int l = 1; l < d; l++) {
+      std::vector<int> next;
+      for (int n : level) {
+        const size_t oc = off[(size_t)n] / 2;
+        if (oc == 0) continue;
+        for (int side = 0; side < 2; side++) {
+          pl.kid[(size_t)n][(size_t)side] = (int)pl.pos.size();
+          next.push_back((int)pl.pos.size());
+          pl.pos.push_back(side ? pl.pos[(size_t)n] + off[(size_t)n] : pl.pos[(size_t)n] - off[(size_t)n]);
+          pl.kid.push_back({-1, -1});
+          off.push_back(oc);
+        }
+      }
+      level.swap(next);
+    }
+  };
+  auto left_spine = [&](size_t p, size_t o, Plan &pl) {  // every level, identity below the cutoff
+    pl.pos.clear();
+    pl.kid.clear();
+    for (; o > 0; o /= 2) {
+      if (!pl.pos.empty()) pl.kid.back()[0] = (int)pl.pos.size();
+      pl.pos.push_back(p);
+      pl.kid.push_back({-1, -1});
+      p -= o;
     }
   };
   // Several ranks: rank r runs the chains (binary searches and samples) of its block of pivots
@@ -284,9 +320,8 @@ std::vector<PairId> Trainer::split() {
     Scope s(timer_, "train.nw_search");
     std::vector<PairId> batch;
     std::vector<size_t> who, first;  // chain of each batch entry's tree; first entry of each chain
-    std::vector<std::vector<size_t>> tpos(P);
-    std::vector<std::vector<char>> tlive(P);
-    for (;;) {
+    std::vector<Plan> plan(P);
+    for (int round = 0;; round++) {
       who.clear();
       for (size_t i = i0; i < i1; i++) {
         if (active[i] && offset[i] == 0) active[i] = 0;
@@ -299,12 +334,12 @@ std::vector<PairId> Trainer::split() {
         q_pos.clear();
         for (size_t t = 0; t < who.size(); t++) {
           const size_t i = who[t];
-          tree(pivot[i], offset[i], look, tpos[i], tlive[i]);
-          for (size_t n = 0; n < tpos[i].size(); n++)
-            if (tlive[i][n]) {
-              q_arr.push_back((uint32_t)i);
-              q_pos.push_back(tpos[i][n]);
-            }
+          if (round == 0 && spine) left_spine(pivot[i], offset[i], plan[i]);
+          else tree(pivot[i], offset[i], look, plan[i]);
+          for (size_t n = 0; n < plan[i].pos.size(); n++) {
+            q_arr.push_back((uint32_t)i);
+            q_pos.push_back(plan[i].pos[n]);
+          }
           first[t + 1] = q_arr.size();
         }
         select();
@@ -319,19 +354,15 @@ std::vector<PairId> Trainer::split() {
       }
       for (size_t t = 0; t < who.size(); t++) {
         const size_t i = who[t];
-        // the aligned nodes of this chain's tree, in batch order
-        size_t q = first[t], n = 0;
-        std::vector<double> val(tpos[i].size(), 0.0);
-        for (size_t m = 0; m < tpos[i].size(); m++)
-          if (tlive[i][m]) val[m] = al[q++];
-        for (int d = 0; d < look && active[i]; d++) {
+        const double *val = al.data() + first[t];  // this chain's nodes, in plan order
+        for (int n = 0; n >= 0 && active[i];) {
           const double algn = val[n];
           if (algn < cfg_.cutoff) {
             pivot[i] -= offset[i];
-            n = 2 * n + 1;
+            n = plan[i].kid[(size_t)n][0];
           } else if (algn > cfg_.cutoff) {
             pivot[i] += offset[i];
-            n = 2 * n + 2;
+            n = plan[i].kid[(size_t)n][1];
           } else {
             active[i] = 0;
             break;

@@ -23,10 +23,10 @@ PY
 for v in ${VARIANTS:-base}; do
   envs=(); [ "$v" != base ] && envs=(${v//,/ })
   echo "== $v"
-  env "${envs[@]}" timeout -k 10 300 python bench.py --steps ${STEPS:-3} --warmup 1 --no-cpu-baseline \
+  env "${envs[@]}" timeout -k 10 300 python bench.py --steps ${STEPS:-3} --warmup 1 --no-cpu-baseline --no-config-d \
     > gpurun_out/ab_$v.log 2>&1 || { echo "bench rc=$?"; tail -n 20 gpurun_out/ab_$v.log; exit 1; }
   summ gpurun_out/ab_$v.log
-  env "${envs[@]}" MC_ACCUM_PROFILE=${PROFV:-1} timeout -k 10 300 python bench.py --steps 2 --warmup 1 --no-cpu-baseline \
+  env "${envs[@]}" MC_ACCUM_PROFILE=${PROFV:-1} timeout -k 10 300 python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-config-d \
     > gpurun_out/ab_prof_$v.log 2>&1 || { echo "bench rc=$?"; tail -n 20 gpurun_out/ab_prof_$v.log; exit 1; }
   grep "^\[accum" gpurun_out/ab_prof_$v.log | tail -n 3 | head -n 2
 done

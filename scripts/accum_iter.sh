@@ -7,7 +7,7 @@ timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_co
   -k "e2e or device_accumulate or B100k or member_cache" --timeout 300 --timeout-method thread -p no:cacheprovider \
   > gpurun_out/accum_parity.log 2>&1 || { echo "parity rc=$?"; tail -n 30 gpurun_out/accum_parity.log; exit 1; }
 tail -n 3 gpurun_out/accum_parity.log
-MC_ACCUM_PROFILE=${PROF:-2} timeout -k 10 300 python bench.py --steps 2 --warmup 1 --no-cpu-baseline \
+MC_ACCUM_PROFILE=${PROF:-2} timeout -k 10 300 python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-config-d \
   > gpurun_out/accum_prof.log 2>&1 || { echo "bench rc=$?"; tail -n 30 gpurun_out/accum_prof.log; exit 1; }
 grep -v '^{' gpurun_out/accum_prof.log | tail -n 4
 python - <<'PY'

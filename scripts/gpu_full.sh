@@ -8,5 +8,5 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -q -x --timeout 600 --timeout
 rc=$?; echo "pytest rc=$rc"; tail -n 5 gpurun_out/pytest_gpu.log
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py \
-  --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/prof.log 2>&1
+  --steps 2 --warmup 1 --no-cpu-baseline --no-config-d > gpurun_out/prof.log 2>&1
 echo "prof rc=$?"; grep '^{' gpurun_out/prof.log | tail -c 600

@@ -9,7 +9,7 @@ timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_co
 tail -n 1 gpurun_out/look_parity.log
 for L in ${LOOKS:-1 2 3}; do
   extra=(); [[ "$L" == *,* ]] && extra=(${L#*,})   # "3,MC_NW_MW_MAX=2048": look 3 plus that setting
-  env MC_NW_LOOKAHEAD=${L%%,*} "${extra[@]}" timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/look_$L.log 2>&1 || exit 1
+  env MC_NW_LOOKAHEAD=${L%%,*} "${extra[@]}" timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-config-d > gpurun_out/look_$L.log 2>&1 || exit 1
   python - gpurun_out/look_$L.log $L <<'PY'
 import json, sys
 d = json.loads([x for x in open(sys.argv[1]) if x.startswith("{")][-1])

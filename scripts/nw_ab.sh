@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 for v in ${VARIANTS:-base}; do
   envs=(); [ "$v" != base ] && envs=(${v//,/ })
-  env "${envs[@]}" timeout -k 10 300 python bench.py --steps ${STEPS:-3} --warmup 1 --no-cpu-baseline \
+  env "${envs[@]}" timeout -k 10 300 python bench.py --steps ${STEPS:-3} --warmup 1 --no-cpu-baseline --no-config-d \
     > gpurun_out/nwab_$v.log 2>&1 || { echo "bench rc=$?"; tail -n 20 gpurun_out/nwab_$v.log; exit 1; }
   python - "$v" gpurun_out/nwab_$v.log <<'PY'
 import json, sys

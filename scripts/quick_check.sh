@@ -9,7 +9,7 @@ if [ -n "${K:-}" ]; then
     -p no:cacheprovider > gpurun_out/qc_pytest.log 2>&1 || { echo "pytest rc=$?"; tail -n 30 gpurun_out/qc_pytest.log; exit 1; }
   tail -n 2 gpurun_out/qc_pytest.log
 fi
-timeout -k 10 300 python -u bench.py --steps ${STEPS:-10} --warmup 2 --no-cpu-baseline > gpurun_out/qc_bench.log 2>&1 \
+timeout -k 10 300 python -u bench.py --steps ${STEPS:-10} --warmup 2 --no-cpu-baseline --no-config-d > gpurun_out/qc_bench.log 2>&1 \
   || { echo "bench rc=$?"; tail -n 20 gpurun_out/qc_bench.log; exit 1; }
 python - <<'PY'
 import json

@@ -10,7 +10,7 @@ trap 'kill $TICK 2>/dev/null' EXIT
 for v in ${VARIANTS:-base}; do
   envs=(); [ "$v" != base ] && envs=(${v//,/ })
   echo "== $v"
-  env "${envs[@]}" timeout -k 10 300 python bench.py --steps ${STEPS:-3} --warmup 1 --no-cpu-baseline \
+  env "${envs[@]}" timeout -k 10 300 python bench.py --steps ${STEPS:-3} --warmup 1 --no-cpu-baseline --no-config-d \
     > gpurun_out/ab_$v.log 2>&1 || { echo "bench rc=$?"; tail -n 20 gpurun_out/ab_$v.log; exit 1; }
   python - gpurun_out/ab_$v.log <<'PY'
 import json, sys
@@ -22,7 +22,7 @@ print("  value %.0f ms/step %.2f roof %.4f us/step %.2f nw_ms %.2f train %.2f ac
     e["nw_roofline"]["ms_per_step"], e["host_phases_ms"]["train"], e["host_phases_ms"]["accumulate"]))
 PY
   if [ -n "${PROF:-}" ]; then
-    env "${envs[@]}" MC_ACCUM_PROFILE=$PROF timeout -k 10 300 python bench.py --steps 1 --warmup 1 --no-cpu-baseline \
+    env "${envs[@]}" MC_ACCUM_PROFILE=$PROF timeout -k 10 300 python bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-config-d \
       > gpurun_out/ab_prof_$v.log 2>&1 || { echo "bench rc=$?"; tail -n 20 gpurun_out/ab_prof_$v.log; exit 1; }
     grep "^\[accum" gpurun_out/ab_prof_$v.log | tail -n 3
   fi

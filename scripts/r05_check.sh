@@ -11,10 +11,10 @@ if [ -n "${K:-}" ]; then
   rc=$?; tail -n 3 gpurun_out/${TAG}_pytest.log; [ $rc -eq 0 ] || exit $rc
 fi
 if [ -z "${NOB:-}" ]; then
-  timeout -k 10 300 python bench.py --steps ${STEPS:-10} --warmup 2 --no-cpu-baseline > gpurun_out/${TAG}_bench_b.log 2>&1 || exit 1
+  timeout -k 10 300 python bench.py --steps ${STEPS:-10} --warmup 2 --no-cpu-baseline --no-config-d > gpurun_out/${TAG}_bench_b.log 2>&1 || exit 1
 fi
 if [ -n "${D:-}" ]; then
-  timeout -k 10 600 python bench.py --workload D --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/${TAG}_bench_d.log 2>&1 || exit 1
+  timeout -k 10 600 python bench.py --workload D --steps 2 --warmup 1 --no-cpu-baseline --no-config-d > gpurun_out/${TAG}_bench_d.log 2>&1 || exit 1
 fi
 if [ -n "${CONFIGS:-}" ]; then
   timeout -k 10 900 python scripts/configs.py $CONFIGS > gpurun_out/${TAG}_configs.log 2>&1 || exit 1

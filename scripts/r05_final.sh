@@ -9,6 +9,6 @@ export TMPDIR=/tmp
 TICK=$!
 trap 'kill $TICK 2>/dev/null' EXIT
 timeout -k 10 600 python bench.py > gpurun_out/final_bench_b.log 2>&1 || exit 1
-timeout -k 10 600 python bench.py --workload D --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/final_bench_d.log 2>&1 || exit 1
+timeout -k 10 600 python bench.py --workload D --steps 3 --warmup 1 --no-cpu-baseline --no-config-d > gpurun_out/final_bench_d.log 2>&1 || exit 1
 timeout -k 10 1100 python scripts/configs.py ${CFGS:-D1M E9100 C20k C100k} > gpurun_out/final_configs.log 2>&1 || exit 1
 grep -h "^{" gpurun_out/final_bench_b.log | tail -1 | head -c 1500; echo

@@ -13,13 +13,13 @@ TICK=$!
 trap 'kill $TICK 2>/dev/null' EXIT
 step() { echo "$1 rc=$2 t=$(date +%s)" | tee -a gpurun_out/fin_status.txt; [ "$2" -eq 0 ] || exit "$2"; }
 timeout -k 10 600 python bench.py > gpurun_out/fin_bench_b.log 2>&1; step bench_b $?
-timeout -k 10 600 python bench.py --workload D --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/fin_bench_d.log 2>&1; step bench_d $?
+timeout -k 10 600 python bench.py --workload D --steps 3 --warmup 1 --no-cpu-baseline --no-config-d > gpurun_out/fin_bench_d.log 2>&1; step bench_d $?
 timeout -k 10 900 python scripts/configs.py ${CFGS:-D1M E9100 C20k C100k} > gpurun_out/fin_configs.log 2>&1; step configs $?
 export MC_ACCUM_PLAIN_LAUNCH=1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/fin_stats -o run -- \
-  python bench.py --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/fin_stats.log 2>&1; step stats $?
+  python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-config-d > gpurun_out/fin_stats.log 2>&1; step stats $?
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/fin_fetch -o run -- \
-  python bench.py --steps 1 --warmup 0 --no-cpu-baseline > gpurun_out/fin_fetch.log 2>&1; step fetch $?
+  python bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-config-d > gpurun_out/fin_fetch.log 2>&1; step fetch $?
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/fin_write -o run -- \
-  python bench.py --steps 1 --warmup 0 --no-cpu-baseline > gpurun_out/fin_write.log 2>&1; step write $?
+  python bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-config-d > gpurun_out/fin_write.log 2>&1; step write $?
 grep -h "^{" gpurun_out/fin_bench_b.log | tail -1 | head -c 1200; echo

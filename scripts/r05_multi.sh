@@ -11,10 +11,10 @@ if [ -z "${NOTEST:-}" ]; then
     -p no:cacheprovider > gpurun_out/multi_pytest.log 2>&1
   rc=$?; tail -n 25 gpurun_out/multi_pytest.log | grep -E "PASS|FAIL|ERROR|passed|failed|skipped" | tail -n 30; [ $rc -eq 0 ] || exit $rc
 fi
-MC_BENCH_ONE_GPU=1 timeout -k 10 600 python bench.py --gpus 2 --steps ${STEPS:-5} --warmup 2 --no-cpu-baseline \
+MC_BENCH_ONE_GPU=1 timeout -k 10 600 python bench.py --gpus 2 --steps ${STEPS:-5} --warmup 2 --no-cpu-baseline --no-config-d \
   --stats-out gpurun_out/multi_b2_stats.json > gpurun_out/multi_b2.log 2>&1 || { echo "b2 rc=$?"; tail -n 30 gpurun_out/multi_b2.log; exit 1; }
 if [ -n "${D:-}" ]; then
-  MC_BENCH_ONE_GPU=1 timeout -k 10 900 python bench.py --gpus 2 --workload D --steps 2 --warmup 1 --no-cpu-baseline \
+  MC_BENCH_ONE_GPU=1 timeout -k 10 900 python bench.py --gpus 2 --workload D --steps 2 --warmup 1 --no-cpu-baseline --no-config-d \
     --stats-out gpurun_out/multi_d2_stats.json > gpurun_out/multi_d2.log 2>&1 || { echo "d2 rc=$?"; tail -n 30 gpurun_out/multi_d2.log; exit 1; }
 fi
 python - <<'PY'

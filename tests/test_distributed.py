@@ -347,6 +347,33 @@ def test_devices_threads_fault_stops_every_rank(cpu_lib, stage, tmp_path):
     assert time.time() - t0 < 60
 
 
+def test_devices_threads_align_fault_stops_every_rank(cpu_lib, tmp_path):
+    """Alignment mode's sharded NW part (cluster.cpp align_sharded_step): a rank whose part fails
+    still joins the identity all-gather with its block marked failed, so both ranks stop."""
+    import time
+    t0 = time.time()
+    r, _, _ = _cli(HARNESS, "al300", tmp_path, "0,1", {"MC_FAULT": "1:align_part"}, timeout=120)
+    assert r.returncode != 0
+    assert "injected fault" in r.stderr, r.stderr[-2000:]
+    assert time.time() - t0 < 60
+
+
+def test_processes_align_fault_stops_every_rank(cpu_lib, tmp_path):
+    """The same with one process per rank (gloo): the run ends promptly with the failing rank's
+    error, no rank waits out the exchange timeout."""
+    import time
+    fa, flags = fixtures.e2e_input("al300", tmp_path)
+    out = str(tmp_path / "al300.clstr")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), WORKER, fa, out, "--"] + flags
+    t0 = time.time()
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, OMP_NUM_THREADS="2", MC_FAULT="1:align_part", MC_DIST_TIMEOUT_S="120"))
+    assert r.returncode != 0
+    assert "injected fault" in r.stdout + r.stderr
+    assert time.time() - t0 < 100  # (well inside the 120 s exchange timeout: no rank waited it out)
+
+
 @pytest.mark.parametrize("stage", ["train", "update"])
 def test_processes_fault_stops_every_rank(cpu_lib, stage, tmp_path):
     """The same with one process per rank (gloo): the surviving rank's exchange fails or the

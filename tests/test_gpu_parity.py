@@ -327,13 +327,13 @@ def test_e2e_cli_byte_identical(eng, name, tmp_path):
         assert out.read_bytes() == f.read()
 
 
-@pytest.mark.parametrize("env", [{"MC_NW_LOOKAHEAD": "1"}, {"MC_NW_LOOKAHEAD": "3"}, {"MC_PAGEABLE_UPLOADS": "1"},
-                                 {"MC_NW_WAVES": "2"}, {"MC_NW_WAVES": "16"}],
-                         ids=["lookahead1", "lookahead3", "pageable", "nw2waves", "nw16waves"])
+@pytest.mark.parametrize("env", [{"MC_NW_LOOKAHEAD": "1"}, {"MC_NW_LOOKAHEAD": "3"}, {"MC_NW_SPINE": "0"},
+                                 {"MC_PAGEABLE_UPLOADS": "1"}, {"MC_NW_WAVES": "2"}, {"MC_NW_WAVES": "16"}],
+                         ids=["lookahead1", "lookahead3", "nospine", "pageable", "nw2waves", "nw16waves"])
 @pytest.mark.parametrize("name", ["b3k300", "fam2k_id85", "c2k_m15_al55"])
 def test_e2e_cli_variants_byte_identical(eng, name, env, tmp_path):
-    """The training search's lookahead depth (Trainer.cpp:703-721: one level per round, the
-    reference's order, or three), the upload path and the NW latency form's width (2 / 16
+    """The training search's speculation (Trainer.cpp:703-721: the left-spine round on or off,
+    one level per round -- the reference's order -- or three), the upload path and the NW latency form's width (2 / 16
     waves per pair for every small batch; c2k_m15_al55: the --align window scans) do not change
     the output."""
     fa, flags = fixtures.e2e_input(name, tmp_path)

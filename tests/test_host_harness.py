@@ -36,16 +36,20 @@ def test_e2e_byte_identical(harness, name, tmp_path):
     assert out.read_bytes() == want
 
 
-@pytest.mark.parametrize("look", ["1", "3"])
+@pytest.mark.parametrize("env", [{"MC_NW_LOOKAHEAD": "1"}, {"MC_NW_LOOKAHEAD": "3"}, {"MC_NW_SPINE": "0"},
+                                 {"MC_NW_SPINE": "0", "MC_NW_LOOKAHEAD": "1"}],
+                         ids=["look1", "look3", "nospine", "nospine_look1"])
 @pytest.mark.parametrize("name", ["a1k", "m2k_id80", "fam2k_id85"])
-def test_e2e_nw_lookahead_depth(harness, name, look, tmp_path):
-    """Trainer::split's binary search aligns MC_NW_LOOKAHEAD levels of every chain's decision
-    tree per dependent round (default 2): one level (the reference's order) and three give the
-    same pivots, so the same .clstr (Trainer.cpp:703-721)."""
+def test_e2e_nw_lookahead_depth(harness, name, env, tmp_path):
+    """Trainer::split's binary search aligns, in its first round, every chain's left spine (the
+    pivots visited while the identities stay below the cutoff; MC_NW_SPINE=0: off), then
+    MC_NW_LOOKAHEAD levels of every chain's decision tree per dependent round (default 2).  One
+    level per round without the spine is the reference's order; every form gives the same
+    pivots, so the same .clstr (Trainer.cpp:703-721)."""
     fa, flags = fixtures.e2e_input(name, tmp_path)
     out = tmp_path / (name + ".clstr")
     r = subprocess.run([harness, fa] + flags + ["--output", str(out), "--quiet"], capture_output=True, text=True,
-                       timeout=900, env=dict(os.environ, MC_NW_LOOKAHEAD=look))
+                       timeout=900, env=dict(os.environ, **env))
     assert r.returncode == 0, r.stderr[-2000:]
     with gzip.open(fixtures.golden("e2e_%s.clstr.gz" % name), "rb") as f:
         assert out.read_bytes() == f.read()
