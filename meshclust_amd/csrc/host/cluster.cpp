@@ -849,65 +849,68 @@ void write_clstr(const std::string &path, const Dataset &ds, const std::vector<C
     }
     return o + n;
   };
-#pragma omp parallel num_threads(T)
-  {
-#pragma omp for schedule(static, 1)
-    for (int t = 0; t < T; t++) {
-      // exact size first, then every line written into the buffer in place
-      const size_t c0 = C * t / T, c1 = C * (t + 1) / T;
-      size_t bytes = 0;
-      for (size_t c = c0; c < c1; c++) {
-        const auto &cen = part[c];
-        if (cen.points.empty()) continue;
-        bytes += 10 + (size_t)ndig((unsigned long long)label[c]);
-        unsigned long long pt = 0;
-        for (uint32_t p : cen.points)
-          bytes += (size_t)ndig(pt++) + 1 + (size_t)ndig(ds.lengths[p]) + 4 + ds.headers[p].size() + 4 +
-                   (p == cen.centre ? 1 : 0) + 1;
-      }
-      std::string &o = out[t];
-      o.resize(bytes);
-      char *w = &o[0];
-      for (size_t c = c0; c < c1; c++) {
-        const auto &cen = part[c];
-        if (cen.points.empty()) continue;
-        memcpy(w, ">Cluster ", 9);
-        w = put(w + 9, (unsigned long long)label[c], ndig((unsigned long long)label[c]));
+  std::vector<size_t> bytes(T, 0);
+  // exact size of every thread's part first
+#pragma omp parallel for schedule(static, 1) num_threads(T)
+  for (int t = 0; t < T; t++) {
+    const size_t c0 = C * t / T, c1 = C * (t + 1) / T;
+    size_t n = 0;
+    for (size_t c = c0; c < c1; c++) {
+      const auto &cen = part[c];
+      if (cen.points.empty()) continue;
+      n += 10 + (size_t)ndig((unsigned long long)label[c]);
+      unsigned long long pt = 0;
+      for (uint32_t p : cen.points)
+        n += (size_t)ndig(pt++) + 1 + (size_t)ndig(ds.lengths[p]) + 4 + ds.headers[p].size() + 4 +
+             (p == cen.centre ? 1 : 0) + 1;
+    }
+    bytes[t] = n;
+  }
+  for (int t = 0; t < T; t++) at[t + 1] = at[t] + bytes[t];
+  // every line written in place into its part
+  auto format = [&](int t, char *w) {
+    const size_t c0 = C * t / T, c1 = C * (t + 1) / T;
+    for (size_t c = c0; c < c1; c++) {
+      const auto &cen = part[c];
+      if (cen.points.empty()) continue;
+      memcpy(w, ">Cluster ", 9);
+      w = put(w + 9, (unsigned long long)label[c], ndig((unsigned long long)label[c]));
+      *w++ = '\n';
+      unsigned long long pt = 0;
+      for (uint32_t p : cen.points) {
+        w = put(w, pt, ndig(pt));
+        pt++;
+        *w++ = '\t';
+        w = put(w, ds.lengths[p], ndig(ds.lengths[p]));
+        memcpy(w, "nt, ", 4);
+        w += 4;
+        const auto h = ds.headers[p];
+        memcpy(w, h.data(), h.size());
+        w += h.size();
+        memcpy(w, "... ", 4);
+        w += 4;
+        if (p == cen.centre) *w++ = '*';
         *w++ = '\n';
-        unsigned long long pt = 0;
-        for (uint32_t p : cen.points) {
-          w = put(w, pt, ndig(pt));
-          pt++;
-          *w++ = '\t';
-          w = put(w, ds.lengths[p], ndig(ds.lengths[p]));
-          memcpy(w, "nt, ", 4);
-          w += 4;
-          const auto h = ds.headers[p];
-          memcpy(w, h.data(), h.size());
-          w += h.size();
-          memcpy(w, "... ", 4);
-          w += 4;
-          if (p == cen.centre) *w++ = '*';
-          *w++ = '\n';
-        }
       }
     }
-#pragma omp single
-    for (int t = 0; t < T; t++) at[t + 1] = at[t] + out[t].size();
-    // every part written at its offset by its own thread (parallel copies into the page cache)
-#pragma omp for schedule(static, 1) reduction(&& : ok)
-    for (int t = 0; t < T; t++) {
-      const char *d = out[t].data();
-      size_t off = 0;
-      while (off < out[t].size()) {
-        const ssize_t r = pwrite(fd, d + off, out[t].size() - off, (off_t)(at[t] + off));
-        if (r < 0 && errno == EINTR) continue;
-        if (r <= 0) {
-          ok = false;
-          break;
-        }
-        off += (size_t)r;
+  };
+  // every part formatted and written at its offset by its own thread (parallel copies into the
+  // page cache; measured against a shared mapping of the file, which every thread formats into
+  // straight: 1.55 vs 1.40 ms for config B's 4 MB -- the mapping's page faults cost more)
+#pragma omp parallel for schedule(static, 1) num_threads(T) reduction(&& : ok)
+  for (int t = 0; t < T; t++) {
+    out[t].resize(bytes[t]);
+    if (bytes[t]) format(t, &out[t][0]);
+    const char *d = out[t].data();
+    size_t off = 0;
+    while (off < out[t].size()) {
+      const ssize_t r = pwrite(fd, d + off, out[t].size() - off, (off_t)(at[t] + off));
+      if (r < 0 && errno == EINTR) continue;
+      if (r <= 0) {
+        ok = false;
+        break;
       }
+      off += (size_t)r;
     }
   }
   ok &= close(fd) == 0;

@@ -222,15 +222,23 @@ std::vector<PairId> Trainer::split() {
     return v < 1 ? 1 : v > 4 ? 4 : v;
   }();
   // The first round aligns each chain's whole "left spine" -- the pivots the search visits while
-  // every identity stays below the cutoff (N/2, N/4, N/8, ...) -- in one batch (MC_NW_SPINE=0: off).
+  // every identity stays below the cutoff (N/2, N/4, N/8, ...) -- in one batch (MC_NW_SPINE=0/1
+  // forces it off / on; by default on for mean read lengths up to 4 kb, below).
   // The array is sorted by k-mer distance to the pivot, so the search walks left until it nears
   // the few points within the cutoff of the pivot (its own cluster): at config B the first ~9 of
   // ~15 levels, in one round of ~2,400 pairs (the throughput form) instead of ~5 dependent rounds.
   // A chain whose identities turn above the cutoff earlier just leaves the rest of its spine
   // unused; every decision is still taken from its own alignment, so the pivots are the same.
-  const bool spine = [] {
+  // The spine pays where a round's fixed costs (a select call, the host walk, a latency-form
+  // batch that fills the chip 1.8 deep) outweigh the alignments it may waste: short reads.  At
+  // 8-12 kb (config E) every wasted pair is 10^8 cells, and E9100's search measured 257 ms with
+  // the spine against 239 ms without, so it is off above a mean length of 4 kb.
+  const bool spine = [&] {
     const char *e = getenv("MC_NW_SPINE");
-    return !e || atoi(e) != 0;
+    if (e) return atoi(e) != 0;
+    uint64_t tot = 0;
+    for (size_t t = 0; t < N; t++) tot += ds_.lengths[t];
+    return N > 0 && tot / N <= 4096;
   }();
   // one round's nodes of chain state (p, o): node n aligns position pos[n]; its children (identity
   // below the cutoff: p - o; above: p + o, both with offset o / 2) are kid[n][0] / kid[n][1], -1

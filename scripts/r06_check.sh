@@ -8,6 +8,7 @@
 #   prof1      MC_ACCUM_PROFILE=1 bench (controller phase timers)
 #   prof4      MC_ACCUM_PROFILE=4 bench (per-worker step trace)
 #   configs    scripts/configs.py $CONFIGS
+#   calib      FETCH_SIZE of the known-byte-count reads of scripts/microbench/fetch_calib
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -31,6 +32,8 @@ for s in ${STEPS:-pytest bench}; do
     prof1) MC_ACCUM_PROFILE=1 run prof1 300 python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-config-d ;;
     prof4) MC_ACCUM_PROFILE=4 run prof4 300 python bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-config-d ;;
     configs) run configs 900 python scripts/configs.py $CONFIGS ;;
+    calib) run calib 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/${TAG}_calib -o run \
+             -- ./scripts/microbench/fetch_calib ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

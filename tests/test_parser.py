@@ -127,3 +127,32 @@ def test_lf_fast_path_matches_line_path(host_built, tmp_path, seed):
                              text=True, check=True, cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         digest[mode] = res.stdout.strip()
     assert digest["fast"] == digest["lines"]
+
+
+def test_chunking_independent(host_built, tmp_path):
+    """The file is cut at record starts into threads x MC_PARSE_CHUNKS_PER_THREAD chunks, each
+    read by the thread that parses it: one chunk and 8 x 16 chunks give the same records, with
+    records that span many chunks (300 kb among 1 kb ones), CRLF and LF records, and cut points
+    that land inside headers, sequence lines and blank lines."""
+    import os
+    import subprocess
+    import sys
+    rng = np.random.default_rng(7)
+    out = []
+    for r in range(600):
+        L = int(rng.choice([25, 999, 1000, 1001, 5000, 300000], p=[0.1, 0.3, 0.3, 0.2, 0.08, 0.02]))
+        seq = rng.choice(list(b"ACGTN"), L, p=[0.24, 0.25, 0.25, 0.25, 0.01]).astype(np.uint8).tobytes()
+        nl = b"\r\n" if r % 97 == 5 else b"\n"
+        w = int(rng.choice([60, 61, 80]))
+        lines = [seq[i:i + w] for i in range(0, len(seq), w)]
+        out.append(b">rec%d %s" % (r, b"x" * int(rng.integers(0, 40))) + nl + nl.join(lines) + nl)
+    p = tmp_path / "chunks.fa"
+    p.write_bytes(b"".join(out))
+    assert p.stat().st_size > 2 << 20
+    digest = {}
+    for threads, per in (("1", "1"), ("8", "16"), ("3", "5")):
+        env = dict(os.environ, MC_PARSE_CHUNKS_PER_THREAD=per)
+        res = subprocess.run([sys.executable, "-c", _DIFF_SCRIPT, str(p), threads], env=env, capture_output=True,
+                             text=True, check=True, cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        digest[(threads, per)] = res.stdout.strip()
+    assert len(set(digest.values())) == 1, digest
