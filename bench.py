@@ -499,9 +499,11 @@ def main():
         line["extra"]["cpu_baseline_note"] = "the reference is timed on config B only (config D takes it hours)"
     if a.workload == "B" and world > 1 and not replicas:
         line["config"]["config_b_at_n_gt_1"] = (
-            "config B's accumulation is replicated by design (its 100k rows fit one GPU's LDS, so a per-step "
-            "exchange would only lengthen the dependent chain: DESIGN.md §6); the training and the mean shift "
-            "split by rank.  extra.config_d is the workload that shards by record")
+            "config B's accumulation is replicated by design whenever one GPU's LDS holds its 100k rows (a "
+            "per-step exchange would only lengthen the dependent chain: DESIGN.md §6) -- here: %s; the training "
+            "and the mean shift split by rank.  extra.config_d is the workload that shards by record"
+            % ("sharded (ranks sharing one GPU: each rank's CU share cannot hold the rows)" if acc_split
+               else "replicated"))
     if d_run is not None:
         dn, dt_, ds_, d_el, d_stats, d_tim, d_first = d_run
         d0 = d_stats[-1]
