@@ -58,6 +58,9 @@ constexpr uint32_t TRACE2_STEPS = 256;
 constexpr int T2W = 6;  // trace2 words per worker and step
 constexpr int KINL = 4;                // kill-log entries carried inline in a step record
 constexpr int REC_HDR = 14;            // centre, S, E, kn, KINL kills, mag / sumsq / len (2 each)
+// flags in the record's kill-log word (header word 3): the span is the exact window; a thin
+// record (a new seed's: no row, no magnitudes -- the dense workers load them)
+constexpr uint32_t REC_EXACT = 0x80000000u, REC_THIN = 0x40000000u, REC_KMASK = 0x3fffffffu;
 constexpr int PART_G = 8;              // granules per partial
 constexpr int INL = 3;                 // flagged positions carried inline in a partial
 constexpr uint32_t PLIST = 1024;       // flagged positions of one step listed in the controller's LDS
@@ -137,6 +140,8 @@ struct AccArgs {
   int psleep;       // s_sleep between the controller's polls of a partial (0, 1, 2, 4)
   int etake;        // a polling thread takes its worker's flagged members as soon as it has the partial
   int xfast;        // nearest-alive window also when an edge bin is empty (off: MC_ACCUM_NO_XFAST)
+  int thin;         // dense workers: a new seed's record goes out without its row (the workers
+                    // load it), before the controller has loaded the seed (MC_ACCUM_THIN=0: off)
   int rpoll;        // dense workers: waves polling the step record (MC_ACCUM_RPOLL, 1..4)
   int rpoll_gap;    // ... wave w starts w * rpoll_gap * 512 clocks late (MC_ACCUM_RPOLL_GAP)
   uint32_t rec_g;
@@ -1039,7 +1044,7 @@ __device__ __forceinline__ void worker_dense(const AccArgs &A, const DevClassifi
           state = 1;
           break;
         }
-        bool ok = true, ahead = false;
+        bool ok = true, okh = true, ahead = false;
         uint32_t xv[RPW];
 #pragma unroll
         for (int u = 0; u < RPW; u++) {
@@ -1047,8 +1052,18 @@ __device__ __forceinline__ void worker_dense(const AccArgs &A, const DevClassifi
           const uint64_t x = j < rec_words ? ld64(rn + j) : gran(want, 0);
           const uint32_t tg = (uint32_t)(x >> 32);
           ok &= tg == want;
+          if (j >= 4 * nch) okh &= tg == want;
           ahead |= (int32_t)(tg - want) > 0;
           xv[u] = (uint32_t)x;
+        }
+        // a thin record (every header granule tagged, bit 30 of its kill-log word) carries no row
+        if (__ballot(!ok) != 0 && __ballot(!okh) == 0) {
+          const int jk = 4 * nch + 3;
+          uint32_t kw = 0;
+#pragma unroll
+          for (int u = 0; u < RPW; u++)
+            if ((jk >> 6) == u) kw = (uint32_t)__builtin_amdgcn_readlane((int)xv[u], jk & 63);
+          if (kw & REC_THIN) ok = true;
         }
         if (__ballot(!ok) == 0) {
 #pragma unroll
@@ -1084,12 +1099,14 @@ __device__ __forceinline__ void worker_dense(const AccArgs &A, const DevClassifi
           break;
         }
         const uint64_t *r = A.ring + (uint64_t)(v % RING) * A.rec_g;
-        bool ok = true;
+        bool ok = true, okh = true;
         for (int j = lane; j < rec_words; j += 64) {
           const uint64_t x = ld64(r + j);
           ok &= (uint32_t)(x >> 32) == v;
+          if (j >= 4 * nch) okh &= (uint32_t)(x >> 32) == v;
           srec[j] = (uint32_t)x;
         }
+        if (__ballot(!ok) != 0 && __ballot(!okh) == 0 && (lds_u32(srec + 4 * nch + 3) & REC_THIN)) ok = true;
         if (__ballot(!ok) == 0) {
           state = 1;
           got = v;
@@ -1114,9 +1131,25 @@ __device__ __forceinline__ void worker_dense(const AccArgs &A, const DevClassifi
     if (trace && t == 0) t_seen = now();
     const uint32_t *hdr = srec + 4 * nch;
     if (hdr[0] == NONE) return;  // accumulation finished
+    if (hdr[3] & REC_THIN) {
+      // a thin record: the new seed's row and magnitudes from the static copies, by this
+      // workgroup (the controller published the record before it had loaded them itself)
+      const uint64_t cp = hdr[0];
+      uint4 rv = make_uint4(0, 0, 0, 0);
+      uint64_t mv = 0;
+      if (t < (uint32_t)nch) rv = A.hr[cp * nch + t];
+      else if (t >= 64 && t < 67) mv = t == 64 ? A.mag_s[cp] : t == 65 ? A.sumsq_s[cp] : A.len_s[cp];
+      if (t < (uint32_t)nch) reinterpret_cast<uint4 *>(srec)[t] = rv;
+      else if (t >= 64 && t < 67) {
+        srec[4 * nch + 4 + KINL + 2 * (t - 64)] = (uint32_t)mv;
+        srec[4 * nch + 5 + KINL + 2 * (t - 64)] = (uint32_t)(mv >> 32);
+      }
+      __syncthreads();
+    }
     const uint64_t P_S = hdr[1], P_E = hdr[2];
-    // bit 31 of the kill-log word: the record's span IS the exact window (no part B follows)
-    const uint32_t kend = hdr[3] & 0x7fffffffu;
+    // bit 31 of the kill-log word: the record's span IS the exact window (no part B follows);
+    // bit 30: a thin record
+    const uint32_t kend = hdr[3] & REC_KMASK;
     const bool exact = (hdr[3] >> 31) != 0;
     const PInfo pc{(uint64_t)hdr[4 + KINL] | ((uint64_t)hdr[5 + KINL] << 32),
                    (uint64_t)hdr[6 + KINL] | ((uint64_t)hdr[7 + KINL] << 32),
@@ -1812,6 +1845,7 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
   __shared__ uint32_t s_pbin[PLIST];   // ... their bvec bins (kills deferred to the next window)
   __shared__ uint64_t s_q[4];
   __shared__ uint32_t s_klast[KINL];
+  __shared__ uint32_t s_span_all;  // spec: the last record's span was every position
   __shared__ int s_abort;
   __shared__ uint64_t s_sumF;
   __shared__ double s_xv[64];  // the ranks' step headers (mailbox)
@@ -1864,6 +1898,7 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
   uint64_t err = 0;
   uint32_t kn = 0;      // kill-log length
   bool rec_exact = false;  // the record being published carries the exact window (no part B)
+  bool thin_out = false;   // this step's record went out thin (its part B is still to come)
   uint32_t npend = 0;   // new members s_plist[0, npend) whose bvec kills are still to be done
   uint64_t t_wait = 0, t_coll = 0, t_mark = 0;
   const uint64_t clk0 = prof_on ? __builtin_amdgcn_s_memtime() : 0, rt0 = prof_on ? now() : 0;
@@ -1898,11 +1933,11 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
   };
   // (thread 0's global stores come after every load of the seed: a load behind a store waits
   // for the store, see publish)
-  auto new_cluster = [&](uint64_t pos, bool kill = false) {
+  auto new_cluster = [&](uint64_t pos, bool kill = false, bool logged = false) {
     if (A.mrow && !WIDE)
       for (int c = threadIdx.x; c < nch; c += NT) mc.row[c] = A.hr[pos * nch + c];
     for (int b = threadIdx.x; b < A.B; b += NT) msum[b] = reinterpret_cast<const T *>(A.hr + pos * nch)[b];
-    if (kill) log_kill(pos);
+    if (kill && !logged) log_kill(pos);
     if (threadIdx.x == 0) {
       if (A.mrow) {
         uint2 w[MINFO_W];
@@ -1925,7 +1960,7 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
     }
     M = 1;
     last_q = 0;
-    if (kill) kn++;
+    if (kill && !logged) kn++;
     // (no drain: the seed's member-list entries are never read back in the kernel -- member 0
     // is always in the LDS cache -- and the kill log is tagged, so the stores need not have
     // landed before the next step is published)
@@ -2018,6 +2053,18 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
       if (j < rec_words) st64(r + j, gran(step, d[u]));
     }
   };
+  // a thin record (dense workers): the header of a new seed's step -- span every position, no
+  // row and no magnitudes (each worker loads them from the static copies) -- published as soon
+  // as get_close has chosen the seed, before the controller has loaded it (wave 0)
+  auto publish_thin = [&](uint32_t pos) {
+    const int h = lane;
+    const int64_t e = (int64_t)kn - KINL + (h - 4);
+    const uint32_t kx = s_klast[e >= 0 ? (uint32_t)e % KINL : 0u];
+    const uint32_t x = h == 0 ? pos : h == 1 ? 0u : h == 2 ? (uint32_t)(A.N - 1) : h == 3 ? (kn | REC_THIN)
+                     : h < 4 + KINL ? (e >= 0 ? kx : NONE) : 0u;
+    if (4 * nch + h < rec_words) st64(A.ring + (uint64_t)(step % RING) * A.rec_g + 4 * nch + h, gran(step, x));
+    if (lane == 0) st32(A.go, step);
+  };
   auto publish = [&](uint64_t S, uint64_t E, bool have) {
     for (int j0 = 0; j0 < rec_words; j0 += 64 * PW) {
       uint32_t d[PW];
@@ -2098,7 +2145,10 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
       const uint64_t rem = A.N - x * 32;
       lbits[x] = rem >= 32 ? ~0u : ((1u << rem) - 1u);
     }
-  if (threadIdx.x == 0) A.cl_off[0] = 0;
+  if (threadIdx.x == 0) {
+    A.cl_off[0] = 0;
+    s_span_all = 0;
+  }
   __syncthreads();
   {
     const uint64_t p = pop();  // MS: Point<T>* last = points.pop()
@@ -2134,23 +2184,26 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
         // position of the span.  The record then says so and no part B follows (configs B and
         // D: reads within 10 % of each other's length make every window such a span).
         rec_exact = fast_after && wt.kf == 0 && (uint64_t)wt.kble == (uint64_t)(lo[wt.bb + 1] - lo[wt.bb]);
-        step++;
         uint64_t tp0 = 0;
         if (prof_on && threadIdx.x == 0) tp0 = now();
         // The record's words are read from LDS before the other waves start the last step's
         // bvec kills: those are LDS atomics on shared Fenwick nodes, and the record's reads
         // queued behind them held every member step's record back by ≈2 µs.
         const uint64_t S0 = fast_after ? lo[wt.fb] : 0, E0 = fast_after ? lo[wt.bb + 1] - 1 : A.N - 1;
-        if (rec_words <= 64 * PW) {  // (uniform: every record of a dense or narrow-row launch)
-          uint32_t d[PW];
-          if (wv == 0) rec_read(0, S0, E0, true, d);
-          if (npend) __syncthreads();
-          if (wv == 0) {
-            rec_store(0, d);
-            if (lane == 0) st32(A.go, step);
+        if (!thin_out) {  // (a thin record is out already: its exact window follows as part B)
+          step++;
+          if (threadIdx.x == BK) s_span_all = S0 == 0 && E0 == A.N - 1;  // (read after the collect's barriers)
+          if (rec_words <= 64 * PW) {  // (uniform: every record of a dense or narrow-row launch)
+            uint32_t d[PW];
+            if (wv == 0) rec_read(0, S0, E0, true, d);
+            if (npend) __syncthreads();
+            if (wv == 0) {
+              rec_store(0, d);
+              if (lane == 0) st32(A.go, step);
+            }
+          } else if (wv == 0) {
+            publish(S0, E0, true);
           }
-        } else if (wv == 0) {
-          publish(S0, E0, true);
         }
         if (prof_on && threadIdx.x == 0) {
           const uint64_t t = now();
@@ -2184,6 +2237,8 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
         S = lo[wt.fb];
         E = lo[wt.bb + 1] - 1;
         rec_exact = false;
+        if (thin_out && wv == 0 && lane < 2) st64(A.ringb + (uint64_t)(step % RING) * 2 + lane, gran(step, (uint32_t)(lane ? E : S)));
+        thin_out = false;
         if (prof_on && threadIdx.x == 0) {
           const uint64_t t = now();
           t_ws[1] += t - t_mark;
@@ -2238,6 +2293,7 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
         t_wk[fast ? 1 : 2] += t - tk0;
         t_wk[fast ? 3 : 4]++;
       }
+      thin_out = false;
       if (count > 0) {
         have = true;
         if (A.spec && wv == 0 && lane < 2) st64(A.ringb + (uint64_t)(step % RING) * 2 + lane, gran(step, (uint32_t)(lane ? E : S)));
@@ -2836,7 +2892,16 @@ __device__ __forceinline__ void controller(const AccArgs &A, uint4 *dyn) {
       // is_min with a result: the best candidate seeds the next cluster (bvec::erase)
       finish_cluster();
       last = (uint32_t)best_pos;
-      new_cluster(best_pos, true);
+      // (thin: its record goes out now, ahead of the seed's loads -- when the last record's span
+      // was every position, so the workers score no more than they did)
+      thin_out = A.thin && s_span_all;
+      if (thin_out) {
+        log_kill(best_pos);
+        kn++;
+        step++;
+        if (wv == 0) publish_thin((uint32_t)best_pos);
+      }
+      new_cluster(best_pos, true, thin_out);
     } else {
       const uint64_t p = pop();
       finish_cluster();

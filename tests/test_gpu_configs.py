@@ -113,10 +113,11 @@ def test_config_B100k_global_bitmap_equals_reference(product):
 
 
 @pytest.mark.parametrize("env,tag", [({"MC_ACCUM_DBG": "3"}, ".dbg3"), ({"MC_CLASSIFY_EXACT": "1"}, ".exact"),
-                                     ({"MC_CLASSIFY_NO_SMALL": "1"}, ".nosmall")])
+                                     ({"MC_CLASSIFY_NO_SMALL": "1"}, ".nosmall"), ({"MC_ACCUM_THIN": "0"}, ".nothin")])
 def test_config_B100k_accum_variants_equal_reference(product, env, tag):
     """The accumulation kernel's opt-in forms (per-bin aggregated bvec kills and the
-    quad-per-member closest search, MC_ACCUM_DBG=3), the workers' exact classifier
+    quad-per-member closest search, MC_ACCUM_DBG=3; every new seed's record published whole,
+    MC_ACCUM_THIN=0), the workers' exact classifier
     (MC_CLASSIFY_EXACT: classify_std everywhere, no division-light decision) and the
     division-light decision without the small-magnitude form (MC_CLASSIFY_NO_SMALL:
     classify_fast) at config B, against the reference's partition."""
