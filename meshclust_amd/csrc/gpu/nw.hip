@@ -596,9 +596,19 @@ int launch_nw(mc_ctx *c, const uint8_t *d_A, const uint64_t *d_aoff, const uint3
     return e ? atoi(e) : 1;
   }();
   // rows per lane of a chained block: 16 (the throughput form's step, 256 registers, two waves
-  // per SIMD) or 8 (MC_NW_CHAIN_R=8: 154 registers, three waves per SIMD, but ~10% more
-  // instructions per cell and twice the blocks; E9100's sampler rounds 269 ms against 239)
-  static const int chain_r = getenv("MC_NW_CHAIN_R") && atoi(getenv("MC_NW_CHAIN_R")) == 8 ? 8 : 16;
+  // per SIMD) or 8 (154 registers, three waves per SIMD, but ~10% more instructions per cell and
+  // twice the blocks).  8 for long pairs (mean row length above 4 kb): E9100's search rounds of
+  // 150 pairs of 8-12 kb (one tree level per round, trainer.cpp) fill the chip's SIMDs ~1.5 deep
+  // at 16 and ~3 deep at 8, 210 ms against 225 (at two levels per round 8 lost, 269 against 239);
+  // 16 otherwise (1 kb pairs fit one block of 16).  MC_NW_CHAIN_R=8 / 16 forces either.
+  static const int chain_r_env = [] {
+    const char *e = getenv("MC_NW_CHAIN_R");
+    const int v = e ? atoi(e) : 0;
+    return v == 8 || v == 16 ? v : 0;
+  }();
+  uint64_t la_sum = 0;
+  for (uint64_t i = 0; i < m; i++) la_sum += alen[i];
+  const int chain_r = chain_r_env ? chain_r_env : la_sum > 4096 * m ? 8 : 16;
   std::vector<uint32_t> ch_pair;  // work items: pair, block, granule offsets in / out
   std::vector<uint16_t> ch_blk;
   std::vector<uint64_t> ch_in, ch_out;

@@ -213,12 +213,21 @@ std::vector<PairId> Trainer::split() {
   // on the device (mc_split_*, split.hip): the (key << 32 | id) arrays stay in HBM and only
   // the positions the binary search and the sampler read are resolved, with std::sort's exact
   // tie order.
+  // reads longer than 4 kb on average (config E's genomes): every alignment is ~10^8 cells
+  const bool long_reads = [&] {
+    uint64_t tot = 0;
+    for (size_t t = 0; t < N; t++) tot += ds_.lengths[t];
+    return N > 0 && tot / N > 4096;
+  }();
   // Rounds after the first align the next `look` levels of every chain's decision tree (2^look - 1
   // pairs per chain); two levels per round measured fastest at config B without the spine round
-  // (9 rounds of 450 pairs in the latency form instead of 16 of 150); MC_NW_LOOKAHEAD = 1..4.
-  const int look = [] {
+  // (9 rounds of 450 pairs in the latency form instead of 16 of 150).  With long reads a round
+  // is bound by its cells, not by its fixed costs, and the branch not taken is a third of them:
+  // one level per round (E9100's search 210 ms against 239, with nw.hip's 8-row chained blocks).
+  // MC_NW_LOOKAHEAD = 1..4 forces it.
+  const int look = [&] {
     const char *e = getenv("MC_NW_LOOKAHEAD");
-    const int v = e ? atoi(e) : 2;
+    const int v = e ? atoi(e) : long_reads ? 1 : 2;
     return v < 1 ? 1 : v > 4 ? 4 : v;
   }();
   // The first round aligns each chain's whole "left spine" -- the pivots the search visits while
@@ -236,9 +245,7 @@ std::vector<PairId> Trainer::split() {
   const bool spine = [&] {
     const char *e = getenv("MC_NW_SPINE");
     if (e) return atoi(e) != 0;
-    uint64_t tot = 0;
-    for (size_t t = 0; t < N; t++) tot += ds_.lengths[t];
-    return N > 0 && tot / N <= 4096;
+    return N > 0 && !long_reads;
   }();
   // one round's nodes of chain state (p, o): node n aligns position pos[n]; its children (identity
   // below the cutoff: p - o; above: p + o, both with offset o / 2) are kid[n][0] / kid[n][1], -1

@@ -53,13 +53,14 @@ def product():
 
 
 @pytest.mark.parametrize("env", [{}, {"MC_ACCUM_NARROW": "1"}, {"MC_ACCUM_STEPS": "1"}, {"MC_ACCUM_NO_XFAST": "1"},
-                                 {"MC_NW_SPINE": "1"}])
+                                 {"MC_NW_SPINE": "1"}, {"MC_NW_LOOKAHEAD": "2", "MC_NW_CHAIN_R": "16"}])
 def test_config_E91_partition_equals_reference(product, tmp_path, env):
     """k = 6 (4 KiB rows): the accumulation kernel's wide form (default), its lane-per-candidate
     form, the host-driven get_close steps and the controller's general window form (no
     nearest-alive queries for windows with an empty edge bin, MC_ACCUM_NO_XFAST), each against
     the reference's partition; and the sampler's left-spine round forced on (it is off by
-    default above a mean length of 4 kb)."""
+    default above a mean length of 4 kb), and its search at two levels per round in chained
+    blocks of 16 rows per lane (the short-read defaults; one level and 8 rows above 4 kb)."""
     fa = str(tmp_path / "E91.fa")
     synth.write_fasta(fa, synth.families(7, 13, 8000, 12000, 0.05, 0.15, 61))
     out = str(tmp_path / "E91.clstr")

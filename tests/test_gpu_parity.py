@@ -245,13 +245,15 @@ print("ok", len(pairs))
 """
 
 
-@pytest.mark.parametrize("env", [{"MC_NW_CHAIN": "0"}, {"MC_NW_CHAIN_R": "8"}, {"MC_NW_CHAIN": "2", "MC_NW_MW_MAX": "0"}],
-                         ids=["sequential", "chain_r8", "chain_throughput"])
+@pytest.mark.parametrize("env", [{"MC_NW_CHAIN": "0"}, {"MC_NW_CHAIN_R": "8"}, {"MC_NW_CHAIN_R": "16"},
+                                 {"MC_NW_CHAIN": "2", "MC_NW_MW_MAX": "0"}],
+                         ids=["sequential", "chain_r8", "chain_r16", "chain_throughput"])
 def test_nw_long_pairs_chain_forms_vs_oracle(built, env):
     """Long pairs (up to 12 kb: many row blocks) in every form of the row-block hand-off: the
     blocks of a pair in sequence inside one workgroup (MC_NW_CHAIN=0), chained single-wave
-    blocks of 8 rows per lane (the default chains 16), and the throughput form's pairs chained
-    too (MC_NW_CHAIN=2).  The settings are read once per process: a child process each."""
+    blocks of 8 and of 16 rows per lane (the default takes 8 for batches averaging above 4 kb),
+    and the throughput form's pairs chained too (MC_NW_CHAIN=2).  The settings are read once per
+    process: a child process each."""
     here = os.path.dirname(os.path.abspath(__file__))
     r = subprocess.run([sys.executable, "-c", _LONG_PAIRS_SCRIPT, here], capture_output=True, text=True,
                        timeout=300, env=dict(os.environ, **env))

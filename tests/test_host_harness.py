@@ -43,7 +43,8 @@ def test_e2e_byte_identical(harness, name, tmp_path):
 def test_e2e_nw_lookahead_depth(harness, name, env, tmp_path):
     """Trainer::split's binary search aligns, in its first round, every chain's left spine (the
     pivots visited while the identities stay below the cutoff; MC_NW_SPINE=0: off), then
-    MC_NW_LOOKAHEAD levels of every chain's decision tree per dependent round (default 2).  One
+    MC_NW_LOOKAHEAD levels of every chain's decision tree per dependent round (default 2; 1 for
+    reads averaging above 4 kb).  One
     level per round without the spine is the reference's order; every form gives the same
     pivots, so the same .clstr (Trainer.cpp:703-721)."""
     fa, flags = fixtures.e2e_input(name, tmp_path)
