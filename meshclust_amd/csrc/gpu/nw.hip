@@ -606,6 +606,14 @@ int launch_nw(mc_ctx *c, const uint8_t *d_A, const uint64_t *d_aoff, const uint3
     const int v = e ? atoi(e) : 0;
     return v == 8 || v == 16 ? v : 0;
   }();
+  // MC_NW_TR_R = 4 / 8: the largest rows per lane of the throughput form (default 16; E9100's
+  // label batch of ~3,000 8-12 kb pairs: 199 ms at 16, 232-240 at 8 -- three waves per SIMD
+  // instead of two do not pay for ~10 % more instructions per cell -- and 327 at 4)
+  static const int tr_rmax = [] {
+    const char *e = getenv("MC_NW_TR_R");
+    const int v = e ? atoi(e) : 16;
+    return v == 4 ? 0 : v == 8 ? 1 : 2;
+  }();
   uint64_t la_sum = 0;
   for (uint64_t i = 0; i < m; i++) la_sum += alen[i];
   const int chain_r = chain_r_env ? chain_r_env : la_sum > 4096 * m ? 8 : 16;
@@ -652,6 +660,7 @@ int launch_nw(mc_ctx *c, const uint8_t *d_A, const uint64_t *d_aoff, const uint3
       rows = w64 << r;
     } else {
       r = la <= 256 ? 0 : la <= 512 ? 1 : 2;  // R = 4, 8, 16
+      if (r > tr_rmax) r = tr_rmax;
       bk = r + (wide ? 3 : 0);
       rows = 64ull * (r == 0 ? 4 : r == 1 ? 8 : 16);
     }
