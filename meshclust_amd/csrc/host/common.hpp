@@ -3,6 +3,7 @@
 #include <chrono>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <map>
 #include <stdexcept>
 #include <string>
@@ -56,14 +57,25 @@ struct PhaseTimer {
   }
 };
 
+// MC_PHASE_LOG=1: every phase's start and end on stderr as it happens (unbuffered), so a run
+// that stops making progress shows where (the multi-rank tests' time limits print the tail)
+inline bool phase_log_on() {
+  static const bool on = getenv("MC_PHASE_LOG") && atoi(getenv("MC_PHASE_LOG")) != 0;
+  return on;
+}
+
 struct Scope {
   PhaseTimer &t;
   std::string k;
   std::chrono::steady_clock::time_point s;
-  Scope(PhaseTimer &tt, std::string kk) : t(tt), k(std::move(kk)), s(std::chrono::steady_clock::now()) {}
+  Scope(PhaseTimer &tt, std::string kk) : t(tt), k(std::move(kk)), s(std::chrono::steady_clock::now()) {
+    if (phase_log_on()) fprintf(stderr, "[phase %p] + %s\n", (void *)&tt, k.c_str());
+  }
   ~Scope() {
     auto e = std::chrono::steady_clock::now();
-    t.add(k, std::chrono::duration<double, std::milli>(e - s).count());
+    const double v = std::chrono::duration<double, std::milli>(e - s).count();
+    t.add(k, v);
+    if (phase_log_on()) fprintf(stderr, "[phase %p] - %s %.3f ms\n", (void *)&t, k.c_str(), v);
   }
 };
 

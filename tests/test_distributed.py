@@ -318,9 +318,14 @@ def _cli(binary, name, tmp_path, devices, env_extra=None, timeout=600, shard_acc
     env.pop("GPU_MAX_HW_QUEUES", None)
     if shard_accum:
         env["MC_SHARD_ACCUM"] = "1"
+    env["MC_PHASE_LOG"] = "1"  # (each rank's phases on stderr: a run past its limit shows where it stopped)
     env.update(env_extra or {})
-    r = subprocess.run([binary, fa] + flags + ["--devices", devices, "--output", out, "--stats-json", st, "--quiet",
-                        "--threads", "4"], capture_output=True, text=True, timeout=timeout, env=env)
+    try:
+        r = subprocess.run([binary, fa] + flags + ["--devices", devices, "--output", out, "--stats-json", st, "--quiet",
+                            "--threads", "4"], capture_output=True, text=True, timeout=timeout, env=env)
+    except subprocess.TimeoutExpired as e:
+        err = e.stderr.decode() if isinstance(e.stderr, bytes) else (e.stderr or "")
+        pytest.fail("--devices %s on %s still running after %d s; its phases so far:\n%s" % (devices, name, timeout, err[-4000:]))
     return r, out, st
 
 
@@ -401,7 +406,7 @@ def test_devices_cli_gpu_byte_identical(name, devices, tmp_path):
     the CUs)."""
     import meshclust_amd as M
     M.build()
-    r, out, st = _cli(M.BIN, name, tmp_path, devices)
+    r, out, st = _cli(M.BIN, name, tmp_path, devices, timeout=150)
     assert r.returncode == 0, r.stderr[-3000:]
     w = len(devices.split(","))
     assert json.load(open(st))["accum_path"] == ("device x%d" % w if w > 1 else "device")
@@ -418,7 +423,7 @@ def test_devices_cli_gpu_default_env_replicated(name, tmp_path):
     stats."""
     import meshclust_amd as M
     M.build()
-    r, out, st = _cli(M.BIN, name, tmp_path, "0,0", shard_accum=False)
+    r, out, st = _cli(M.BIN, name, tmp_path, "0,0", shard_accum=False, timeout=150)
     assert r.returncode == 0, r.stderr[-3000:]
     stats = json.load(open(st))
     assert stats["accum_path"] == "device (replicated x2)", stats["accum_path"]
