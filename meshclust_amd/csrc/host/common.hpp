@@ -64,18 +64,22 @@ inline bool phase_log_on() {
   return on;
 }
 
+inline double phase_clock_ms() {  // (steady clock, ms; the phase log's timestamps)
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 struct Scope {
   PhaseTimer &t;
   std::string k;
   std::chrono::steady_clock::time_point s;
   Scope(PhaseTimer &tt, std::string kk) : t(tt), k(std::move(kk)), s(std::chrono::steady_clock::now()) {
-    if (phase_log_on()) fprintf(stderr, "[phase %p] + %s\n", (void *)&tt, k.c_str());
+    if (phase_log_on()) fprintf(stderr, "[phase %p %.3f] + %s\n", (void *)&tt, phase_clock_ms(), k.c_str());
   }
   ~Scope() {
     auto e = std::chrono::steady_clock::now();
     const double v = std::chrono::duration<double, std::milli>(e - s).count();
     t.add(k, v);
-    if (phase_log_on()) fprintf(stderr, "[phase %p] - %s %.3f ms\n", (void *)&t, k.c_str(), v);
+    if (phase_log_on()) fprintf(stderr, "[phase %p %.3f] - %s %.3f ms\n", (void *)&t, phase_clock_ms(), k.c_str(), v);
   }
 };
 

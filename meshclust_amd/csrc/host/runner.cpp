@@ -282,7 +282,10 @@ RunResult run_pipeline(const Dataset &ds, mc_ctx *ctx, Options opt, bool upload,
   tc.threads = threads;
   tc.verbose = verbose;
   tc.comm = comm;
-  if (len_thread.joinable()) len_thread.join();
+  {
+    Scope s(rr.timer, "len_order.wait");
+    if (len_thread.joinable()) len_thread.join();
+  }
   if (len_err) std::rethrow_exception(len_err);
   tc.length_order = std::move(len_order);
   Trainer tr(ds, ctx, tc, rr.timer);
