@@ -339,6 +339,13 @@ int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, 
   A.res = pl.res;
   A.cc = pl.compact ? (uint4 *)c->s_k.p : nullptr;
   A.srows = pl.dstream ? (uint4 *)c->s_k.p : nullptr;
+  if (pl.dstream && !(getenv("MC_ACCUM_DRES") && atoi(getenv("MC_ACCUM_DRES")) == 0)) {
+    // the LDS the launch holds beyond the worker's record and two position lists (accum_plan's
+    // dfix), in whole entries of nch + 1 chunks, at most one per thread
+    const size_t dfix = (size_t)(pl.rec_g + 3) / 4 * 16 + 2 * (size_t)((fcap + 3) / 4 * 4) * 4;
+    const size_t per = (size_t)(nch + 1) * 16;
+    A.dres = pl.lds > dfix ? (uint32_t)std::min<size_t>(NT, (pl.lds - dfix) / per) : 0u;
+  }
   A.mrow = pl.mrow;
   A.mem_pos = d_mem_pos;
   A.mkeys = d_mkeys;
@@ -364,9 +371,9 @@ int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, 
     A.trace2 = atoi(getenv("MC_ACCUM_PROFILE")) >= 4 ? (uint64_t *)((char *)c->s_h.p + tb) : nullptr;
   }
   if (getenv("MC_ACCUM_PROFILE"))
-    fprintf(stderr, "[accum] variant: width %d nch %d wide %d dense %d dstream %d resident chunks/worker %d compact %d global-bitmap %d member-cache %u lds %zu G %u rank %u/%u fcap %llu\n",
+    fprintf(stderr, "[accum] variant: width %d nch %d wide %d dense %d dstream %d resident chunks/worker %d compact %d global-bitmap %d member-cache %u lds %zu G %u rank %u/%u fcap %llu dres %u\n",
             c->width, nch, (int)pl.wide, (int)pl.dense, (int)pl.dstream, pl.res, (int)pl.compact, (int)pl.gbits, pl.mrow, pl.lds, G,
-            A.rank, A.W, (unsigned long long)pl.fcap);
+            A.rank, A.W, (unsigned long long)pl.fcap, A.dres);
   DevClassifier cls = c->cls;
   void *args[] = {&A, &cls};
   timed_begin(c);

@@ -155,6 +155,8 @@ struct AccArgs {
   int res;        // chunks per worker whose rows live in its LDS (0: rows stream from memory)
   uint4 *cc;      // streaming: per-chunk compacted copies of the alive rows (null: read hs)
   uint4 *srows;   // dense streaming workers: two row buffers of fcap entries per worker
+  uint32_t dres;  // ... entries 0 .. dres-1 of a worker's list (each thread's first) also in its
+                  // LDS, which the controller's member cache sizes the launch's LDS for anyway
   uint32_t mrow;  // member cache entries (LDS)
   // output
   uint32_t *mem_pos;    // N: member static positions, cluster after cluster
@@ -199,6 +201,11 @@ __device__ __forceinline__ uint4 lds_u4(const uint4 *p) {
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 __device__ __forceinline__ void glb_st16(MC_GLB u32x4_t *p, const uint4 &v) { *p = (u32x4_t){v.x, v.y, v.z, v.w}; }
+__device__ __forceinline__ void lds_st16(MC_LDS u32x4_t *p, const uint4 &v) { *p = (u32x4_t){v.x, v.y, v.z, v.w}; }
+__device__ __forceinline__ uint4 lds_ld16(const MC_LDS u32x4_t *p) {
+  const u32x4_t v = *p;
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
 __device__ __forceinline__ WinTab lds_wt(const WinTab *p) {
   static_assert(sizeof(WinTab) == 40, "WinTab is read as five 8-byte words");
   const MC_LDS uint64_t *q = (const MC_LDS uint64_t *)p;
@@ -1504,6 +1511,11 @@ __device__ __forceinline__ void worker_dstream(const AccArgs &A, const DevClassi
   auto slot = [&](uint32_t e, int k) -> uint32_t {  // uint4 index of entry e's chunk k in a buffer
     return ((e >> 6) * CH + (uint32_t)k) * 64u + (e & 63u);
   };
+  // entries below dres (each thread's first, j = 0) are scanned from an LDS copy, chunk k of
+  // entry e at lres[k * dres + e]: as the rebuilds shrink the list, more and more of it is
+  // resident (the HBM buffers keep every row: the rebuild reads them)
+  const uint32_t dres = A.dres;
+  MC_LDS u32x4_t *lres = (MC_LDS u32x4_t *)(lpos[1] + (A.fcap + 3) / 4 * 4);
   const bool small_on = sizeof(T) == 1 && A.fc.on && A.fc.mk;
   // entry e = t + NT j: this worker's (e / DT)-th tile, offset e % DT (positions increase with
   // the entry, so the entries below N are a prefix)
@@ -1516,10 +1528,16 @@ __device__ __forceinline__ void worker_dstream(const AccArgs &A, const DevClassi
     if (p >= A.N) break;
     lpos[0][e] = (uint32_t)p;
     alive |= 1u << j;
-    for (int k = 0; k < nch; k++) glb_st16(rb[0] + slot(e, k), A.hs[(uint64_t)k * A.npad + p]);
+    for (int k = 0; k < nch; k++) {
+      const uint4 x = A.hs[(uint64_t)k * A.npad + p];
+      glb_st16(rb[0] + slot(e, k), x);
+      if (e < dres) lds_st16(lres + (uint32_t)k * dres + e, x);
+    }
     const PInfo pi{A.mag_s[p], A.sumsq_s[p], A.len_s[p]};
     const PSm ps = psmall(pi, pterms(pi.mag, pi.sumsq, A.B));
-    glb_st16(rb[0] + slot(e, nch), make_uint4(ps.mag, ps.len, ps.ok ? ps.ap : ~0u, ps.np));
+    const uint4 xi = make_uint4(ps.mag, ps.len, ps.ok ? ps.ap : ~0u, ps.np);
+    glb_st16(rb[0] + slot(e, nch), xi);
+    if (e < dres) lds_st16(lres + (uint32_t)nch * dres + e, xi);
   }
   drain();  // (the rows are read back with sc1 loads after the barrier below)
   if (t == 0) {
@@ -1682,11 +1700,18 @@ __device__ __forceinline__ void worker_dstream(const AccArgs &A, const DevClassi
         const uint32_t p = lp[e];
         if (p < W_S || p > W_E) continue;
         nscan++;
-        uint4 v[NC];
+        uint4 v[NC], inf;
+        if (e < dres) {
 #pragma unroll
-        for (int k = 0; k < NC; k++)
-          if (k < nch) v[k] = ld_sc1_16(R, slot(e, k) * 16u);
-        const uint4 inf = ld_sc1_16(R, slot(e, nch) * 16u);
+          for (int k = 0; k < NC; k++)
+            if (k < nch) v[k] = lds_ld16(lres + (uint32_t)k * dres + e);
+          inf = lds_ld16(lres + (uint32_t)nch * dres + e);
+        } else {
+#pragma unroll
+          for (int k = 0; k < NC; k++)
+            if (k < nch) v[k] = ld_sc1_16(R, slot(e, k) * 16u);
+          inf = ld_sc1_16(R, slot(e, nch) * 16u);
+        }
         const SmallK sk = lds_smallk(&s_sk);
         Acc<T> acc;
 #pragma unroll
@@ -1809,7 +1834,11 @@ __device__ __forceinline__ void worker_dstream(const AccArgs &A, const DevClassi
         }
         if (al) {
           const uint32_t e = t + NT * j;
-          for (int k = 0; k <= nch; k++) glb_st16(rb[nxt] + slot(r, k), ld_sc1_16(rr[cur], slot(e, k) * 16u));
+          for (int k = 0; k <= nch; k++) {
+            const uint4 x = ld_sc1_16(rr[cur], slot(e, k) * 16u);
+            glb_st16(rb[nxt] + slot(r, k), x);
+            if (r < dres) lds_st16(lres + (uint32_t)k * dres + r, x);  // (the rebuild reads only the HBM copies)
+          }
           lpos[nxt][r] = lp[e];
         }
         base += tot;

@@ -127,12 +127,14 @@ def test_config_B100k_accum_variants_equal_reference(product, env, tag):
 
 
 @pytest.mark.parametrize("env,tag", [({"MC_ACCUM_GRID": "64"}, ".g64"), ({"MC_ACCUM_GRID": "32"}, ".g32"),
-                                     ({"MC_ACCUM_GRID": "64", "MC_ACCUM_NO_DSTREAM": "1"}, ".g64chunks")])
+                                     ({"MC_ACCUM_GRID": "64", "MC_ACCUM_NO_DSTREAM": "1"}, ".g64chunks"),
+                                     ({"MC_ACCUM_GRID": "64", "MC_ACCUM_DRES": "0"}, ".g64nores")])
 def test_config_B100k_streaming_forms_equal_reference(product, env, tag):
     """The streaming accumulation forms config D takes on one to four GPUs, forced at config B by a
     small grid (more candidates per worker than one workgroup holds): the dense streaming workers
-    (one position-ordered list per worker, rows in HBM, rebuilt as candidates die) at 63 and 31
-    workers, and the 512-position-chunk streaming form (MC_ACCUM_NO_DSTREAM)."""
+    (one position-ordered list per worker, rows in HBM, rebuilt as candidates die; each thread's
+    first entry also in LDS) at 63 and 31 workers and with every row streamed (MC_ACCUM_DRES=0),
+    and the 512-position-chunk streaming form (MC_ACCUM_NO_DSTREAM)."""
     st = _big("B100k", product, 300, env=env, tag=tag)
     assert st["accum_path"] == "device"
 
