@@ -319,7 +319,7 @@ int launch_accum(mc_ctx *c, const uint32_t *d_bin_lo, const uint64_t *d_bounds, 
   A.ring = (uint64_t *)((char *)c->s_a.p + 256);
   A.ringb = A.ring + (size_t)RING * pl.rec_g;
   A.spec = (pl.dense || pl.dstream) && !getenv("MC_ACCUM_NO_SPEC") ? 1 : 0;
-  A.thin = A.spec && pl.dense && !(getenv("MC_ACCUM_THIN") && atoi(getenv("MC_ACCUM_THIN")) == 0) ? 1 : 0;
+  A.thin = A.spec && (pl.dense || pl.dstream) && !(getenv("MC_ACCUM_THIN") && atoi(getenv("MC_ACCUM_THIN")) == 0) ? 1 : 0;
   A.poll1 = getenv("MC_ACCUM_POLL1") ? 1 : 0;
   A.etake = getenv("MC_ACCUM_EARLY_TAKE") && atoi(getenv("MC_ACCUM_EARLY_TAKE")) ? 1 : 0;
   A.xfast = getenv("MC_ACCUM_NO_XFAST") ? 0 : 1;

@@ -140,7 +140,7 @@ struct AccArgs {
   int psleep;       // s_sleep between the controller's polls of a partial (0, 1, 2, 4)
   int etake;        // a polling thread takes its worker's flagged members as soon as it has the partial
   int xfast;        // nearest-alive window also when an edge bin is empty (off: MC_ACCUM_NO_XFAST)
-  int thin;         // dense workers: a new seed's record goes out without its row (the workers
+  int thin;         // dense (and dense streaming) workers: a new seed's record goes out without its row (the workers
                     // load it), before the controller has loaded the seed (MC_ACCUM_THIN=0: off)
   int rpoll;        // dense workers: waves polling the step record (MC_ACCUM_RPOLL, 1..4)
   int rpoll_gap;    // ... wave w starts w * rpoll_gap * 512 clocks late (MC_ACCUM_RPOLL_GAP)
@@ -970,6 +970,23 @@ __device__ __forceinline__ void worker(const AccArgs &A, const DevClassifier &C,
 constexpr int DT = 64;
 constexpr int DMAXCH = 16;  // chunks per row the dense form takes (a row per thread in registers while compacting)
 
+// A thin record (the controller's publish_thin): the new seed's row and magnitudes from the
+// static copies into the record's LDS copy, by the workgroup (the controller published the record
+// before it had loaded them itself).  Ends with a barrier.
+__device__ __forceinline__ void load_thin_record(const AccArgs &A, uint32_t *srec, int nch, uint64_t cp) {
+  const uint32_t t = threadIdx.x;
+  uint4 rv = make_uint4(0, 0, 0, 0);
+  uint64_t mv = 0;
+  if (t < (uint32_t)nch) rv = A.hr[cp * nch + t];
+  else if (t >= 64 && t < 67) mv = t == 64 ? A.mag_s[cp] : t == 65 ? A.sumsq_s[cp] : A.len_s[cp];
+  if (t < (uint32_t)nch) reinterpret_cast<uint4 *>(srec)[t] = rv;
+  else if (t >= 64 && t < 67) {
+    srec[4 * nch + 4 + KINL + 2 * (t - 64)] = (uint32_t)mv;
+    srec[4 * nch + 5 + KINL + 2 * (t - 64)] = (uint32_t)(mv >> 32);
+  }
+  __syncthreads();
+}
+
 template <typename T, int NCH, bool PROF>
 __device__ __forceinline__ void worker_dense(const AccArgs &A, const DevClassifier &C, uint4 *dyn) {
   // profiling state only in the PROF instantiation (MC_ACCUM_PROFILE): the production kernel
@@ -1138,21 +1155,7 @@ __device__ __forceinline__ void worker_dense(const AccArgs &A, const DevClassifi
     if (trace && t == 0) t_seen = now();
     const uint32_t *hdr = srec + 4 * nch;
     if (hdr[0] == NONE) return;  // accumulation finished
-    if (hdr[3] & REC_THIN) {
-      // a thin record: the new seed's row and magnitudes from the static copies, by this
-      // workgroup (the controller published the record before it had loaded them itself)
-      const uint64_t cp = hdr[0];
-      uint4 rv = make_uint4(0, 0, 0, 0);
-      uint64_t mv = 0;
-      if (t < (uint32_t)nch) rv = A.hr[cp * nch + t];
-      else if (t >= 64 && t < 67) mv = t == 64 ? A.mag_s[cp] : t == 65 ? A.sumsq_s[cp] : A.len_s[cp];
-      if (t < (uint32_t)nch) reinterpret_cast<uint4 *>(srec)[t] = rv;
-      else if (t >= 64 && t < 67) {
-        srec[4 * nch + 4 + KINL + 2 * (t - 64)] = (uint32_t)mv;
-        srec[4 * nch + 5 + KINL + 2 * (t - 64)] = (uint32_t)(mv >> 32);
-      }
-      __syncthreads();
-    }
+    if (hdr[3] & REC_THIN) load_thin_record(A, srec, nch, hdr[0]);
     const uint64_t P_S = hdr[1], P_E = hdr[2];
     // bit 31 of the kill-log word: the record's span IS the exact window (no part B follows);
     // bit 30: a thin record
@@ -1564,14 +1567,17 @@ __device__ __forceinline__ void worker_dstream(const AccArgs &A, const DevClassi
       bool late = false;
       const uint64_t *rn = A.ring + (uint64_t)(want % RING) * A.rec_g;
       for (uint32_t it = 1;; it++) {
-        bool ok = true, ahead = false;
+        bool ok = true, okh = true, ahead = false;
         for (int j = lane; j < rec_words; j += 64) {
           const uint64_t x = ld64(rn + j);
           const uint32_t tg = (uint32_t)(x >> 32);
           ok &= tg == want;
+          if (j >= 4 * nch) okh &= tg == want;
           ahead |= (int32_t)(tg - want) > 0;
           srec[j] = (uint32_t)x;
         }
+        // (a thin record: every header granule tagged, bit 30 of its kill-log word; no row)
+        if (__ballot(!ok) != 0 && __ballot(!okh) == 0 && (lds_u32(srec + 4 * nch + 3) & REC_THIN)) ok = true;
         if (__ballot(!ok) == 0) {
           state = 1;
           break;
@@ -1600,12 +1606,14 @@ __device__ __forceinline__ void worker_dstream(const AccArgs &A, const DevClassi
           break;
         }
         const uint64_t *r = A.ring + (uint64_t)(v % RING) * A.rec_g;
-        bool ok = true;
+        bool ok = true, okh = true;
         for (int j = lane; j < rec_words; j += 64) {
           const uint64_t x = ld64(r + j);
           ok &= (uint32_t)(x >> 32) == v;
+          if (j >= 4 * nch) okh &= (uint32_t)(x >> 32) == v;
           srec[j] = (uint32_t)x;
         }
+        if (__ballot(!ok) != 0 && __ballot(!okh) == 0 && (lds_u32(srec + 4 * nch + 3) & REC_THIN)) ok = true;
         if (__ballot(!ok) == 0) {
           state = 1;
           got = v;
@@ -1625,8 +1633,9 @@ __device__ __forceinline__ void worker_dstream(const AccArgs &A, const DevClassi
     seen = s_go;
     const uint32_t *hdr = srec + 4 * nch;
     if (hdr[0] == NONE) return;  // accumulation finished
+    if (hdr[3] & REC_THIN) load_thin_record(A, srec, nch, hdr[0]);
     uint64_t W_S = hdr[1], W_E = hdr[2];
-    const uint32_t kend = hdr[3] & 0x7fffffffu;
+    const uint32_t kend = hdr[3] & REC_KMASK;
     const bool exact = (hdr[3] >> 31) != 0;
     const PInfo pc{(uint64_t)hdr[4 + KINL] | ((uint64_t)hdr[5 + KINL] << 32),
                    (uint64_t)hdr[6 + KINL] | ((uint64_t)hdr[7 + KINL] << 32),

@@ -139,12 +139,15 @@ def test_config_B100k_streaming_forms_equal_reference(product, env, tag):
     assert st["accum_path"] == "device"
 
 
-@pytest.mark.parametrize("env", [{}, {"MC_ACCUM_STEPS": "1"}, {"MC_ACCUM_GRID": "64"}])
+@pytest.mark.parametrize("env", [{}, {"MC_ACCUM_STEPS": "1"}, {"MC_ACCUM_GRID": "64"},
+                                 {"MC_ACCUM_GRID": "64", "MC_ACCUM_THIN": "0"}])
 def test_config_D100k_partition_equals_reference(product, env):
     """Config D's shape (10 reads per template, 10,000 clusters) at 100k reads: the device loop
     and the host-driven steps against the reference's own partition (tests/golden/cfg_D100k.npz,
-    oracle/_ref/meshclust --threads 1, 48 min here)."""
-    st = _big("D100k", product, 300, env=env, tag=".steps" if "MC_ACCUM_STEPS" in env else ".g64" if env else "")
+    oracle/_ref/meshclust --threads 1, 48 min here); the dense streaming workers (grid 64) with
+    thin and with whole new-seed records."""
+    tag = "".join(".%s%s" % (k[9:].lower(), v) for k, v in sorted(env.items()))
+    st = _big("D100k", product, 300, env=env, tag=tag)
     assert st["accum_path"] == ("steps (MC_ACCUM_STEPS)" if "MC_ACCUM_STEPS" in env else "device")
 
 
