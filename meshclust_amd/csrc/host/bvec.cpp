@@ -4,6 +4,10 @@
 #include "bvec.hpp"
 
 #include <algorithm>
+#include <cstdlib>
+#ifdef __AVX2__
+#include <immintrin.h>
+#endif
 #include <limits>
 
 #include "common.hpp"
@@ -12,10 +16,34 @@
 namespace mc {
 
 BVec::BVec(const std::vector<uint64_t> &lengths_by_id, uint64_t bin_size) : len_(lengths_by_id) {
-  std::vector<uint64_t> lengths = lengths_by_id;
-  std::sort(lengths.begin(), lengths.end());
-  for (uint64_t i = 0; i < lengths.size(); i += bin_size) begin_bounds_.push_back(lengths[i]);
+  // the sorted lengths at ranks 0, bin_size, 2 bin_size, ...: from a histogram of the lengths
+  // when they are small (every read up to 64 Mb), else from the sort itself
+  uint64_t mx = 0;
+  for (uint64_t l : lengths_by_id) mx = l > mx ? l : mx;
+  const size_t n = lengths_by_id.size();
+  if (n && mx < (1ull << 26) && mx < 64 * (uint64_t)n + 1024) {
+    std::vector<uint32_t> cnt(mx + 1, 0);
+    for (uint64_t l : lengths_by_id) cnt[l]++;
+    uint64_t v = 0, below = 0;  // ranks [below, below + cnt[v]) hold length v
+    for (uint64_t i = 0; i < n; i += bin_size) {
+      while (below + cnt[v] <= i) below += cnt[v++];
+      begin_bounds_.push_back(v);
+    }
+  } else {
+    std::vector<uint64_t> lengths = lengths_by_id;
+    std::sort(lengths.begin(), lengths.end());
+    for (uint64_t i = 0; i < lengths.size(); i += bin_size) begin_bounds_.push_back(lengths[i]);
+  }
   data_.resize(begin_bounds_.size());
+  sizes_.assign(begin_bounds_.size(), 0);
+  if (n && begin_bounds_.size() < 0xffffffffull) {
+    uint64_t lo = ~0ull;
+    for (uint64_t l : lengths_by_id) lo = l < lo ? l : lo;
+    if (mx - lo < (1ull << 22)) {
+      memo_lo_ = lo;
+      memo_tab_.assign(mx - lo + 1, {(uint32_t)-1, (uint32_t)-1});
+    }
+  }
 }
 
 bool BVec::index_of(uint64_t point, size_t *pfront, size_t *pback) const {
@@ -94,31 +122,76 @@ bool BVec::inner_index_of(uint64_t length, size_t &idx, size_t *pfront, size_t *
 void BVec::insert(uint32_t id) {
   uint64_t len = len_[id];
   size_t front = 0, back = 0;
-  // index_of depends only on the length and the (fixed) bin bounds: memoise it
-  auto it = std::lower_bound(index_memo_.begin(), index_memo_.end(), len,
-                             [](const std::pair<uint64_t, std::pair<size_t, size_t>> &e, uint64_t v) { return e.first < v; });
-  if (it != index_memo_.end() && it->first == len) {
-    front = it->second.first;
-    back = it->second.second;
+  // index_of depends only on the length and the (fixed) bin bounds: memoise it (a table indexed
+  // by the length when the lengths span a small range -- every insert's lookup one load, not a
+  // binary search with a mispredicted branch per level -- else a sorted list)
+  if (len >= memo_lo_ && len - memo_lo_ < memo_tab_.size()) {
+    auto &e = memo_tab_[len - memo_lo_];
+    if (e.first == (uint32_t)-1) {
+      index_of(len, &front, &back);
+      e = {(uint32_t)front, (uint32_t)back};
+    }
+    front = e.first;
+    back = e.second;
   } else {
-    index_of(len, &front, &back);
-    index_memo_.insert(it, {len, {front, back}});
-  }
-  std::vector<size_t> &min_sizes = min_sizes_;
-  min_sizes.clear();
-  size_t minimum = std::numeric_limits<size_t>::max();
-  for (size_t i = front; i <= back; i++) {
-    size_t sz = data_[i].size();
-    if (sz < minimum) {
-      minimum = sz;
-      min_sizes.clear();
-      min_sizes.push_back(i);
-    } else if (sz == minimum) {
-      min_sizes.push_back(i);
+    auto it = std::lower_bound(index_memo_.begin(), index_memo_.end(), len,
+                               [](const std::pair<uint64_t, std::pair<size_t, size_t>> &e, uint64_t v) { return e.first < v; });
+    if (it != index_memo_.end() && it->first == len) {
+      front = it->second.first;
+      back = it->second.second;
+    } else {
+      index_of(len, &front, &back);
+      index_memo_.insert(it, {len, {front, back}});
     }
   }
-  if (min_sizes.empty()) throw Error("bvec: no bins to insert into", 1);
-  data_.at(min_sizes[min_sizes.size() / 2]).push_back(id);
+  // the middle one of the bins front..back with the fewest entries (min_sizes[size / 2]): the
+  // smallest size over the range, how many bins have it, then the (count / 2)-th of them -- two
+  // passes over the contiguous bin sizes (config D: every insert's range is tens of bins wide)
+  if (front > back || back >= sizes_.size()) throw Error("bvec: no bins to insert into", 1);
+  const uint32_t *sz = sizes_.data();
+  const size_t n = back - front + 1;
+  uint32_t minimum = 0xffffffffu;
+  size_t count = 0, i = 0;
+#ifdef __AVX2__
+  // eight bins per step: the minimum, then a mask of the bins at it (popcount), and the k-th
+  // of them found eight bins at a time
+  __m256i vm = _mm256_set1_epi32(-1);
+  for (; i + 8 <= n; i += 8) vm = _mm256_min_epu32(vm, _mm256_loadu_si256((const __m256i *)(sz + front + i)));
+  alignas(32) uint32_t lanes[8];
+  _mm256_store_si256((__m256i *)lanes, vm);
+  for (int l = 0; l < 8; l++) minimum = lanes[l] < minimum ? lanes[l] : minimum;
+  for (; i < n; i++) minimum = sz[front + i] < minimum ? sz[front + i] : minimum;
+  const __m256i vmin = _mm256_set1_epi32((int)minimum);
+  auto mask8 = [&](size_t j) {
+    return (uint32_t)_mm256_movemask_ps(
+        _mm256_castsi256_ps(_mm256_cmpeq_epi32(_mm256_loadu_si256((const __m256i *)(sz + front + j)), vmin)));
+  };
+  for (i = 0; i + 8 <= n; i += 8) count += (size_t)__builtin_popcount(mask8(i));
+  for (; i < n; i++) count += sz[front + i] == minimum;
+  size_t k = count / 2, bin = front;
+  for (i = 0; i + 8 <= n; i += 8) {
+    uint32_t m = mask8(i);
+    const size_t c = (size_t)__builtin_popcount(m);
+    if (k >= c) {
+      k -= c;
+      continue;
+    }
+    while (k--) m &= m - 1;
+    bin = front + i + (size_t)__builtin_ctz(m);
+    break;
+  }
+  if (i + 8 > n)
+    for (bin = front + i;; bin++)
+      if (sz[bin] == minimum && k-- == 0) break;
+#else
+  for (; i < n; i++) minimum = sz[front + i] < minimum ? sz[front + i] : minimum;
+  for (i = 0; i < n; i++) count += sz[front + i] == minimum;
+  size_t k = count / 2, bin = front;
+  for (;; bin++)
+    if (sz[bin] == minimum && k-- == 0) break;
+#endif
+  data_[bin].push_back(id);
+  sizes_[bin]++;
 }
 
 void BVec::insert_finalize(int threads) {

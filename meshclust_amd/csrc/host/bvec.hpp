@@ -60,7 +60,9 @@ class BVec {
   std::vector<uint32_t> bin_of_;  // static position -> bin (bins never change membership)
   std::vector<uint64_t> plen_;    // static position -> length
   std::vector<std::pair<uint64_t, std::pair<size_t, size_t>>> index_memo_;  // length -> index_of
-  std::vector<size_t> min_sizes_;
+  uint64_t memo_lo_ = 0;                                  // ... or by length - memo_lo_
+  std::vector<std::pair<uint32_t, uint32_t>> memo_tab_;  // (0xffffffff: not looked up yet)
+  std::vector<uint32_t> sizes_;  // entries per bin while inserting (insert's scan reads these)
 };
 
 }  // namespace mc

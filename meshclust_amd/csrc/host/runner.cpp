@@ -255,6 +255,36 @@ RunResult run_pipeline(const Dataset &ds, mc_ctx *ctx, Options opt, bool upload,
       if (t.joinable()) t.join();
     }
   } join_len{len_thread};
+  // The bvec (Runner.cpp:345-350: construct, insert every point, insert_finalize) depends only
+  // on the lengths, so a host thread builds it while the upload, K1 and the trainer run (the
+  // host mostly waits on the GPU there), with a quarter of the cores for its per-bin sorts (the
+  // trainer's teams keep the rest); its time -- the constructor included -- overlaps them.
+  std::unique_ptr<BVec> bvp;
+  double bvec_ms = 0, bvec_lap[2] = {0, 0};  // whole build; inserts, finalize
+  std::exception_ptr bvec_err;
+  std::thread bvec_thread([&]() {
+    try {
+      using clk = std::chrono::steady_clock;
+      const auto b0 = clk::now();
+      bvp.reset(new BVec(ds.lengths, 1000));
+      const auto b1 = clk::now();
+      for (uint32_t id = 0; id < ds.size(); id++) bvp->insert(id);
+      const auto b2 = clk::now();
+      bvp->insert_finalize(std::max(1, threads / 4));
+      const auto b3 = clk::now();
+      bvec_ms = std::chrono::duration<double, std::milli>(b3 - b0).count();
+      bvec_lap[0] = std::chrono::duration<double, std::milli>(b2 - b1).count();
+      bvec_lap[1] = std::chrono::duration<double, std::milli>(b3 - b2).count();
+    } catch (...) {
+      bvec_err = std::current_exception();
+    }
+  });
+  struct JoinBvec {
+    std::thread &t;
+    ~JoinBvec() {
+      if (t.joinable()) t.join();
+    }
+  } join_bvec{bvec_thread};
   fault_point(comm, "upload");
   if (upload) {
     Scope s(rr.timer, "upload");
@@ -289,30 +319,9 @@ RunResult run_pipeline(const Dataset &ds, mc_ctx *ctx, Options opt, bool upload,
   if (len_err) std::rethrow_exception(len_err);
   tc.length_order = std::move(len_order);
   Trainer tr(ds, ctx, tc, rr.timer);
-  // The bvec (Runner.cpp:345-350: construct, insert every point, insert_finalize) depends only
-  // on the lengths, so a host thread builds it while the trainer runs, with a quarter of the
-  // cores (the trainer's teams keep the rest); its time -- the constructor's length sort
-  // included -- overlaps "train".
-  std::unique_ptr<BVec> bvp;
-  double bvec_ms = 0;
-  std::exception_ptr bvec_err;
-  std::thread bvec_thread([&]() {
-    try {
-      const auto b0 = std::chrono::steady_clock::now();
-      bvp.reset(new BVec(ds.lengths, 1000));
-      for (uint32_t id = 0; id < ds.size(); id++) bvp->insert(id);
-      bvp->insert_finalize(std::max(1, threads / 4));
-      bvec_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - b0).count();
-    } catch (...) {
-      bvec_err = std::current_exception();
-    }
-  });
-  try {
+  {
     Scope s(rr.timer, "train");
     tr.train();
-  } catch (...) {
-    bvec_thread.join();
-    throw;
   }
   {
     Scope s(rr.timer, "bvec.wait");
@@ -320,6 +329,8 @@ RunResult run_pipeline(const Dataset &ds, mc_ctx *ctx, Options opt, bool upload,
   }
   fault_point(comm, "train");
   rr.timer.add("bvec.overlapped", bvec_ms);
+  rr.timer.add("bvec.overlapped.insert", bvec_lap[0]);
+  rr.timer.add("bvec.overlapped.finalize", bvec_lap[1]);
   if (bvec_err) std::rethrow_exception(bvec_err);
   mc_classifier cls = tr.classifier();
   check(mc_set_classifier(ctx, &cls), "mc_set_classifier");
