@@ -280,16 +280,6 @@ std::vector<PairId> Trainer::split() {
       level.swap(next);
     }
   };
-  auto left_spine = [&](size_t p, size_t o, Plan &pl) {  // every level, identity below the cutoff
-    pl.pos.clear();
-    pl.kid.clear();
-    for (; o > 0; o /= 2) {
-      if (!pl.pos.empty()) pl.kid.back()[0] = (int)pl.pos.size();
-      pl.pos.push_back(p);
-      pl.kid.push_back({-1, -1});
-      p -= o;
-    }
-  };
   // Several ranks: rank r runs the chains (binary searches and samples) of its block of pivots
   // [i0, i1) -- each chain needs only its own pivot's sorted array -- and the sampled pairs are
   // all-gathered at the end (one exchange; the pairs go into a header-ordered set, so the
@@ -297,6 +287,29 @@ std::vector<PairId> Trainer::split() {
   const int W = cfg_.comm && cfg_.comm->world > 1 ? cfg_.comm->world : 1;
   const size_t per = (P + (size_t)W - 1) / (size_t)W;
   const size_t i0 = std::min(P, per * (size_t)(W > 1 ? cfg_.comm->rank : 0)), i1 = std::min(P, i0 + per);
+  // The spine round aligns the first L levels of every chain, L = 2,048 / chains: the NW
+  // throughput form holds 2,048 waves at once on MI355X (256 CUs x 4 SIMDs x 2 waves of 256
+  // registers), and a batch one wave larger runs a second, mostly empty generation.  Config B's
+  // 150 chains: 13 of ~15 levels, 1,950 pairs; the search 4.9-5.9 -> 4.2 ms
+  // (profiles/r06/ab/spine_levels.txt).  The deeper levels go to the next rounds (identical
+  // pivots either way).  MC_NW_SPINE_LEVELS = L forces L.
+  const int spine_levels = [&] {
+    const char *e = getenv("MC_NW_SPINE_LEVELS");
+    const int v = e ? atoi(e) : 0;
+    if (v > 0) return v;
+    const size_t chains = i1 > i0 ? i1 - i0 : 1;
+    return (int)std::max<size_t>(1, 2048 / chains);
+  }();
+  auto left_spine = [&](size_t p, size_t o, Plan &pl) {  // every level, identity below the cutoff
+    pl.pos.clear();
+    pl.kid.clear();
+    for (int lv = 0; o > 0 && lv < spine_levels; o /= 2, lv++) {
+      if (!pl.pos.empty()) pl.kid.back()[0] = (int)pl.pos.size();
+      pl.pos.push_back(p);
+      pl.kid.push_back({-1, -1});
+      p -= o;
+    }
+  };
   const uint64_t nw_pairs0 = nw_pairs, nw_cells0 = nw_cells;
   {
     Scope s(timer_, "train.sort_keys");

@@ -37,12 +37,13 @@ def test_e2e_byte_identical(harness, name, tmp_path):
 
 
 @pytest.mark.parametrize("env", [{"MC_NW_LOOKAHEAD": "1"}, {"MC_NW_LOOKAHEAD": "3"}, {"MC_NW_SPINE": "0"},
-                                 {"MC_NW_SPINE": "0", "MC_NW_LOOKAHEAD": "1"}],
-                         ids=["look1", "look3", "nospine", "nospine_look1"])
+                                 {"MC_NW_SPINE": "0", "MC_NW_LOOKAHEAD": "1"}, {"MC_NW_SPINE_LEVELS": "3"}],
+                         ids=["look1", "look3", "nospine", "nospine_look1", "spine3"])
 @pytest.mark.parametrize("name", ["a1k", "m2k_id80", "fam2k_id85"])
 def test_e2e_nw_lookahead_depth(harness, name, env, tmp_path):
     """Trainer::split's binary search aligns, in its first round, every chain's left spine (the
-    pivots visited while the identities stay below the cutoff; MC_NW_SPINE=0: off), then
+    pivots visited while the identities stay below the cutoff, its first 2,048 / chains levels or
+    MC_NW_SPINE_LEVELS; MC_NW_SPINE=0: off), then
     MC_NW_LOOKAHEAD levels of every chain's decision tree per dependent round (default 2; 1 for
     reads averaging above 4 kb).  One
     level per round without the spine is the reference's order; every form gives the same
