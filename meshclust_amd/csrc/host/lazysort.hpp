@@ -19,6 +19,9 @@
 #include <algorithm>
 #include <cstdint>
 #include <vector>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 
 namespace mc {
 
@@ -130,6 +133,9 @@ class LazyIntroSort {
     } else {
       std::iter_swap(f, b);
     }
+#ifdef _OPENMP
+    if (n >= par_min && omp_in_parallel()) return hoare_cut_par(f, n);
+#endif
     return hoare_cut(f, n);
   }
 
@@ -187,6 +193,83 @@ class LazyIntroSort {
     }
     return std::min(li, last_r);
   }
+
+#ifdef _OPENMP
+ public:
+  // ranges of at least par_min words are partitioned by the team (hoare_cut_par); the checks
+  // lower it to exercise the parallel form on small arrays
+  static inline int64_t par_min = 32768;
+
+ private:
+  // k-th (from 1) set bit of the words m[0, nw), given the prefix popcounts c (c[w] = bits in
+  // m[0, w)): its position
+  static int64_t select_bit(const std::vector<uint64_t> &m, const std::vector<int64_t> &c, int64_t k) {
+    const int64_t w = (int64_t)(std::upper_bound(c.begin(), c.end(), k - 1) - c.begin()) - 1;
+    uint64_t bits = m[w];
+    for (int64_t r = k - c[w]; r > 1; r--) bits &= bits - 1;
+    return (w << 6) + __builtin_ctzll(bits);
+  }
+  // hoare_cut's swaps and cut with the team: the stopper masks by tasks, the k-th stoppers by
+  // prefix popcounts, K (the last k with l_k < r_k, monotone) by bisection, the K independent
+  // swaps by tasks, each walking its own run of k from its first pair
+  static int64_t hoare_cut_par(uint64_t *f, int64_t n) {
+    const uint64_t pk = f[0] >> 32;
+    const int64_t nw = (n + 63) >> 6;
+    std::vector<uint64_t> ge(nw), le(nw);
+    constexpr int64_t G = 512;  // words per task
+#pragma omp taskloop grainsize(1) shared(ge, le)
+    for (int64_t c = 0; c < (nw + G - 1) / G; c++) {
+      for (int64_t w = c * G; w < std::min(nw, (c + 1) * G); w++) {
+        const int64_t base = w << 6, cnt = std::min<int64_t>(64, n - base);
+        uint64_t g = 0, l = 0;
+        for (int64_t b = 0; b < cnt; b++) {
+          const uint64_t k = f[base + b] >> 32;
+          g |= (uint64_t)(k >= pk) << b;
+          l |= (uint64_t)(k <= pk) << b;
+        }
+        ge[w] = g;
+        le[w] = l;
+      }
+    }
+    ge[0] &= ~1ull;  // the left scan starts at f+1; the right scan may stop at the pivot, f[0]
+    std::vector<int64_t> cg(nw + 1), cl(nw + 1);
+    cg[0] = cl[0] = 0;
+    for (int64_t w = 0; w < nw; w++) {
+      cg[w + 1] = cg[w] + __builtin_popcountll(ge[w]);
+      cl[w + 1] = cl[w] + __builtin_popcountll(le[w]);
+    }
+    const int64_t CL = cg[nw], TL = cl[nw];
+    auto lk = [&](int64_t k) { return select_bit(ge, cg, k); };           // k-th left stopper
+    auto rk = [&](int64_t k) { return select_bit(le, cl, TL - k + 1); };  // k-th from the right
+    int64_t lo = 0, hi = std::min(CL, TL) + 1;  // P(lo) true, P(hi) false
+    while (hi - lo > 1) {
+      const int64_t k = lo + (hi - lo) / 2;
+      if (lk(k) < rk(k)) lo = k;
+      else hi = k;
+    }
+    const int64_t K = lo;
+    constexpr int64_t S = 4096;  // swaps per task
+#pragma omp taskloop grainsize(1) shared(ge, le, cg, cl)
+    for (int64_t t = 0; t < (K + S - 1) / S; t++) {
+      const int64_t k0 = 1 + t * S, k1 = std::min(K, k0 + S - 1);
+      int64_t li = lk(k0), ri = rk(k0);
+      for (int64_t k = k0;; k++) {
+        std::iter_swap(f + li, f + ri);
+        if (k == k1) break;
+        int64_t w = (li + 1) >> 6;  // next left stopper after li
+        uint64_t bits = ge[w] & (~0ull << ((li + 1) & 63));
+        while (!bits) bits = ge[++w];
+        li = (w << 6) + __builtin_ctzll(bits);
+        w = (ri - 1) >> 6;  // previous right stopper before ri
+        bits = le[w] & (~0ull >> (63 - ((ri - 1) & 63)));
+        while (!bits) bits = le[--w];
+        ri = (w << 6) + 63 - __builtin_clzll(bits);
+      }
+    }
+    const int64_t l_next = K < CL ? lk(K + 1) : n, r_last = K >= 1 ? rk(K) : n;
+    return std::min(l_next, r_last);
+  }
+#endif
 
   // stable insertion sort (std::__insertion_sort / __unguarded_linear_insert move only
   // strictly smaller elements)

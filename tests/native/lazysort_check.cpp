@@ -47,6 +47,17 @@ int main() {
       printf("MISMATCH sort_words case %d n=%lld kmax=%u depth=%d\n", t, (long long)n, kmax, depth);
       return 1;
     }
+    // ... with every range of 17 words or more partitioned by the team (hoare_cut_par)
+    full = a;
+    mc::LazyIntroSort::par_min = 17;
+#pragma omp parallel num_threads(4)
+#pragma omp single
+    mc::LazyIntroSort::sort_words(full.data(), n, depth, 64);
+    mc::LazyIntroSort::par_min = 32768;
+    if (full != want) {
+      printf("MISMATCH sort_words (parallel cuts) case %d n=%lld kmax=%u depth=%d\n", t, (long long)n, kmax, depth);
+      return 1;
+    }
     cases++;
   }
   printf("OK %d cases\n", cases);
