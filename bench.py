@@ -383,7 +383,9 @@ def main():
                      if workload == "B" else
                      ("priced against HBM by algorithmic bytes (SURVEY.md §8(d)); on one to four GPUs "
                       "the workers stream every window's rows from HBM (dense streaming form, DESIGN.md "
-                      "§3.1c); at eight each rank's share of the rows is LDS-resident (§6)")}
+                      "§3.1c), except each thread's first list entry, kept in the launch's spare LDS (the "
+                      "achieved figure counts those rows' bytes too: §5.0); at eight each rank's share of "
+                      "the rows is LDS-resident (§6)")}
         if device_loop and workload == "B":
             r["latency_floor"] = latency_floor(r["us_per_step"], stats)
         if workload == "B" and not shard and world == 1:  # (the counters are of the config-B launch)
