@@ -36,6 +36,7 @@ BVec::BVec(const std::vector<uint64_t> &lengths_by_id, uint64_t bin_size) : len_
   }
   data_.resize(begin_bounds_.size());
   sizes_.assign(begin_bounds_.size(), 0);
+  pend_.reserve(n);
   if (n && begin_bounds_.size() < 0xffffffffull) {
     uint64_t lo = ~0ull;
     for (uint64_t l : lengths_by_id) lo = l < lo ? l : lo;
@@ -190,11 +191,16 @@ void BVec::insert(uint32_t id) {
   for (;; bin++)
     if (sz[bin] == minimum && k-- == 0) break;
 #endif
-  data_[bin].push_back(id);
+  pend_.push_back(((uint64_t)bin << 32) | id);  // (placed into the bins by insert_finalize)
   sizes_[bin]++;
 }
 
 void BVec::insert_finalize(int threads) {
+  // the inserts' bins, in insertion order (the order a bin's ids had when pushed one by one)
+  for (size_t b = 0; b < data_.size(); b++) data_[b].reserve(data_[b].size() + sizes_[b]);
+  for (uint64_t e : pend_) data_[e >> 32].push_back((uint32_t)e);
+  pend_.clear();
+  pend_.shrink_to_fit();
   // std::sort of each bin by length (bvec.cpp's insert_finalize): the same permutation from
   // LazyIntroSort::sort_words on (length << 32 | id) words, bins and subranges as tasks
   bool wide = false;

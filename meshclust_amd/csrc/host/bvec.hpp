@@ -63,6 +63,7 @@ class BVec {
   uint64_t memo_lo_ = 0;                                  // ... or by length - memo_lo_
   std::vector<std::pair<uint32_t, uint32_t>> memo_tab_;  // (0xffffffff: not looked up yet)
   std::vector<uint32_t> sizes_;  // entries per bin while inserting (insert's scan reads these)
+  std::vector<uint64_t> pend_;   // the inserts so far, bin << 32 | id (insert_finalize places them)
 };
 
 }  // namespace mc
