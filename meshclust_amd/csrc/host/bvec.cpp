@@ -223,19 +223,28 @@ void BVec::insert_finalize(int threads) {
       }
     }
   }
-  order_.clear();
-  bin_of_.clear();
-  plen_.clear();
+  // from here on bins hold static positions (ascending): bin r's entries are the positions
+  // from its offset on (the bins in order), each bin filled by one thread
+  std::vector<uint64_t> off(data_.size() + 1, 0);
+  for (size_t r = 0; r < data_.size(); r++) off[r + 1] = off[r] + data_[r].size();
+  const uint64_t tot = off.back();
+  order_.assign(tot, 0);
+  bin_of_.assign(tot, 0);
+  plen_.assign(tot, 0);
   spos_.assign(len_.size(), std::numeric_limits<uint64_t>::max());
-  for (size_t r = 0; r < data_.size(); r++)
-    for (uint32_t &e : data_[r]) {  // from here on bins hold static positions (ascending)
+#pragma omp parallel for num_threads(threads > 0 ? threads : 1) schedule(dynamic, 16)
+  for (int64_t r = 0; r < (int64_t)data_.size(); r++) {
+    uint64_t p = off[r];
+    for (uint32_t &e : data_[r]) {
       const uint32_t id = e;
-      e = (uint32_t)order_.size();
-      spos_[id] = order_.size();
-      order_.push_back(id);
-      bin_of_.push_back((uint32_t)r);
-      plen_.push_back(len_[id]);
+      e = (uint32_t)p;
+      spos_[id] = p;  // (ids are unique: no two threads write one entry)
+      order_[p] = id;
+      bin_of_[p] = (uint32_t)r;
+      plen_[p] = len_[id];
+      p++;
     }
+  }
 }
 
 uint32_t BVec::pop() {
