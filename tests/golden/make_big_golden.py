@@ -1,4 +1,5 @@
-"""Reference partitions at the BASELINE.json sizes (config B 100k, config D 1M).
+"""Reference partitions at the BASELINE.json sizes (config B 100k, config D's shape at 100k,
+config E scaled to 9,100 genomes).
 
 Runs ONLY in the build container: the reference (oracle/_ref/meshclust, compiled from the
 read-only sources by oracle/Makefile) clusters the synthetic input that meshclust_amd.synth
@@ -42,7 +43,20 @@ BIG = {
     # config D's shape (10 reads per template, 10,000 clusters) at a size the serial
     # reference finishes in about an hour
     "D100k": ((100000, 1000, 10000, 0.03, 51), ["--id", "0.90"]),
+    # config E scaled (scripts/configs.py E9100): 70 families x 130 genomes of 8-12 kb
+    "E9100": (("families", 70, 130, 8000, 12000, 0.05, 0.15, 61), ["--id", "0.80"]),
 }
+
+
+def n_reads(gen):
+    return gen[1] * gen[2] if gen[0] == "families" else gen[0]
+
+
+def make_input(gen, path):
+    if gen[0] == "families":
+        synth.write_fasta(path, synth.families(*gen[1:]))
+    else:
+        synth.generate(path, *gen)
 
 
 def read_id(header):
@@ -106,7 +120,7 @@ def main():
     os.makedirs(a.workdir, exist_ok=True)
     fa = os.path.join(a.workdir, a.name + ".fa")
     if not os.path.exists(fa):
-        synth.generate(fa + ".tmp", *gen)
+        make_input(gen, fa + ".tmp")
         os.replace(fa + ".tmp", fa)
     out = os.path.join(a.workdir, a.name + ".clstr")
     if a.reuse is not None:
@@ -116,7 +130,7 @@ def main():
         subprocess.run([REF, fa] + flags + ["--threads", str(a.threads), "--output", out], check=True,
                        stdout=subprocess.DEVNULL)
         wall = time.time() - t0
-    s = summary(clusters_of(out), gen[0])
+    s = summary(clusters_of(out), n_reads(gen))
     np.savez_compressed(os.path.join(HERE, "cfg_%s.npz" % a.name), n=s["n"], clusters=s["clusters"],
                         centres=s["centres"], digest=s["digest"],
                         **({"centre_of": s["centre_of"]} if "centre_of" in s else {}))

@@ -74,7 +74,7 @@ def _input(name):
     gen, _ = BG.BIG[name]
     fa = os.path.join(_cache_dir(), "%s.fa" % name)
     if not os.path.exists(fa):
-        synth.generate(fa + ".tmp", *gen)
+        BG.make_input(gen, fa + ".tmp")
         os.replace(fa + ".tmp", fa)
     return fa
 
