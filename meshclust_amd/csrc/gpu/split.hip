@@ -552,8 +552,11 @@ __global__ __launch_bounds__(ST) void select_kernel(SelArgs a) {
             s_cache[idx].left = s_nn;
             s_cache[idx].cut = cut;
           }
-          s_idx = pos < cut ? s_nn : s_nn + 1;
-          s_nd = pos < cut ? lc : rc;
+          // (the child taken built from selects of its fields: a select of the two structs was
+          // materialised in scratch memory, a store and a reload per partition)
+          const bool goleft = pos < cut;
+          s_idx = goleft ? s_nn : s_nn + 1;
+          s_nd = SplitNode{goleft ? x.lo : cut, goleft ? cut : x.hi, 0, x.depth - 1, -1, 0, 0};
           s_nn += 2;
         }
       }

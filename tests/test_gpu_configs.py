@@ -217,8 +217,8 @@ def _families_input(name, *gen):
 @pytest.mark.timeout(900)
 def test_config_E9100_properties(product):
     """Config E scaled (70 families x 130 genomes, 8-12 kb, k = 6, --id 0.80: the input that
-    gives 8 GPUs work).  No reference partition exists at this size (the reference needs hours):
-    the partition must be a partition with member centres, and identical across the accumulation
+    gives 8 GPUs work): the reference's partition (tests/golden/cfg_E9100.npz, when generated),
+    a partition with member centres, and identical across the accumulation
     kernel's wide form, its lane-per-candidate form (MC_ACCUM_NARROW), the host-driven get_close
     steps, the controller's general window form (MC_ACCUM_NO_XFAST), and the NW kernels' forms (every batch in the throughput form / in the 8-wave latency
     form).  E91 pins these forms against the reference (test_config_E91_partition_equals_reference)."""
@@ -227,6 +227,12 @@ def test_config_E9100_properties(product):
     st = _run(fa, ["--id", "0.80"], base, 600)
     assert st["k"] == 6 and st["n"] == 9100 and st["accum_path"] == "device"
     want = BG.canonical_digest(_properties(base, 9100))
+    gpath = fixtures.golden("cfg_E9100.npz")
+    if os.path.exists(gpath):  # the reference's own partition (tests/golden/make_big_golden.py E9100)
+        g = np.load(gpath)
+        got = BG.clusters_of(base)
+        assert sorted(c for c, _ in got) == [int(x) for x in g["centres"]], "centre sets differ"
+        assert want == str(g["digest"])
     for tag, env in (("narrow", {"MC_ACCUM_NARROW": "1"}), ("steps", {"MC_ACCUM_STEPS": "1"}),
                      ("noxfast", {"MC_ACCUM_NO_XFAST": "1"}),
                      ("nwtp", {"MC_NW_MW_MAX": "0"}), ("nw8", {"MC_NW_MW_MAX": "100000000", "MC_NW_WAVES": "8"})):
