@@ -111,18 +111,22 @@ __global__ __launch_bounds__(NT) void distance_keys_kernel(HistView H, const uin
       const bool valid = i < m;
       const uint32_t id = valid ? ids[i] : 0;
       const uint8_t *row = H.hist + (uint64_t)id * H.pitch;
+      // (both loops over the 16 slots unrolled: a runtime-bounded loop indexed the array
+      // dynamically, which put it in scratch memory -- 272 bytes per lane, a reload per pivot)
       uint4 mine[16];
       const int per = (nch + 15) / 16;
-      for (int q = 0; q < per && q < 16; q++) {
-        int ch = lig + 16 * q;
-        mine[q] = (valid && ch < nch) ? reinterpret_cast<const uint4 *>(row)[ch] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+      for (int q = 0; q < 16; q++) {
+        const int ch = lig + 16 * q;
+        mine[q] = (q < per && valid && ch < nch) ? reinterpret_cast<const uint4 *>(row)[ch] : make_uint4(0, 0, 0, 0);
       }
       const uint64_t magi = valid ? H.mag[id] : 0;
       for (uint32_t pp = 0; pp < pn; pp++) {
         Acc<T> acc;
-        for (int q = 0; q < per && q < 16; q++) {
-          int ch = lig + 16 * q;
-          if (ch < nch) acc.add(mine[q], plds[pp * nch + ch]);
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+          const int ch = lig + 16 * q;
+          if (q < per && ch < nch) acc.add(mine[q], plds[pp * nch + ch]);
         }
         // rows wider than 256 chunks are streamed from global (k >= 7 at 1 byte)
         for (int ch = lig + 256; ch < nch; ch += 16)
